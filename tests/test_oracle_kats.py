@@ -1,0 +1,622 @@
+"""Pin the CPU oracle to ringpop-go's own swim test assertions (known-answer tests).
+
+Each test restates one reference test and cites it. The oracle is the parity checker for the
+MI355X engine, so these tests are what make the engine's parity claims mean "ringpop-go's swim".
+Fingerprint32 absolute values stay parity-unpinned (no FarmHash vectors exist in the reference
+or in this image). Checksums are pinned only by the reference's relational assertions.
+"""
+import json
+import os
+
+import pytest
+
+from oracle_ffi import (ALIVE, FAULTY, LEAVE, SUSPECT, TOMBSTONE, UNKNOWN, SOURCE_NONE, EV_HEAL, EV_KILL,
+                        OracleSim, fingerprint32, perm, perm_inv, philox)
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+STATUSES = [ALIVE, SUSPECT, FAULTY, LEAVE, TOMBSTONE]
+
+
+def states20(inc0=1000):
+    # member_test.go:50-57 — (inc, status) pairs of ever increasing precedence
+    return [(inc0 + i, st) for i in range(4) for st in STATUSES]
+
+
+# --------------------------------------------------------------------------------------------
+# member_test.go
+# --------------------------------------------------------------------------------------------
+def test_non_local_override_truth_table():
+    """member_test.go:77-98: change j overrides member i iff j > i (20x20)."""
+    from oracle_ffi import lib
+    s = states20()
+    table = [[lib().or_non_local_override(s[i][0], s[i][1], s[j][0], s[j][1]) for j in range(20)] for i in range(20)]
+    for i in range(20):
+        for j in range(20):
+            assert bool(table[i][j]) == (j > i)
+    with open(os.path.join(GOLDEN, "reference_kats.json")) as f:
+        kat = json.load(f)
+    assert table == kat["non_local_override_20x20"]
+
+
+def test_local_override_truth_table():
+    """member_test.go:100-121: override iff status in {suspect,faulty,tombstone} and inc >= local."""
+    from oracle_ffi import lib
+    s = states20()
+    table = []
+    for i in range(20):
+        row = []
+        for j in range(20):
+            got = lib().or_local_override(1, s[i][0], s[j][0], s[j][1])
+            exp = s[j][1] in (SUSPECT, FAULTY, TOMBSTONE) and s[j][0] >= s[i][0]
+            assert bool(got) == exp
+            assert lib().or_local_override(0, s[i][0], s[j][0], s[j][1]) == 0
+            row.append(got)
+        table.append(row)
+    with open(os.path.join(GOLDEN, "reference_kats.json")) as f:
+        assert table == json.load(f)["local_override_20x20"]
+
+
+# --------------------------------------------------------------------------------------------
+# memberlist_test.go — node 0 is "127.0.0.1:3001"; members 1..4 are 3002..3005
+# --------------------------------------------------------------------------------------------
+INC = 1_444_000_000_000
+
+
+def node(n=6, **kw):
+    s = OracleSim(n, t0_ms=INC, init="self", **kw)
+    return s
+
+
+def test_multiple_updates():
+    """memberlist_test.go:177-206"""
+    s = node()
+    ch = [(1, ALIVE, INC), (2, SUSPECT, INC), (3, FAULTY, INC), (4, LEAVE, INC)]
+    applied = s.update(0, ch)
+    assert len(applied) == 4
+    assert [s.member(0, m)[0] for m in (1, 2, 3, 4)] == [ALIVE, SUSPECT, FAULTY, LEAVE]
+
+
+def test_checksum_changes_and_order_independence():
+    """memberlist_test.go:101-125: same membership => equal checksum; a change => new checksum."""
+    a = node(5)
+    b = node(5)
+    for m in (0, 1, 2, 3):
+        a.make_change(0, m, INC, ALIVE)
+    for m in (3, 0, 2, 1):
+        b.make_change(0, m, INC, ALIVE)
+    assert a.checksum(0) == b.checksum(0)
+    old = a.checksum(0)
+    a.make_change(0, 4, INC, ALIVE)
+    assert a.checksum(0) != old
+
+
+def test_local_leave_override():
+    """memberlist_test.go:127-148"""
+    for delta, exp in ((1, LEAVE), (0, LEAVE), (-1, ALIVE)):
+        s = node()
+        s.make_change(0, 0, INC + delta, LEAVE)
+        assert s.member(0, 0)[0] == exp
+
+
+@pytest.mark.parametrize("status", [FAULTY, SUSPECT])
+def test_local_faulty_suspect_always_refuted(status):
+    """memberlist_test.go:150-175"""
+    s = node()
+    for delta in (-1, 0, 1):
+        s.make_change(0, 0, INC + delta, status)
+        assert s.member(0, 0)[0] == ALIVE
+
+
+def test_update_triggers_reincarnation():
+    """memberlist_test.go:208-230: refute rewrites to alive, source = self, inc = local inc."""
+    s = node()
+    applied = s.update(0, [(0, SUSPECT, INC, 5, 1337)])
+    assert len(applied) == 1
+    m, st, inc, src, sinc = applied[0]
+    assert st == ALIVE and src == 0
+    assert inc == s.member(0, 0)[1] and sinc == s.member(0, 0)[1]
+
+
+def test_alive_to_faulty():
+    """memberlist_test.go:232-246"""
+    s = node()
+    s.make_change(0, 1, INC, ALIVE)
+    s.make_change(0, 1, INC - 1, FAULTY)
+    assert s.member(0, 1)[0] == ALIVE
+    s.make_change(0, 1, INC, FAULTY)
+    assert s.member(0, 1)[0] == FAULTY
+
+
+def test_update_empty_and_tombstone():
+    """memberlist_test.go:257-290, 360-363"""
+    s = node()
+    assert s.update(0, []) == []
+    s.make_change(0, 1, INC, ALIVE)
+    s.update(0, [(1, TOMBSTONE, INC)])  # faulty + tombstone flag arrives as tombstone
+    assert s.member(0, 1)[0] == TOMBSTONE
+    assert s.make_change(0, 5, 42, TOMBSTONE) == 0  # unknown member tombstone not applied
+    assert s.member(0, 5)[0] == UNKNOWN
+
+
+def test_random_pingable():
+    """memberlist_test.go:292-306"""
+    s = node()
+    for m in (1, 2, 3):
+        s.make_change(0, m, INC, ALIVE)
+    assert len(s.random_pingable(0, 4, 2)) == 2
+    assert len(s.random_pingable(0, 1, 2)) == 1
+    got = s.random_pingable(0, 4, 2)
+    assert 2 not in got and 0 not in got and len(set(got)) == len(got)
+
+
+def test_reachable_members():
+    """memberlist_test.go:308-345"""
+    s = node()
+    s.make_change(0, 1, INC, ALIVE)
+    s.make_change(0, 2, INC, SUSPECT)
+    s.make_change(0, 3, INC, FAULTY)
+    assert s.count_reachable(0) == 3
+
+
+# --------------------------------------------------------------------------------------------
+# disseminator_test.go (node 0 = 192.0.2.1:1; 1..4 other members)
+# --------------------------------------------------------------------------------------------
+def test_changes_recorded_and_counted():
+    """disseminator_test.go:57-81: MakeAlive records a change per address (+1 for the local node)."""
+    s = OracleSim(6, t0_ms=INC, init=None)
+    s.make_change(0, 0, INC, ALIVE)  # SetupTest: MakeAlive(local)
+    for i, m in enumerate((1, 2, 3, 4)):
+        assert s.changes_count(0) == i + 1
+        s.make_change(0, m, INC, ALIVE)
+    assert s.changes_count(0) == 5
+
+
+def test_membership_as_changes():
+    """disseminator_test.go:119-129"""
+    s = node()
+    for m in (1, 2, 3):
+        s.make_change(0, m, INC, ALIVE)
+    mac = s.membership_as_changes(0)
+    assert len(mac) == 4 and all(c[3] == 0 for c in mac)
+
+
+def test_issue_as_sender_and_tombstone():
+    """disseminator_test.go:131-175"""
+    s = node()
+    s.make_change(0, 1, INC, ALIVE)
+    s.make_change(0, 2, INC, SUSPECT)
+    s.make_change(0, 3, INC, FAULTY)
+    assert len(s.issue_as_sender(0)) == 3
+    s2 = node()
+    s2.make_change(0, 1, INC, ALIVE)
+    s2.clear_changes(0)
+    s2.make_change(0, 1, INC, TOMBSTONE)
+    ch = s2.issue_as_sender(0)
+    assert len(ch) == 1 and ch[0][1] == TOMBSTONE  # travels as faulty + tombstone flag
+    r, fs = s2.issue_as_receiver(0, 4, s2.member(0, 0)[1], s2.checksum(0))
+    assert len(r) == 1 and r[0][1] == TOMBSTONE and not fs
+
+
+def test_issue_as_receiver():
+    """disseminator_test.go:177-204"""
+    s = node()
+    s.make_change(0, 1, INC, ALIVE)
+    s.make_change(0, 2, INC, SUSPECT)
+    s.make_change(0, 3, INC, FAULTY)
+    ch, fs = s.issue_as_receiver(0, 0, s.member(0, 0)[1], s.checksum(0))
+    assert len(ch) == 0 and not fs  # same sender/receiver: everything filtered
+    ch, fs = s.issue_as_receiver(0, 1, INC, s.checksum(0))
+    assert len(ch) == 3 and not fs
+    s.clear_changes(0)
+    ch, fs = s.issue_as_receiver(0, 1, INC, s.checksum(0))
+    assert len(ch) == 0 and not fs
+    ch, fs = s.issue_as_receiver(0, 1, INC, (s.checksum(0) + 1) & 0xFFFFFFFF)
+    assert len(ch) == 4 and fs  # full sync: one change per member
+
+
+def test_bump_piggyback():
+    """disseminator_test.go:206-254"""
+    s = node()
+    for m, st in ((1, ALIVE), (2, SUSPECT), (3, FAULTY)):
+        s.make_change(0, m, INC, st)
+    assert {m: v[0] for m, v in s.dis_entries(0).items()} == {1: 0, 2: 0, 3: 0}
+    sent = s.issue_as_sender(0)
+    assert {m: v[0] for m, v in s.dis_entries(0).items()} == {1: 0, 2: 0, 3: 0}
+    s.bump(0, sent)
+    assert {m: v[0] for m, v in s.dis_entries(0).items()} == {1: 1, 2: 1, 3: 1}
+    s2 = node()
+    for m, st in ((1, ALIVE), (2, SUSPECT), (3, FAULTY)):
+        s2.make_change(0, m, INC, st)
+    s2.issue_as_receiver(0, 1, INC, s2.checksum(0))
+    assert {m: v[0] for m, v in s2.dis_entries(0).items()} == {1: 1, 2: 1, 3: 1}
+
+
+@pytest.mark.parametrize("side", ["sender", "receiver"])
+def test_changes_deleted_after_maxp(side):
+    """disseminator_test.go:256-315: maxP = pFactor = 2; deleted after two propagations."""
+    s = node()
+    s.set_maxp(0, 2, 2)
+    s.make_change(0, 1, INC, ALIVE)
+    assert s.maxp(0) == 2  # 2 * ceil(log10(1 + 1))
+    assert s.dis_entries(0)[1][0] == 0
+    for expect_p in (1, None):
+        if side == "sender":
+            ch = s.issue_as_sender(0)
+            s.bump(0, ch)
+        else:
+            ch, _ = s.issue_as_receiver(0, 1, INC, s.checksum(0))
+        assert len(ch) == 1
+        if expect_p is None:
+            assert 1 not in s.dis_entries(0)
+        else:
+            assert s.dis_entries(0)[1][0] == expect_p
+    if side == "sender":
+        ch = s.issue_as_sender(0)
+    else:
+        ch, _ = s.issue_as_receiver(0, 1, INC, s.checksum(0))
+    assert ch == []
+
+
+def test_filter_changes_from_sender():
+    """disseminator_test.go:317-384: (source, sourceInc) == sender's filters a change out."""
+    def make():
+        s = node()
+        li = s.member(0, 0)[1]
+        s.update(0, [(1, ALIVE, INC, 0, li), (2, SUSPECT, INC, 1, INC), (3, FAULTY, INC, 0, li)])
+        return s, li
+
+    cases = [((1, INC), [1, 3]), ((0, None), [2]), ((1, INC - 1), [1, 2, 3]), ((2, INC), [1, 2, 3]),
+             ((3, INC), [1, 2, 3])]
+    for (sender, sinc), exp in cases:
+        s, li = make()
+        ch, _ = s.issue_as_receiver(0, sender, li if sinc is None else sinc, s.checksum(0) ^ 1)
+        assert sorted(c[0] for c in ch) == exp
+
+
+# --------------------------------------------------------------------------------------------
+# memberlist_iter_test.go
+# --------------------------------------------------------------------------------------------
+def test_iter_none_usable():
+    """memberlist_iter_test.go:51-58"""
+    s = node(3)
+    s.make_change(0, 1, INC, FAULTY)
+    s.make_change(0, 2, INC, LEAVE)
+    assert s.next(0) == -1
+
+
+def test_iter_over_five():
+    """memberlist_iter_test.go:60-79: each of 5 members visited 4x in 20 calls."""
+    s = node(6)
+    for m in range(1, 6):
+        s.make_change(0, m, INC, ALIVE)
+    counts = {}
+    for _ in range(20):
+        m = s.next(0)
+        assert m > 0
+        counts[m] = counts.get(m, 0) + 1
+    assert counts == {m: 4 for m in range(1, 6)}
+
+
+def test_iter_skips():
+    """memberlist_iter_test.go:81-103"""
+    s = node(5)
+    s.make_change(0, 1, INC, ALIVE)
+    s.make_change(0, 2, INC, FAULTY)
+    s.make_change(0, 3, INC, ALIVE)
+    s.make_change(0, 4, INC, LEAVE)
+    counts = {}
+    for _ in range(10):
+        m = s.next(0)
+        counts[m] = counts.get(m, 0) + 1
+    assert counts == {1: 5, 3: 5}
+
+
+# --------------------------------------------------------------------------------------------
+# state_transitions_test.go (Faulty timeout 10 s; the mock clock starts at 0)
+# --------------------------------------------------------------------------------------------
+def timer_node():
+    s = OracleSim(3, t0_ms=0, period_ms=1000, faulty_ms=10_000, init="self")
+    s.make_change(0, 0, INC, ALIVE)
+    return s
+
+
+def advance(s, o, ms):
+    s.set_round(s.round + ms // 1000)
+    s.fire_timers(o)
+
+
+def test_timer_schedule_twice_and_local():
+    """state_transitions_test.go:73-91"""
+    s = timer_node()
+    s.schedule(0, 1, SUSPECT, INC)
+    first = s.timer_entries(0)[1]
+    s.schedule(0, 1, SUSPECT, INC)
+    assert s.timer_entries(0)[1] == first
+    s.schedule(0, 0, SUSPECT, INC)
+    assert 0 not in s.timer_entries(0)
+
+
+def test_suspect_becomes_faulty():
+    """state_transitions_test.go:102-113: faulty after 5 s."""
+    s = timer_node()
+    s.make_change(0, 1, INC, SUSPECT)
+    advance(s, 0, 4000)
+    assert s.member(0, 1)[0] == SUSPECT
+    advance(s, 0, 1000)
+    assert s.member(0, 1)[0] == FAULTY
+
+
+def test_faulty_becomes_tombstone_then_evicted():
+    """state_transitions_test.go:115-145"""
+    s = timer_node()
+    s.make_change(0, 1, INC, FAULTY)
+    advance(s, 0, 10_000)
+    assert s.member(0, 1)[0] == TOMBSTONE
+    advance(s, 0, 60_000)
+    assert s.member(0, 1)[0] == UNKNOWN  # evicted: no longer in the memberlist
+    assert s.num_members(0) == 1
+
+
+def test_timer_canceled():
+    """state_transitions_test.go:167-185"""
+    s = timer_node()
+    s.make_change(0, 1, INC, ALIVE)
+    s.schedule(0, 1, SUSPECT, INC)
+    s.cancel(0, 1)
+    assert 1 not in s.timer_entries(0)
+    advance(s, 0, 5000)
+    assert s.member(0, 1)[0] == ALIVE
+
+
+def test_first_subject_incarnation_kept():
+    """Quirk: state_transitions.go:130-136 keeps the FIRST suspect subject; MakeFaulty fails."""
+    s = timer_node()
+    s.make_change(0, 1, INC, SUSPECT)
+    s.make_change(0, 1, INC + 5, SUSPECT)  # applied (newer inc) but the timer is not rescheduled
+    assert s.timer_entries(0)[1][3] == INC
+    advance(s, 0, 5000)
+    assert s.member(0, 1) == (SUSPECT, INC + 5)
+
+
+# --------------------------------------------------------------------------------------------
+# node_bootstrap_test.go:186-201 — maxP for 11 nodes
+# --------------------------------------------------------------------------------------------
+def test_maxp_eleven_nodes():
+    s = OracleSim(11)
+    assert s.maxp(0) == 30
+    fresh = OracleSim(11, init="self")
+    assert fresh.maxp(0) == 15  # initial maxP == pFactor
+
+
+def test_maxp_formula_matches_float_log():
+    import math
+    from oracle_ffi import lib  # noqa: F401
+    for n in list(range(0, 2000)) + [9999, 10000, 10001, 99999, 100000, 100001, 999999, 1000000]:
+        exact = len(str(n)) if n > 0 else 0
+        assert int(math.ceil(math.log(n + 1) / math.log(10))) == exact
+
+
+# --------------------------------------------------------------------------------------------
+# multi-node scenarios: gossip_test.go, heal_partition_test.go, disseminator_test.go full sync
+# --------------------------------------------------------------------------------------------
+def run_until(s, pred, max_rounds=400, events=()):
+    for _ in range(max_rounds):
+        r = s.round
+        s.step([e for e in events if e[0] == r])
+        if pred():
+            return s.round
+    raise AssertionError("did not converge")
+
+
+def test_updates_are_propagated():
+    """gossip_test.go:78-108: one protocol period carries the peer's four changes."""
+    # members: 0 node, 1 peer, 2..5 fake addresses (not running)
+    s = OracleSim(6, init="self")
+    for o in (0, 1):
+        for m in (0, 1):
+            s.set_member(o, m, ALIVE, s.t0_ms)
+    for m in (2, 3, 4, 5):
+        s.set_live(m, False)
+    s.make_change(1, 2, s.t0_ms, ALIVE)
+    s.make_change(1, 3, s.t0_ms, FAULTY)
+    s.make_change(1, 4, s.t0_ms, SUSPECT)
+    s.make_change(1, 5, s.t0_ms, LEAVE)
+    assert s.changes_count(1) == 4
+    s.step()
+    assert [s.member(0, m)[0] for m in (2, 3, 4, 5)] == [ALIVE, FAULTY, SUSPECT, LEAVE]
+
+
+def test_suspicion_started():
+    """gossip_test.go:110-122: pinging an unreachable member starts its suspect timer."""
+    s = OracleSim(5)
+    s.set_live(4, False)
+    for _ in range(8):
+        s.step()
+    assert any(4 in s.timer_entries(o) for o in range(4))
+
+
+def test_bidirectional_full_sync():
+    """disseminator_test.go:399-447: a knows b, b doesn't know a; a pings b → b reverse-syncs."""
+    s = OracleSim(2, init="self")
+    s.set_member(0, 1, ALIVE, s.t0_ms)
+    s.step()
+    assert s.member(1, 0)[0] == ALIVE
+    assert s.counters()["full_syncs"] == 1 and s.counters()["rfs_done"] == 1
+
+
+def partitioned_sim(nA, nB, status_ab=None, status_ba=None, offA=3, offB=5):
+    """heal_partition_test.go:413-454: two bootstrapped partitions with per-partition mock clocks."""
+    n = nA + nB
+    s = OracleSim(n, t0_ms=0, period_ms=0, init="self")
+    A, B = list(range(nA)), list(range(nA, n))
+    for P in (A, B):
+        for o in P:
+            for m in P:
+                s.set_member(o, m, ALIVE, 0)
+    if status_ab is not None:  # A.AddPartitionWithStatus(B, status)
+        for o in A:
+            for m in B:
+                s.make_change(o, m, 0, status_ab)
+            s.clear_changes(o)
+    if status_ba is not None:
+        for o in B:
+            for m in A:
+                s.make_change(o, m, 0, status_ba)
+            s.clear_changes(o)
+    for o in A:
+        s.set_clock_offset(o, offA)
+    for o in B:
+        s.set_clock_offset(o, offB)
+    return s, A, B
+
+
+def has_partition_as(s, X, Y, inc, status):
+    return all(s.member(x, y) == (status, inc) for x in X for y in Y)
+
+
+def heal_and_settle(s, o, settle=80):
+    targets = s.heal(o)
+    for _ in range(settle):
+        s.step()
+        if all(s.changes_count(q) == 0 for q in range(s.n)):
+            break
+    return targets
+
+
+def test_partition_heal_with_faulties():
+    """heal_partition_test.go:36-77: two heals; A@3 / B@5 alive everywhere at the end."""
+    s, A, B = partitioned_sim(5, 5, FAULTY, FAULTY)
+    targets = heal_and_settle(s, A[0])
+    assert len(targets) == 1 and targets[0] in B
+    assert has_partition_as(s, A, A, 3, ALIVE) and has_partition_as(s, A, B, 0, FAULTY)
+    assert has_partition_as(s, B, B, 5, ALIVE) and has_partition_as(s, B, A, 0, FAULTY)
+    targets = heal_and_settle(s, A[0])
+    assert len(targets) == 1 and targets[0] in B
+    run_until(s, lambda: s.converged() and all(s.count_reachable(o) == s.n for o in range(s.n)))
+    assert has_partition_as(s, A, A, 3, ALIVE) and has_partition_as(s, A, B, 5, ALIVE)
+    assert has_partition_as(s, B, B, 5, ALIVE) and has_partition_as(s, B, A, 3, ALIVE)
+
+
+def test_partition_heal_with_missing():
+    """heal_partition_test.go:79-100: one heal merges two mutually unknown partitions."""
+    s, A, B = partitioned_sim(5, 5)
+    targets = s.heal(A[0])
+    assert len(targets) == 1 and targets[0] in B
+    run_until(s, lambda: s.converged() and all(s.count_reachable(o) == s.n for o in range(s.n)))
+    for X in (A, B):
+        for Y in (A, B):
+            assert has_partition_as(s, X, Y, 0, ALIVE)
+
+
+@pytest.mark.parametrize("which", [1, 2])
+def test_partition_heal_with_faulty_and_missing(which):
+    """heal_partition_test.go:102-164: two heals needed."""
+    if which == 1:
+        s, A, B = partitioned_sim(5, 5, FAULTY, None)
+    else:
+        s, A, B = partitioned_sim(5, 5, None, FAULTY)
+    t1 = heal_and_settle(s, A[0])
+    assert len(t1) == 1 and t1[0] in B
+    t2 = heal_and_settle(s, A[0])
+    assert len(t2) == 1 and t2[0] in B
+    run_until(s, lambda: s.converged() and all(s.count_reachable(o) == s.n for o in range(s.n)))
+
+
+def test_partition_heal_semi_partition():
+    """heal_partition_test.go:202-215: A knows B alive, B doesn't know A → full syncs heal it."""
+    s, A, B = partitioned_sim(5, 5, ALIVE, None)
+    run_until(s, lambda: s.converged() and all(s.count_reachable(o) == s.n for o in range(s.n)))
+
+
+def test_partition_heal_multiple_partitions():
+    """heal_partition_test.go:217-263: 5 targets on the first heal, 4 on the second."""
+    sizes = [5, 1, 1, 1, 2, 2]
+    n = sum(sizes)
+    s = OracleSim(n, t0_ms=0, period_ms=0, init="self")
+    parts, base = [], 0
+    for k in sizes:
+        parts.append(list(range(base, base + k)))
+        base += k
+    for P in parts:
+        for o in P:
+            for m in P:
+                s.set_member(o, m, ALIVE, 0)
+    A, Bs = parts[0], parts[1:]
+    for Bp in Bs[:4]:
+        for o in A:
+            for m in Bp:
+                s.make_change(o, m, 0, FAULTY)
+    for o in A:
+        s.clear_changes(o)
+        s.set_clock_offset(o, 3)
+    for Bp in Bs:
+        for o in Bp:
+            s.set_clock_offset(o, 5)
+    t1 = heal_and_settle(s, A[0])
+    assert len(t1) == 5
+    t2 = heal_and_settle(s, A[0])
+    assert len(t2) == 4
+    run_until(s, lambda: s.converged() and all(s.count_reachable(o) == s.n for o in range(s.n)))
+
+
+def test_partition_heal_max_failures():
+    """heal_partition_test.go:374-392: 20 unreachable hosts → heal stops after 10 failures."""
+    s = OracleSim(22, init="self")
+    for o in (0, 1):
+        for m in (0, 1):
+            s.set_member(o, m, ALIVE, s.t0_ms)
+    for m in range(2, 22):
+        s.set_live(m, False)
+    assert s.heal(0) == []
+    assert s.counters()["heal_attempts"] == 10 and s.counters()["heal_failures"] == 10
+
+
+def test_reap_faulty_members():
+    """handlers_test.go:246-263: reap turns faulty into tombstone cluster-wide."""
+    from oracle_ffi import EV_REAP
+    s = OracleSim(5)
+    s.set_live(4, False)
+    s.make_change(0, 4, s.t0_ms, FAULTY)
+    run_until(s, lambda: s.converged() and all(s.member(o, 4)[0] == FAULTY for o in range(4)))
+    r = s.round
+    run_until(s, lambda: s.converged() and all(s.member(o, 4)[0] == TOMBSTONE for o in range(4)),
+              events=[(r, EV_REAP, 1, 0)])
+
+
+# --------------------------------------------------------------------------------------------
+# arithmetic building blocks
+# --------------------------------------------------------------------------------------------
+def test_philox_random123_kat():
+    """Random123 kat_vectors for philox4x32-10."""
+    assert philox([0, 0, 0, 0], [0, 0]) == [0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8]
+    assert philox([0xffffffff] * 4, [0xffffffff] * 2) == [0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd]
+    assert philox([0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344], [0xa4093822, 0x299f31d0]) == \
+        [0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1]
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 16, 17, 100, 4096, 5000])
+def test_permutation_is_bijective(n):
+    for o, ep in ((0, 0), (3, 7)):
+        img = [perm(1, o, ep, n, i) for i in range(n)]
+        assert sorted(img) == list(range(n))
+        assert all(perm_inv(1, o, ep, n, img[i]) == i for i in range(n))
+
+
+def test_fingerprint32_paths_are_total():
+    # every length dispatch (0-4, 5-12, 13-24, >24) is exercised and deterministic (parity unpinned)
+    vals = [fingerprint32(bytes(range(k))) for k in range(0, 64)]
+    assert len(set(vals)) == len(vals)
+
+
+def test_checksum_faithful_equals_static_order():
+    """memberlist.go:106-128: sort-based string == index-order string for fixed-width addresses."""
+    a = OracleSim(64, faithful_checksum=True)
+    b = OracleSim(64, faithful_checksum=False)
+    ev = [(0, EV_KILL, 7, 0), (0, EV_KILL, 33, 0)]
+    for r in range(40):
+        a.step([e for e in ev if e[0] == r])
+        b.step([e for e in ev if e[0] == r])
+        assert (a.checksums() == b.checksums()).all()
+    assert a.checksum_string(0) == b.checksum_string(0)
+    s = b.checksum_string(0).decode()
+    assert s.startswith("10.000.000.000:7000alive1500000000000;")
