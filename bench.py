@@ -1,0 +1,162 @@
+"""bench.py — member-rounds/sec of the MI355X SWIM engine on BASELINE.json's 65,536-member config.
+
+Workload (BASELINE.json configs[2], the metric's "64k members"): 65,536 members, converged start,
+1 % (655) killed at round 10, then the suspect wave and the faulty wave ~25 rounds later.
+One "step" is one synchronous protocol round of every member (docs/ROUND_SEMANTICS.md §4).
+--warmup W rounds (default 10: rounds 0-9, steady state) run untimed. --steps K rounds (default
+90: rounds 10-99, the kill and both cascades) are timed between barrier+synchronize brackets.
+value = members x K x world_size / max-over-ranks time. With --gpus N>1 each rank simulates its own
+independent 65,536-member cluster (weak scaling, no data-path collective). Observer-row
+sharding of one cluster over several GPUs is future work.
+
+The JSON line carries:
+  roofline     : for the kernel family with the most device time, its algorithmic bytes per launch /
+                 HIP-event-measured average launch time vs the 8 TB/s HBM peak.
+  cpu_baseline : the C oracle (single thread) on a bounded sample of the same protocol, rank 0 only.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "ringpop-go_amd"))
+
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def dist_env():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return ws, rank, local
+
+
+def cpu_baseline(seconds_budget=25.0):
+    """Oracle (tests/oracle_ffi.py, CPU restatement) on a bounded sample of the config-3 protocol."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from oracle_ffi import OracleSim
+    from swimsim import workloads as W
+
+    n, rounds = 4096, 40
+    wl = W.config3(n=n, rounds=rounds)
+    sim = OracleSim(n)
+    t0 = time.perf_counter()
+    done = 0
+    for r in range(rounds):
+        sim.step(wl.events_for(r))
+        done += 1
+        if time.perf_counter() - t0 > seconds_budget:
+            break
+    dt = time.perf_counter() - t0
+    return {
+        "value": round(n * done / dt, 1),
+        "unit": "member-rounds/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"C oracle (oracle/swim_oracle.c, -O2, 1 thread) on the config-3 protocol at N={n} "
+                  f"(1% killed at r=10), rounds 0-{done - 1}, {dt:.1f} s; per-member-round cost grows ~linearly in N",
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=90)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--members", type=int, default=65536)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    ws, rank, local = dist_env()
+    import torch
+
+    if ws > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
+    dev = local if torch.cuda.is_available() else 0
+    if torch.cuda.is_available():
+        torch.cuda.set_device(dev)
+
+    import swimsim
+    from swimsim import workloads as W
+
+    n = args.members
+    total_rounds = args.warmup + args.steps
+    wl = W.config3(n=n, rounds=total_rounds)
+    eng = swimsim.Cluster(n, device=dev)
+
+    def barrier():
+        if ws > 1:
+            import torch.distributed as dist
+
+            dist.barrier()
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+
+    for r in range(args.warmup):
+        eng.step(1, wl.events_for(r))
+    eng.enable_timing(True)
+    barrier()
+    t0 = time.perf_counter()
+    ev = [e for e in wl.events if args.warmup <= e[0] < total_rounds]
+    eng.step(args.steps, ev)
+    barrier()
+    dt = time.perf_counter() - t0
+    if ws > 1:
+        import torch.distributed as dist
+
+        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{dev}" if torch.cuda.is_available() else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    kt = eng.kernel_times()
+    counters = eng.counters()
+    eng.enable_timing(False)
+    dominant = max(kt.items(), key=lambda kv: kv[1]["avg_ms"] * kv[1]["launches"])
+    # the roofline is reported for the dominant family when it moves algorithmic bytes; the
+    # merge family (recv_merge) is the north-star kernel and is reported alongside in DESIGN.md
+    fam, info = dominant
+    per_launch_bytes = info["alg_bytes"] / max(1, info["launches"])
+    achieved = per_launch_bytes / (info["avg_ms"] * 1e-3) / 1e9 if info["avg_ms"] > 0 else 0.0
+    merge = kt.get("recv_merge", {})
+    merge_gbps = (merge.get("alg_bytes", 0) / max(1, merge.get("launches", 1))) / (merge.get("avg_ms", 1) * 1e-3) / 1e9 \
+        if merge.get("avg_ms", 0) > 0 else 0.0
+
+    if rank == 0:
+        value = n * args.steps * ws / dt
+        line = {
+            "metric": "simulated member-rounds/sec at 64k members",
+            "value": round(value, 1),
+            "unit": "member-rounds/s",
+            "n_gpus": ws,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt * 1e3 / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (converged 65,536-member cluster; 655 members killed at round 10; Philox seed 11)",
+            "config": {"workload": "config3_cascade: 65536 members, 1% killed at r=10, rounds 10-99 timed",
+                       "members": n, "rounds_timed": args.steps, "parallelism": f"replicas x{ws}" if ws > 1 else "1 GPU"},
+            "roofline": {"bound": "hbm", "kernel": fam, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": None,
+                         "avg_launch_ms": round(info["avg_ms"], 5), "launches": info["launches"],
+                         "merge_kernel_GBps": round(merge_gbps, 2)},
+            "kernel_ms": {k: round(v["avg_ms"] * v["launches"], 3) for k, v in kt.items()},
+            "counters": counters,
+        }
+        if not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline()
+        print(json.dumps(line))
+    if ws > 1:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

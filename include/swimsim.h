@@ -1,0 +1,156 @@
+/*
+ * swimsim.h — C ABI of libswimsim.so, the MI355X-native SWIM protocol-round engine.
+ *
+ * This is the drop-in boundary for ringpop-go's swim hot path. The reference has no FFI: its
+ * path sits behind the Go interface swim.NodeInterface (swim/node.go:137-147) and the internal
+ * Memberlist / Disseminator / stateTransitions types. Each entry point below says which
+ * reference call it replaces. INTEGRATION.md shows the cgo binding a maintainer would add.
+ *
+ * Conventions
+ *  - One handle = one simulated cluster of N members. Observer o is member o's swim.Node.
+ *  - Incarnations cross the ABI as int64 milliseconds, like swim.Member.Incarnation
+ *    (member.go:52). Inside they are kept as e = (inc - t0_ms) / protocol_period_ms.
+ *  - Status codes equal statePrecedence (member.go:112-128): alive 0, suspect 1, faulty 2,
+ *    leave 3, tombstone 4. SWIMSIM_UNKNOWN (7) means "not in this node's memberlist".
+ *  - Return values: 0 = OK, negative = SWIMSIM_E*. swimsim_last_error() gives the message.
+ *    HIP errors are mapped, never aborted on.
+ *  - Calls on one handle must be serialized. swimsim_step() blocks and is deterministic.
+ *  - The caller owns every output buffer (caller allocates, library fills). No device pointer
+ *    escapes.
+ */
+#ifndef SWIMSIM_H
+#define SWIMSIM_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SWIMSIM_ABI_VERSION 1
+
+enum {
+    SWIMSIM_OK = 0,
+    SWIMSIM_EINVAL = -1,     /* bad argument */
+    SWIMSIM_ENOMEM = -2,     /* device allocation failed */
+    SWIMSIM_EHIP = -3,       /* HIP runtime error */
+    SWIMSIM_ECAPACITY = -4,  /* a device pool overflowed (message / dense-snapshot pool) */
+    SWIMSIM_ERANGE = -5      /* incarnation not representable as t0 + e*period */
+};
+
+enum { SWIMSIM_ALIVE = 0, SWIMSIM_SUSPECT = 1, SWIMSIM_FAULTY = 2, SWIMSIM_LEAVE = 3, SWIMSIM_TOMBSTONE = 4,
+       SWIMSIM_UNKNOWN = 7 };
+#define SWIMSIM_SOURCE_NONE (-1)
+
+/* Mirrors swim.Options (swim/node.go:45-100) plus the simulation inputs. A zero field means
+ * the reference default (util.SelectInt / SelectDuration semantics, util/util.go:220-245). */
+typedef struct swimsim_config {
+    uint32_t num_members;              /* N */
+    uint32_t device;                   /* HIP device ordinal */
+    int64_t t0_ms;                     /* clock at round 0 = initial incarnation (default 1.5e12) */
+    uint32_t protocol_period_ms;       /* MinProtocolPeriod, default 200 (node.go:80) */
+    uint32_t suspect_timeout_ms;       /* StateTimeouts.Suspect, default 5 s (node.go:75) */
+    uint32_t faulty_timeout_ms;        /* StateTimeouts.Faulty, default 24 h (node.go:76) */
+    uint32_t tombstone_timeout_ms;     /* StateTimeouts.Tombstone, default 1 min (node.go:77) */
+    uint32_t ping_request_size;        /* PingRequestSize, default 3 (node.go:86) */
+    uint32_t max_reverse_full_sync_jobs; /* MaxReverseFullSyncJobs, default 5 (node.go:96) */
+    uint32_t p_factor;                 /* disseminator pFactor, default 15 (disseminator.go:35) */
+    uint64_t seed;                     /* Philox key (docs/ROUND_SEMANTICS.md §6) */
+    const char *addresses;             /* NULL: synthetic "10.%03u.%03u.%03u:7000"; else N fixed-width,
+                                          strictly ascending addresses, each addr_stride bytes */
+    uint32_t addr_stride;
+    uint32_t max_rounds;               /* incarnation table capacity (default 65536 rounds) */
+    uint64_t message_pool_bytes;       /* change-record pool; 0 = automatic */
+    uint32_t observer_begin, observer_end; /* shard of observer rows held by this handle; 0,0 = all */
+} swimsim_config;
+
+/* Events applied in phase E of a round (docs/ROUND_SEMANTICS.md §4). */
+enum {
+    SWIMSIM_EV_KILL = 1,        /* process stops (unreachable, frozen) */
+    SWIMSIM_EV_REVIVE = 2,      /* process back + Reincarnate (handlers.go:140-143) */
+    SWIMSIM_EV_REINCARNATE = 3, /* memberlist.Reincarnate (memberlist.go:234-236) */
+    SWIMSIM_EV_LEAVE = 4,       /* adminLeaveHandler (handlers.go:145-148) */
+    SWIMSIM_EV_PARTITION = 5,   /* set partition label of member a to b */
+    SWIMSIM_EV_HEAL = 6,        /* discoverProviderHealer.Heal on observer a (heal_via_discover_provider.go:120) */
+    SWIMSIM_EV_REAP = 7         /* reapFaultyMembersHandler on observer a (handlers.go:154-163) */
+};
+typedef struct swimsim_event { uint32_t round; uint32_t kind; int32_t a; int32_t b; } swimsim_event;
+
+enum {
+    SWIMSIM_C_ROUNDS, SWIMSIM_C_PINGS, SWIMSIM_C_PINGS_OK, SWIMSIM_C_PINGREQS, SWIMSIM_C_HELPER_CALLS,
+    SWIMSIM_C_HELPER_ERRORS, SWIMSIM_C_INCONCLUSIVE, SWIMSIM_C_SUSPECT_DECL, SWIMSIM_C_APPLIED,
+    SWIMSIM_C_REFUTES, SWIMSIM_C_FULL_SYNCS, SWIMSIM_C_FULL_SYNCS_PINGREQ, SWIMSIM_C_RFS_DONE,
+    SWIMSIM_C_RFS_OMITTED, SWIMSIM_C_TIMERS_FIRED, SWIMSIM_C_MSG_CHANGES, SWIMSIM_C_HEAL_ATTEMPTS,
+    SWIMSIM_C_HEAL_FAILURES, SWIMSIM_NCOUNTERS
+};
+
+typedef struct swimsim swimsim_t;
+
+/* ---- lifecycle: swim.NewNode (node.go:194-238) for every member, Destroy (node.go:306-318) ---- */
+int swimsim_create(const swimsim_config *cfg, swimsim_t **out);
+int swimsim_destroy(swimsim_t *h);
+const char *swimsim_last_error(swimsim_t *h);
+int swimsim_abi_version(void);
+
+/* ---- initial state ---- */
+/* converged bootstrap: bootstrapNodes + waitForConvergence + ClearChanges (heal_partition_test.go:416-422) */
+int swimsim_init_converged(swimsim_t *h);
+/* every node knows only itself (NewNode + MakeAlive(self)), maxP = pFactor (disseminator.go:62) */
+int swimsim_init_self_only(swimsim_t *h);
+/* raw row write, no side effects (scenario setup) */
+int swimsim_set_member(swimsim_t *h, uint32_t observer, uint32_t member, int32_t status, int64_t inc_ms);
+/* memberlist.MakeChange (memberlist.go:282-307): returns #applied (0/1) or an error */
+int swimsim_make_change(swimsim_t *h, uint32_t observer, uint32_t member, int64_t inc_ms, int32_t status);
+/* disseminator.ClearChanges (disseminator.go:217-221) */
+int swimsim_clear_changes(swimsim_t *h, uint32_t observer);
+int swimsim_set_live(swimsim_t *h, uint32_t member, int32_t live);
+int swimsim_set_partition(swimsim_t *h, uint32_t member, int32_t label);
+int swimsim_set_round(swimsim_t *h, uint32_t round);
+
+/* ---- the hot path: nrounds protocol periods of every live node (gossip.ProtocolPeriod,
+ *      gossip.go:178-188, for all N nodes under docs/ROUND_SEMANTICS.md). events are applied
+ *      in phase E of the round equal to their .round field. ---- */
+int swimsim_step(swimsim_t *h, uint32_t nrounds, const swimsim_event *events, size_t nevents);
+/* Heal() on one observer right now (heal_via_discover_provider.go:120-177); targets may be NULL */
+int swimsim_heal(swimsim_t *h, uint32_t observer, int32_t *targets, size_t cap, size_t *ntargets);
+
+/* ---- read-back: NodeInterface / memberlist / disseminator views ---- */
+uint32_t swimsim_round(swimsim_t *h);
+/* GetChecksum (node.go:137-147 → memberlist.Checksum, memberlist.go:73-80), all observers */
+int swimsim_checksums(swimsim_t *h, uint32_t *out);
+/* memberlist.GetMembers (memberlist.go:459-468) as a dense row: status[N], inc_ms[N] */
+int swimsim_row(swimsim_t *h, uint32_t observer, uint8_t *status, int64_t *inc_ms);
+/* CountReachableMembers (memberlist.go:485-497) */
+int swimsim_count_reachable(swimsim_t *h, uint32_t observer, uint32_t *out);
+/* GetReachableMembers (memberlist.go:471-483): member indices, ascending */
+int swimsim_reachable(swimsim_t *h, uint32_t observer, uint32_t *idx, size_t cap, size_t *n);
+/* NumPingableMembers (memberlist.go:188-198), disseminator.maxP (disseminator.go:49),
+ * ChangesCount (disseminator.go:239-244), NumMembers (memberlist.go:174-179) */
+int swimsim_node_stats(swimsim_t *h, uint32_t observer, int32_t *pingable, int32_t *maxp,
+                       int32_t *changes, int32_t *members);
+/* disseminator.changes: members, p, source (or -1), source incarnation (ms) */
+int swimsim_changes(swimsim_t *h, uint32_t observer, int32_t *member, int32_t *p, int32_t *source,
+                    int64_t *source_inc_ms, size_t cap, size_t *n);
+/* stateTransitions.timers: members, state, fired, deadline (ms), subject incarnation (ms) */
+int swimsim_timers(swimsim_t *h, uint32_t observer, int32_t *member, int32_t *state, int32_t *fired,
+                   int64_t *deadline_ms, int64_t *subject_inc_ms, size_t cap, size_t *n);
+/* memberlistIter state: currentIndex, number of reshuffles */
+int swimsim_iter_state(swimsim_t *h, uint32_t observer, int64_t *idx, uint32_t *epoch);
+/* phase-S ping targets of the last round (-1 = none) */
+int swimsim_last_targets(swimsim_t *h, int32_t *out);
+int swimsim_counters(swimsim_t *h, uint64_t *out);
+/* canonical state digests (same definition as the oracle): rows, dissemination, timers */
+int swimsim_digest(swimsim_t *h, uint64_t *rows, uint64_t *dissemination, uint64_t *timers);
+/* converged (test_utils.go:188-198): no live node has changes and all live checksums equal */
+int swimsim_converged(swimsim_t *h, int32_t *out);
+
+/* ---- measurement ---- */
+/* average device time (ms) of each kernel family since the last reset, for roofline reporting */
+int swimsim_kernel_times(swimsim_t *h, const char **names, double *avg_ms, uint64_t *launches,
+                         double *alg_bytes, size_t cap, size_t *n);
+int swimsim_enable_timing(swimsim_t *h, int32_t enable);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

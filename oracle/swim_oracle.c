@@ -158,7 +158,7 @@ or_sim *or_create(const or_config *cfg) {
     s->st = (uint8_t *)malloc(nn);
     s->inc = (int64_t *)malloc(nn * sizeof(int64_t));
     memset(s->st, OR_UNKNOWN, nn);
-    memset(s->inc, 0, nn * sizeof(int64_t));
+    for (size_t i = 0; i < nn; i++) s->inc[i] = cfg->t0_ms;  /* never-known entries read e = 0 */
     s->o = (obs *)calloc(s->n, sizeof(obs));
     for (uint32_t i = 0; i < s->n; i++) {
         omap_init(&s->o[i].dis);

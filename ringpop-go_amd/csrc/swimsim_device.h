@@ -1,0 +1,209 @@
+// swimsim_device.h — device-side data layout and inline building blocks of the MI355X engine.
+//
+// Layout in HBM (one handle, NL observer rows of a padded stride NP = roundup(N, 64)):
+//   mw  u32 [NL][NP]   member word = (e << 3) | status. e = (inc - t0)/period. Status codes =
+//                      statePrecedence (swim/member.go:112-128), 7 = not in the memberlist.
+//                      (e,status) as one integer makes nonLocalOverride (member.go:79-93) a single
+//                      unsigned compare.
+//   dp  u8  [NL][NP]   disseminator piggyback counter p (disseminator.go:39-42); 0xFF = no entry
+//   tst u8  [NL][NP]   timer state (suspect 1 / faulty 2 / tombstone 4) | 0x80 fired
+//   aux u32x4[NL][NP]  {dissem source, dissem source e, timer deadline round, timer subject e}
+//   dblk u64 [NL][NBW] bit b: 64-member block b may hold dissemination entries
+//   tblk u32 [NL][NB]  lower bound of the unfired timer deadlines in block b
+// Messages are pools of 16-byte change records {member | status<<24, e, source, source e}, or
+// dense row snapshots for MembershipAsChanges (disseminator.go:107-123).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace swimdev {
+
+constexpr uint32_t ST_ALIVE = 0, ST_SUSPECT = 1, ST_FAULTY = 2, ST_LEAVE = 3, ST_TOMB = 4, ST_UNKNOWN = 7;
+constexpr uint32_t SRC_NONE = 0xFFFFFFFFu;
+constexpr uint32_t NO_DEADLINE = 0xFFFFFFFFu;
+constexpr uint8_t DP_NONE = 0xFF;
+
+enum Counter {
+    C_ROUNDS, C_PINGS, C_PINGS_OK, C_PINGREQS, C_HELPER_CALLS, C_HELPER_ERRORS, C_INCONCLUSIVE,
+    C_SUSPECT_DECL, C_APPLIED, C_REFUTES, C_FULL_SYNCS, C_FULL_SYNCS_PINGREQ, C_RFS_DONE, C_RFS_OMITTED,
+    C_TIMERS_FIRED, C_MSG_CHANGES, C_HEAL_ATTEMPTS, C_HEAL_FAILURES, C_NCOUNTERS,
+    // measurement-only counters (not part of the parity record)
+    C_X_MERGED = C_NCOUNTERS, C_X_APPLIED, C_X_ISSUED, C_X_CS_ROWS, C_NALL
+};
+
+enum ErrBits : uint32_t {
+    E_POOL = 1, E_DENSE = 2, E_ECAP = 4, E_SHORT = 8, E_ITER = 16, E_COUNT = 32
+};
+
+struct MsgDesc {        // a change list in flight
+    uint32_t off_lo, off_hi;  // sparse: record offset in the pool; dense: slot index in off_lo
+    uint32_t len;             // records (dense: number of known members)
+    uint32_t kind;            // 0 sparse, 1 dense, 2 none
+};
+
+struct DS {
+    uint32_t N, NP, NL, lo, NB, NBW;
+    uint32_t W;
+    uint32_t pfactor, K, maxjobs;
+    uint32_t to_susp, to_faulty, to_tomb;  // timeouts in rounds
+    uint32_t ecap;
+    uint64_t seed;
+    uint32_t *mw;
+    uint8_t *dp;
+    uint8_t *tst;
+    uint4 *aux;
+    int32_t *ping, *maxp, *dcnt;
+    uint32_t *dirty, *cs;
+    int32_t *it_idx;
+    uint32_t *it_ep, *tmin, *njobs, *jobs;
+    unsigned long long *dblk;
+    uint32_t *tblk;
+    uint8_t *live;
+    int32_t *part;
+    const uint32_t *addrw;  // [N][6]
+    const uint32_t *tailw;  // [ecap*4][8]
+    unsigned long long *ctr;
+    uint32_t *err;
+    uint4 *pool;
+    unsigned long long *pool_cur;
+    unsigned long long pool_cap;
+    uint32_t *dense;        // [dense_cap][NP]
+    uint4 *dense_meta;      // {source, source e, known count, unused}
+    uint32_t *dense_cur;
+    uint32_t dense_cap;
+};
+
+__host__ __device__ inline bool is_pingable(uint32_t st) { return st <= ST_SUSPECT; }
+
+__host__ __device__ inline int32_t digits10(int32_t n) {
+    int32_t d = 0;
+    while (n > 0) { d++; n /= 10; }
+    return d;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Philox4x32-10 (Salmon et al. 2011, Random123 constants) and the Feistel permutation
+// ---------------------------------------------------------------------------------------------
+struct U4 { uint32_t x, y, z, w; };
+
+__host__ __device__ inline U4 philox10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint64_t seed) {
+    uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+    for (int r = 0; r < 10; r++) {
+        if (r) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+        uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+        uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+        uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        c1 = (uint32_t)p1;
+        c3 = (uint32_t)p0;
+        c0 = n0;
+        c2 = n2;
+    }
+    return U4{c0, c1, c2, c3};
+}
+
+__host__ __device__ inline uint32_t pick(const U4 &v, uint32_t i) {
+    return (i & 3) == 0 ? v.x : (i & 3) == 1 ? v.y : (i & 3) == 2 ? v.z : v.w;
+}
+
+__host__ __device__ inline uint32_t mulhi_n(uint32_t x, uint32_t n) { return (uint32_t)(((uint64_t)x * n) >> 32); }
+
+__host__ __device__ inline uint32_t fmix32(uint32_t h) {
+    h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
+    return h;
+}
+
+struct Feistel {
+    uint32_t k0, k1, k2, k3, half, mask;
+    __host__ __device__ void init(uint64_t seed, uint32_t o, uint32_t epoch, uint32_t n) {
+        U4 k = philox10(epoch, o, 1u, 0u, seed);
+        k0 = k.x; k1 = k.y; k2 = k.z; k3 = k.w;
+        uint32_t b = 2;
+        while (b < 32 && ((uint64_t)1 << b) < n) b += 2;
+        half = b / 2;
+        mask = (1u << half) - 1u;
+    }
+    __host__ __device__ uint32_t enc(uint32_t x) const {
+        uint32_t L = x >> half, R = x & mask, t;
+        t = L ^ (fmix32(R ^ k0) & mask); L = R; R = t;
+        t = L ^ (fmix32(R ^ k1) & mask); L = R; R = t;
+        t = L ^ (fmix32(R ^ k2) & mask); L = R; R = t;
+        t = L ^ (fmix32(R ^ k3) & mask); L = R; R = t;
+        return (L << half) | R;
+    }
+    __host__ __device__ uint32_t dec(uint32_t x) const {
+        uint32_t L = x >> half, R = x & mask, t;
+        t = R ^ (fmix32(L ^ k3) & mask); R = L; L = t;
+        t = R ^ (fmix32(L ^ k2) & mask); R = L; L = t;
+        t = R ^ (fmix32(L ^ k1) & mask); R = L; L = t;
+        t = R ^ (fmix32(L ^ k0) & mask); R = L; L = t;
+        return (L << half) | R;
+    }
+    __host__ __device__ uint32_t perm(uint32_t idx, uint32_t n) const {
+        uint32_t x = idx;
+        do { x = enc(x); } while (x >= n);
+        return x;
+    }
+    __host__ __device__ uint32_t inv(uint32_t m, uint32_t n) const {
+        uint32_t x = m;
+        do { x = dec(x); } while (x >= n);
+        return x;
+    }
+};
+
+// ---------------------------------------------------------------------------------------------
+// FarmHash-32 "mk" pieces (go-farm Fingerprint32; glide.lock:18-19, call site memberlist.go:86)
+// ---------------------------------------------------------------------------------------------
+constexpr uint32_t FH_C1 = 0xcc9e2d51u, FH_C2 = 0x1b873593u;
+
+__host__ __device__ inline uint32_t ror32(uint32_t v, int s) { return (v >> s) | (v << (32 - s)); }
+
+__host__ __device__ inline uint32_t fh_mur(uint32_t a, uint32_t h) {
+    a *= FH_C1; a = ror32(a, 17); a *= FH_C2;
+    h ^= a; h = ror32(h, 19);
+    return h * 5 + 0xe6546b64u;
+}
+
+struct FH {
+    uint32_t h, g, f;
+    __host__ __device__ void block(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t e) {
+        h += a; g += b; f += c;
+        h = fh_mur(d, h) + e;
+        g = fh_mur(c, g) + a;
+        f = fh_mur(b + e * FH_C1, f) + d;
+        f += g; g += f;
+    }
+    // len > 24 prologue from the last 20 bytes t0..t4 (= Fetch32 at len-20, -16, -12, -8, -4)
+    __host__ __device__ void init(uint32_t len, uint32_t t0, uint32_t t1, uint32_t t2, uint32_t t3, uint32_t t4) {
+        h = len; g = FH_C1 * len; f = g;
+        uint32_t a0 = ror32(t4 * FH_C1, 17) * FH_C2;
+        uint32_t a1 = ror32(t3 * FH_C1, 17) * FH_C2;
+        uint32_t a2 = ror32(t1 * FH_C1, 17) * FH_C2;
+        uint32_t a3 = ror32(t2 * FH_C1, 17) * FH_C2;
+        uint32_t a4 = ror32(t0 * FH_C1, 17) * FH_C2;
+        h ^= a0; h = ror32(h, 19); h = h * 5 + 0xe6546b64u;
+        h ^= a2; h = ror32(h, 19); h = h * 5 + 0xe6546b64u;
+        g ^= a1; g = ror32(g, 19); g = g * 5 + 0xe6546b64u;
+        g ^= a3; g = ror32(g, 19); g = g * 5 + 0xe6546b64u;
+        f += a4; f = ror32(f, 19) + 113;
+    }
+    __host__ __device__ uint32_t fin() {
+        g = ror32(g, 11) * FH_C1; g = ror32(g, 17) * FH_C1;
+        f = ror32(f, 11) * FH_C1; f = ror32(f, 17) * FH_C1;
+        h = ror32(h + g, 19); h = h * 5 + 0xe6546b64u; h = ror32(h, 17) * FH_C1;
+        h = ror32(h + f, 19); h = h * 5 + 0xe6546b64u; h = ror32(h, 17) * FH_C1;
+        return h;
+    }
+};
+
+// canonical state digest mix (identical definition in oracle/swim_oracle.c or_digest)
+__host__ __device__ inline uint64_t fmix64(uint64_t k) {
+    k ^= k >> 33; k *= 0xff51afd7ed558ccdULL; k ^= k >> 33; k *= 0xc4ceb9fe1a85ec53ULL; k ^= k >> 33;
+    return k;
+}
+__host__ __device__ inline uint64_t mix4(uint64_t a, uint64_t b, uint64_t c, uint64_t d) {
+    return fmix64(a * 0x9E3779B97F4A7C15ULL ^
+                  fmix64(b * 0xC2B2AE3D27D4EB4FULL ^ fmix64(c * 0x165667B19E3779F9ULL ^ fmix64(d + 0xD6E8FEB86659FD93ULL))));
+}
+
+}  // namespace swimdev

@@ -1,0 +1,996 @@
+// swimsim_engine.hip — host side of libswimsim.so: device memory, the round driver of
+// docs/ROUND_SEMANTICS.md §4, the heal orchestration (§5) and the C ABI of include/swimsim.h.
+//
+// The host decides control flow only: event order, wave counts, heal target order. Every
+// member-state computation runs in the gfx950 kernels of swimsim_kernels.hip. There is no
+// CPU fallback: if the device is unusable, swimsim_create() fails.
+#include "swimsim_kernels.hip"
+
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/swimsim.h"
+
+using namespace swimdev;
+
+namespace {
+
+const char *kStatus[4] = {"alive", "suspect", "faulty", "leave"};
+
+struct Timed {
+    int fam;
+    hipEvent_t a, b;
+};
+
+enum Fam { F_TIMERS, F_SELECT, F_ISSUE, F_SORT, F_RECV, F_RESP, F_PINGREQ, F_JOBS, F_CHECKSUM, F_EVENTS, F_NFAM };
+const char *kFamName[F_NFAM] = {"timers", "select", "issue", "sort", "recv_merge", "resp_merge", "pingreq",
+                                "rfs_jobs", "checksum", "events"};
+
+}  // namespace
+
+struct swimsim {
+    // configuration
+    uint32_t N = 0, NP = 0, NL = 0, lo = 0, W = 19, K = 3, maxjobs = 5, pfactor = 15;
+    int64_t t0 = 0;
+    uint32_t period = 200;
+    uint32_t to_susp = 25, to_faulty = 0, to_tomb = 0;
+    uint64_t seed = 1;
+    uint32_t ecap = 0, max_tl = 0;
+    bool fast_cs = false;
+    int device = 0;
+    hipStream_t s = nullptr;
+    DS d{};
+    // host mirrors
+    std::vector<uint8_t> live;
+    std::vector<int32_t> part;
+    std::vector<std::string> addrs;
+    uint32_t round = 0;
+    uint64_t host_ctr[SWIMSIM_NCOUNTERS] = {0};
+    // work buffers
+    int32_t *tgt = nullptr;
+    uint8_t *failed = nullptr;
+    MsgDesc *sdesc = nullptr, *rdesc = nullptr, *sdesc2 = nullptr, *rdesc2 = nullptr, *snapdesc = nullptr, *hdesc = nullptr;
+    uint32_t *sI = nullptr, *sC = nullptr, *sI2 = nullptr, *sC2 = nullptr;
+    uint32_t *H = nullptr, *nh = nullptr;
+    uint32_t *keys_in = nullptr, *vals_in = nullptr, *keys_out = nullptr, *vals_out = nullptr;
+    uint32_t *ukeys = nullptr, *counts = nullptr, *offs = nullptr, *nruns = nullptr, *info = nullptr;
+    void *cub_tmp = nullptr;
+    size_t cub_bytes = 0;
+    uint32_t *list = nullptr, *cnt = nullptr;
+    uint4 *defer = nullptr;
+    uint32_t *defer_cnt = nullptr;
+    uint32_t *exh_list = nullptr, *exh_cnt = nullptr, *scratch = nullptr;
+    uint8_t *need = nullptr;
+    uint4 *evbuf = nullptr;
+    uint32_t *ev_applied = nullptr;
+    uint32_t evcap = 0;
+    unsigned long long *digest_buf = nullptr;
+    uint32_t *hinfo = nullptr;  // pinned
+    std::vector<void *> allocs;
+    // timing
+    bool timing = false;
+    std::vector<Timed> pending;
+    std::vector<hipEvent_t> evpool;
+    double fam_ms[F_NFAM] = {0};
+    uint64_t fam_n[F_NFAM] = {0};
+    uint64_t fam_bytes_base[C_NALL] = {0};
+    std::string err;
+
+    int fail(int code, const char *fmt, ...) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        err = buf;
+        return code;
+    }
+};
+
+#define HIPCHK(h, x)                                                                             \
+    do {                                                                                         \
+        hipError_t e_ = (x);                                                                     \
+        if (e_ != hipSuccess) return (h)->fail(SWIMSIM_EHIP, "%s: %s", #x, hipGetErrorString(e_)); \
+    } while (0)
+
+namespace {
+
+template <typename T>
+int dalloc(swimsim *h, T **p, size_t count, const char *what) {
+    void *q = nullptr;
+    size_t bytes = std::max<size_t>(count * sizeof(T), 16);
+    hipError_t e = hipMalloc(&q, bytes);
+    if (e != hipSuccess) return h->fail(SWIMSIM_ENOMEM, "hipMalloc(%s, %zu bytes): %s", what, bytes, hipGetErrorString(e));
+    h->allocs.push_back(q);
+    *p = (T *)q;
+    return 0;
+}
+
+hipEvent_t take_event(swimsim *h) {
+    if (!h->evpool.empty()) {
+        hipEvent_t e = h->evpool.back();
+        h->evpool.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    hipEventCreate(&e);
+    return e;
+}
+
+struct Scope {
+    swimsim *h;
+    int fam;
+    hipEvent_t a{}, b{};
+    Scope(swimsim *h_, int f) : h(h_), fam(f) {
+        if (h->timing) {
+            a = take_event(h);
+            hipEventRecord(a, h->s);
+        }
+    }
+    ~Scope() {
+        if (h->timing) {
+            b = take_event(h);
+            hipEventRecord(b, h->s);
+            h->pending.push_back(Timed{fam, a, b});
+        }
+    }
+};
+
+void drain_timing(swimsim *h) {
+    if (h->pending.empty()) return;
+    hipStreamSynchronize(h->s);
+    for (auto &t : h->pending) {
+        float ms = 0;
+        hipEventElapsedTime(&ms, t.a, t.b);
+        h->fam_ms[t.fam] += ms;
+        h->fam_n[t.fam]++;
+        h->evpool.push_back(t.a);
+        h->evpool.push_back(t.b);
+    }
+    h->pending.clear();
+}
+
+inline uint32_t blocks_for_waves(uint32_t waves) { return (waves + 3) / 4; }      // 4 waves per 256-thread block
+inline uint32_t blocks_for_threads(uint32_t n) { return (n + 255) / 256; }
+
+int build_tail_table(swimsim *h, uint32_t ecap) {
+    std::vector<uint32_t> t((size_t)ecap * 4 * 8, 0u);
+    uint32_t max_tl = 0;
+    for (uint32_t e = 0; e < ecap; e++) {
+        char digits[32];
+        snprintf(digits, sizeof digits, "%lld", (long long)(h->t0 + (int64_t)e * h->period));
+        for (uint32_t s = 0; s < 4; s++) {
+            char buf[64];
+            int n = snprintf(buf, sizeof buf, "%s%s;", kStatus[s], digits);
+            if (n > 24) return h->fail(SWIMSIM_EINVAL, "incarnation %s too long for the checksum tail table", digits);
+            uint8_t bytes[24] = {0};
+            memcpy(bytes, buf, (size_t)n);
+            uint32_t *dst = &t[((size_t)e * 4 + s) * 8];
+            for (int w = 0; w < 6; w++)
+                dst[w] = (uint32_t)bytes[4 * w] | ((uint32_t)bytes[4 * w + 1] << 8) | ((uint32_t)bytes[4 * w + 2] << 16) |
+                         ((uint32_t)bytes[4 * w + 3] << 24);
+            dst[6] = (uint32_t)n;
+            max_tl = std::max(max_tl, (uint32_t)n);
+        }
+    }
+    uint32_t *dev = nullptr;
+    if (int rc = dalloc(h, &dev, t.size(), "tail table")) return rc;
+    HIPCHK(h, hipMemcpy(dev, t.data(), t.size() * 4, hipMemcpyHostToDevice));
+    h->d.tailw = dev;
+    h->ecap = ecap;
+    h->d.ecap = ecap;
+    h->max_tl = max_tl;
+    h->fast_cs = (h->W == 19 && h->W + max_tl <= 40);
+    return 0;
+}
+
+int check_err(swimsim *h) {
+    uint32_t e = 0;
+    HIPCHK(h, hipMemcpyAsync(&e, h->d.err, 4, hipMemcpyDeviceToHost, h->s));
+    HIPCHK(h, hipStreamSynchronize(h->s));
+    if (!e) return 0;
+    hipMemsetAsync(h->d.err, 0, 4, h->s);
+    if (e & E_POOL) return h->fail(SWIMSIM_ECAPACITY, "message pool overflow (raise message_pool_bytes)");
+    if (e & E_DENSE) return h->fail(SWIMSIM_ECAPACITY, "dense snapshot pool overflow");
+    if (e & E_ECAP) return h->fail(SWIMSIM_ECAPACITY, "incarnation beyond the checksum table");
+    if (e & E_SHORT) return h->fail(SWIMSIM_EINVAL, "checksum string of <= 24 bytes is not supported");
+    if (e & E_ITER) return h->fail(SWIMSIM_EINVAL, "iterator found no pingable member despite a positive count");
+    return h->fail(SWIMSIM_EINVAL, "dissemination count mismatch (internal error %u)", e);
+}
+
+// --- sorting a (key, value) inbox and run-length encoding it ---
+int sort_inbox(swimsim *h, uint32_t n, uint32_t *host_info) {
+    Scope sc(h, F_SORT);
+    int endbit = 1;
+    while ((1u << endbit) <= h->N) endbit++;
+    size_t bytes = h->cub_bytes;
+    HIPCHK(h, hipcub::DeviceRadixSort::SortPairs(h->cub_tmp, bytes, h->keys_in, h->keys_out, h->vals_in, h->vals_out,
+                                                 (int)n, 0, endbit, h->s));
+    bytes = h->cub_bytes;
+    HIPCHK(h, hipcub::DeviceRunLengthEncode::Encode(h->cub_tmp, bytes, h->keys_out, h->ukeys, h->counts, h->nruns,
+                                                    (int)n, h->s));
+    bytes = h->cub_bytes;
+    HIPCHK(h, hipcub::DeviceScan::ExclusiveSum(h->cub_tmp, bytes, h->counts, h->offs, (int)n, h->s));
+    HIPCHK(h, hipMemsetAsync(h->info, 0, 8, h->s));
+    hipLaunchKernelGGL(k_runs_info, dim3(blocks_for_threads(n)), dim3(256), 0, h->s, h->ukeys, h->counts, h->nruns, h->N,
+                       h->info);
+    HIPCHK(h, hipMemcpyAsync(host_info, h->info, 16, hipMemcpyDeviceToHost, h->s));
+    HIPCHK(h, hipStreamSynchronize(h->s));
+    return 0;
+}
+
+void checksum_dirty(swimsim *h, int mode) {
+    Scope sc(h, F_CHECKSUM);
+    hipMemsetAsync(h->cnt, 0, 4, h->s);
+    hipLaunchKernelGGL(k_list, dim3(blocks_for_threads(h->NL)), dim3(256), 0, h->s, h->d, mode, h->tgt, h->failed,
+                       h->list, h->cnt);
+    launch_checksum(h->d, h->list, h->cnt, h->NL, h->fast_cs, h->s);
+}
+
+// defer list holds uint4 {row, ...}: copy rows out and checksum them
+__global__ void k_defer_rows(const uint4 *defer, const uint32_t *defer_cnt, uint32_t *list, uint32_t *cnt) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) *cnt = *defer_cnt;
+    if (i < *defer_cnt) list[i] = defer[i].x;
+}
+
+void checksum_deferred(swimsim *h, uint32_t maxn) {
+    Scope sc(h, F_CHECKSUM);
+    hipLaunchKernelGGL(k_defer_rows, dim3(blocks_for_threads(maxn)), dim3(256), 0, h->s, h->defer, h->defer_cnt, h->list,
+                       h->cnt);
+    launch_checksum(h->d, h->list, h->cnt, maxn, h->fast_cs, h->s);
+}
+
+// run the receive waves over a sorted inbox (phase D when phase==0, phase Q2 when phase==1)
+void run_waves(swimsim *h, int phase, uint32_t nruns_valid, uint32_t maxcount) {
+    RecvArgs a{};
+    a.ukeys = h->ukeys; a.counts = h->counts; a.offs = h->offs; a.vals = h->vals_out;
+    a.nruns_max = nruns_valid;
+    a.phase = phase;
+    a.sdesc = phase == 0 ? h->sdesc : h->sdesc2;
+    a.sI = phase == 0 ? h->sI : h->sI2;
+    a.sC = phase == 0 ? h->sC : h->sC2;
+    a.rdesc = phase == 0 ? h->rdesc : h->rdesc2;
+    a.defer = h->defer;
+    a.defer_cnt = h->defer_cnt;
+    a.r = h->round;
+    for (uint32_t w = 0; w < maxcount; w++) {
+        a.w = w;
+        {
+            Scope sc(h, phase == 0 ? F_RECV : F_PINGREQ);
+            hipMemsetAsync(h->defer_cnt, 0, 4, h->s);
+            hipLaunchKernelGGL(k_recv, dim3(blocks_for_waves(nruns_valid)), dim3(256), 0, h->s, h->d, a);
+        }
+        checksum_deferred(h, nruns_valid);
+        {
+            Scope sc(h, phase == 0 ? F_RECV : F_PINGREQ);
+            hipLaunchKernelGGL(k_recv_finish, dim3(blocks_for_waves(nruns_valid)), dim3(256), 0, h->s, h->d, h->defer,
+                               h->defer_cnt, a.rdesc, phase);
+        }
+    }
+}
+
+int flush_events(swimsim *h, std::vector<uint4> &evs) {
+    if (evs.empty()) return 0;
+    Scope sc(h, F_EVENTS);
+    if (evs.size() > h->evcap) return h->fail(SWIMSIM_EINVAL, "too many events in one round (%zu)", evs.size());
+    HIPCHK(h, hipMemcpyAsync(h->evbuf, evs.data(), evs.size() * sizeof(uint4), hipMemcpyHostToDevice, h->s));
+    hipLaunchKernelGGL(k_events, dim3(1), dim3(64), 0, h->s, h->d, h->evbuf, (uint32_t)evs.size(), h->round, h->ev_applied);
+    evs.clear();
+    return 0;
+}
+
+int upload_topology(swimsim *h) {
+    HIPCHK(h, hipMemcpyAsync(h->d.live, h->live.data(), h->N, hipMemcpyHostToDevice, h->s));
+    HIPCHK(h, hipMemcpyAsync(h->d.part, h->part.data(), h->N * 4, hipMemcpyHostToDevice, h->s));
+    return 0;
+}
+
+bool host_reach(swimsim *h, uint32_t a, uint32_t b) { return h->live[a] && h->live[b] && h->part[a] == h->part[b]; }
+
+int ensure_clean_checksum(swimsim *h, uint32_t ol) {
+    hipLaunchKernelGGL(k_list_one, dim3(1), dim3(64), 0, h->s, h->list, h->cnt, ol, h->d);
+    launch_checksum(h->d, h->list, h->cnt, 1, h->fast_cs, h->s);
+    return 0;
+}
+
+// sendPingWithChanges o → t, response discarded (heal_partition.go:97-124)
+int ping_with(swimsim *h, uint32_t o, uint32_t t, const MsgDesc *md_dev) {
+    ensure_clean_checksum(h, o - h->lo);
+    uint32_t sinc_cs[2];
+    uint32_t w;
+    HIPCHK(h, hipMemcpyAsync(&w, h->d.mw + (size_t)(o - h->lo) * h->NP + o, 4, hipMemcpyDeviceToHost, h->s));
+    HIPCHK(h, hipMemcpyAsync(&sinc_cs[1], h->d.cs + (o - h->lo), 4, hipMemcpyDeviceToHost, h->s));
+    HIPCHK(h, hipStreamSynchronize(h->s));
+    sinc_cs[0] = w >> 3;
+    hipMemsetAsync(h->defer_cnt, 0, 4, h->s);
+    hipLaunchKernelGGL(k_ping_with, dim3(1), dim3(64), 0, h->s, h->d, t - h->lo, o, md_dev, sinc_cs[0], sinc_cs[1],
+                       h->hdesc + 7, h->defer, h->defer_cnt, h->round);
+    checksum_deferred(h, 1);
+    hipLaunchKernelGGL(k_recv_finish, dim3(1), dim3(64), 0, h->s, h->d, h->defer, h->defer_cnt, h->hdesc + 6, 2);
+    return 0;
+}
+
+int do_heal(swimsim *h, uint32_t o, std::vector<int32_t> *ret) {
+    const uint32_t ol = o - h->lo;
+    std::vector<uint32_t> row(h->NP);
+    HIPCHK(h, hipMemcpyAsync(row.data(), h->d.mw + (size_t)ol * h->NP, h->NP * 4, hipMemcpyDeviceToHost, h->s));
+    HIPCHK(h, hipStreamSynchronize(h->s));
+    std::vector<int32_t> targets;
+    for (uint32_t m = 0; m < h->N; m++)                                      // heal_via_discover_provider.go:136-142
+        if ((row[m] & 7u) >= ST_FAULTY) targets.push_back((int32_t)m);
+    for (uint32_t i = 0; i < targets.size(); i++) {                          // ShuffleStringsInPlace (util.go:189-194)
+        const U4 v = philox10(h->round, o, 3u, i >> 2, h->seed);
+        const uint32_t j = mulhi_n(pick(v, i), i + 1);
+        std::swap(targets[i], targets[j]);
+    }
+    auto del = [](std::vector<int32_t> &t, int32_t v) {                      // del (…:181-191)
+        for (size_t i = 0; i < t.size(); i++) {
+            if (t[i] != v) continue;
+            t[i] = t.back();
+            t.pop_back();
+            i--;
+        }
+    };
+    int failures = 0;
+    while (!targets.empty() && failures < 10) {
+        const int32_t target = targets[0];
+        del(targets, target);
+        h->host_ctr[SWIMSIM_C_HEAL_ATTEMPTS]++;
+        if (!host_reach(h, o, (uint32_t)target)) {                           // sendJoinRequest fails
+            failures++;
+            h->host_ctr[SWIMSIM_C_HEAL_FAILURES]++;
+            continue;
+        }
+        const uint32_t tol = (uint32_t)target - h->lo;
+        HIPCHK(h, hipMemsetAsync(h->d.dense_cur, 0, 4, h->s));
+        hipLaunchKernelGGL(k_snapshot_row, dim3(1), dim3(64), 0, h->s, h->d, ol, h->hdesc + 0);      // MA
+        hipLaunchKernelGGL(k_snapshot_row, dim3(1), dim3(64), 0, h->s, h->d, tol, h->hdesc + 1);     // MB
+        hipLaunchKernelGGL(k_heal_diff, dim3(1), dim3(64), 0, h->s, h->d, h->hdesc + 0, h->hdesc + 1, h->hdesc + 2,
+                           h->hdesc + 3);
+        MsgDesc hd[4];
+        HIPCHK(h, hipMemcpyAsync(hd, h->hdesc, sizeof hd, hipMemcpyDeviceToHost, h->s));
+        HIPCHK(h, hipStreamSynchronize(h->s));
+        if (hd[0].kind != 1 || hd[1].kind != 1) return h->fail(SWIMSIM_ECAPACITY, "dense snapshot pool overflow in heal");
+        if (hd[2].len || hd[3].len) {                                        // reincarnateNodes (97-108)
+            if (hd[2].len) hipLaunchKernelGGL(k_apply_msg, dim3(1), dim3(64), 0, h->s, h->d, ol, h->hdesc + 2, h->round);
+            if (hd[3].len)
+                if (int rc = ping_with(h, o, (uint32_t)target, h->hdesc + 3)) return rc;
+        } else {                                                             // mergePartitions (112-124)
+            hipLaunchKernelGGL(k_apply_msg, dim3(1), dim3(64), 0, h->s, h->d, ol, h->hdesc + 1, h->round);
+            hipLaunchKernelGGL(k_snapshot_row, dim3(1), dim3(64), 0, h->s, h->d, ol, h->hdesc + 4);
+            if (int rc = ping_with(h, o, (uint32_t)target, h->hdesc + 4)) return rc;
+        }
+        std::vector<uint32_t> mb(h->NP);                                     // pingableHosts(MB)
+        HIPCHK(h, hipMemcpyAsync(mb.data(), h->d.dense + (size_t)hd[1].off_lo * h->NP, h->NP * 4, hipMemcpyDeviceToHost,
+                                 h->s));
+        HIPCHK(h, hipStreamSynchronize(h->s));
+        for (uint32_t m = 0; m < h->N; m++) {
+            const uint32_t st = mb[m] & 7u;
+            if (st != ST_UNKNOWN && is_pingable(st == ST_TOMB ? ST_FAULTY : st)) del(targets, (int32_t)m);
+        }
+        if (ret) ret->push_back(target);
+    }
+    return 0;
+}
+
+// one protocol round (docs/ROUND_SEMANTICS.md §4)
+int step_one(swimsim *h, const swimsim_event *ev, size_t nev) {
+    const uint32_t r = h->round;
+    HIPCHK(h, hipMemsetAsync(h->d.pool_cur, 0, 8, h->s));
+    // ---- E: events ----
+    std::vector<uint4> batch;
+    bool topo_dirty = false;
+    for (size_t i = 0; i < nev; i++) {
+        const swimsim_event &e = ev[i];
+        if (e.round != r) continue;
+        const uint32_t a = (uint32_t)e.a;
+        if (a >= h->N) return h->fail(SWIMSIM_EINVAL, "event member %d out of range", e.a);
+        switch (e.kind) {
+        case SWIMSIM_EV_KILL: h->live[a] = 0; topo_dirty = true; break;
+        case SWIMSIM_EV_REVIVE:
+            h->live[a] = 1; topo_dirty = true;
+            batch.push_back(make_uint4(2, a, a, 0));
+            break;
+        case SWIMSIM_EV_REINCARNATE: if (h->live[a]) batch.push_back(make_uint4(2, a, a, 0)); break;
+        case SWIMSIM_EV_LEAVE: if (h->live[a]) batch.push_back(make_uint4(3, a, a, 0)); break;
+        case SWIMSIM_EV_PARTITION: h->part[a] = e.b; topo_dirty = true; break;
+        case SWIMSIM_EV_REAP: if (h->live[a]) batch.push_back(make_uint4(4, a, a, 0)); break;
+        case SWIMSIM_EV_HEAL:
+            if (!h->live[a]) break;
+            if (int rc = flush_events(h, batch)) return rc;
+            if (int rc = upload_topology(h)) return rc;
+            topo_dirty = false;
+            if (int rc = do_heal(h, a, nullptr)) return rc;
+            break;
+        default: return h->fail(SWIMSIM_EINVAL, "unknown event kind %u", e.kind);
+        }
+    }
+    if (int rc = flush_events(h, batch)) return rc;
+    if (topo_dirty)
+        if (int rc = upload_topology(h)) return rc;
+    // ---- T: timers ----
+    {
+        Scope sc(h, F_TIMERS);
+        hipLaunchKernelGGL(k_timers, dim3(blocks_for_waves(h->NL)), dim3(256), 0, h->s, h->d, r);
+    }
+    // ---- S: target selection ----
+    {
+        Scope sc(h, F_SELECT);
+        hipMemsetAsync(h->exh_cnt, 0, 4, h->s);
+        hipLaunchKernelGGL(k_select, dim3(blocks_for_threads(h->NL)), dim3(256), 0, h->s, h->d, h->tgt, h->exh_list,
+                           h->exh_cnt);
+        hipLaunchKernelGGL(k_select_exhaust, dim3(64), dim3(64), 0, h->s, h->d, h->exh_list, h->exh_cnt, h->scratch);
+    }
+    // ---- I: issue (ping requests) ----
+    checksum_dirty(h, 1);
+    {
+        Scope sc(h, F_ISSUE);
+        hipLaunchKernelGGL(k_issue, dim3(blocks_for_waves(h->NL)), dim3(256), 0, h->s, h->d, 0, h->tgt, h->failed,
+                           h->sdesc, h->sI, h->sC);
+        HIPCHK(h, hipMemsetAsync(h->info + 2, 0, 4, h->s));
+        hipLaunchKernelGGL(k_pairs_direct, dim3(blocks_for_threads(h->NL)), dim3(256), 0, h->s, h->d, h->tgt, h->keys_in,
+                           h->vals_in, h->failed, h->info);
+    }
+    // ---- D: deliver in waves ----
+    uint32_t *hi = h->hinfo;
+    HIPCHK(h, hipMemcpyAsync(hi + 4, h->info + 2, 4, hipMemcpyDeviceToHost, h->s));
+    if (int rc = sort_inbox(h, h->NL, hi)) return rc;
+    const uint32_t nfailed = hi[4];
+    HIPCHK(h, hipMemsetAsync(h->d.dense_cur, 0, 4, h->s));
+    run_waves(h, 0, hi[0], hi[1]);
+    // ---- R: responses ----
+    {
+        Scope sc(h, F_RESP);
+        hipLaunchKernelGGL(k_resp, dim3(blocks_for_waves(h->NL)), dim3(256), 0, h->s, h->d, h->tgt, h->failed, h->sdesc,
+                           h->rdesc, r);
+    }
+    // ---- Q: indirect pings ----
+    if (nfailed) {
+        {
+            Scope sc(h, F_PINGREQ);
+            hipLaunchKernelGGL(k_helpers, dim3(blocks_for_threads(h->NL)), dim3(256), 0, h->s, h->d, h->tgt, h->failed,
+                               h->H, h->nh, r);
+        }
+        checksum_dirty(h, 2);
+        {
+            Scope sc(h, F_PINGREQ);
+            hipLaunchKernelGGL(k_issue, dim3(blocks_for_waves(h->NL)), dim3(256), 0, h->s, h->d, 1, h->tgt, h->failed,
+                               h->sdesc2, h->sI2, h->sC2);
+            hipLaunchKernelGGL(k_pairs_helpers, dim3(blocks_for_threads(h->NL * h->K)), dim3(256), 0, h->s, h->d,
+                               h->failed, h->H, h->nh, h->keys_in, h->vals_in);
+        }
+        if (int rc = sort_inbox(h, h->NL * h->K, hi)) return rc;
+        HIPCHK(h, hipMemsetAsync(h->d.dense_cur, 0, 4, h->s));
+        run_waves(h, 1, hi[0], hi[1]);
+        {
+            Scope sc(h, F_PINGREQ);
+            hipLaunchKernelGGL(k_resolve, dim3(blocks_for_waves(h->NL)), dim3(256), 0, h->s, h->d, h->tgt, h->failed,
+                               h->H, h->nh, h->sdesc2, h->rdesc2, r);
+        }
+    }
+    // ---- F: reverse full syncs ----
+    {
+        Scope sc(h, F_JOBS);
+        HIPCHK(h, hipMemsetAsync(h->d.dense_cur, 0, 4, h->s));
+        hipLaunchKernelGGL(k_jobs_mark, dim3(blocks_for_threads(h->NL)), dim3(256), 0, h->s, h->d, h->need);
+        hipLaunchKernelGGL(k_jobs_snap, dim3(blocks_for_waves(h->NL)), dim3(256), 0, h->s, h->d, h->need, h->snapdesc);
+        for (uint32_t q = 0; q < h->maxjobs; q++)
+            hipLaunchKernelGGL(k_jobs_merge, dim3(blocks_for_waves(h->NL)), dim3(256), 0, h->s, h->d, q, h->snapdesc, r);
+        hipLaunchKernelGGL(k_jobs_reset, dim3(blocks_for_threads(h->NL)), dim3(256), 0, h->s, h->d, h->need);
+    }
+    // ---- C: checksums of dirty rows ----
+    checksum_dirty(h, 0);
+    h->round++;
+    h->host_ctr[SWIMSIM_C_ROUNDS]++;
+    HIPCHK(h, hipGetLastError());
+    return 0;
+}
+
+int ensure_ecap(swimsim *h, uint32_t upto) {
+    if (upto < h->ecap) return 0;
+    uint32_t c = h->ecap;
+    while (c <= upto) c *= 2;
+    HIPCHK(h, hipStreamSynchronize(h->s));
+    return build_tail_table(h, c);
+}
+
+int to_e(swimsim *h, int64_t inc_ms, uint32_t *e) {
+    const int64_t dlt = inc_ms - h->t0;
+    if (dlt < 0 || dlt % h->period) return h->fail(SWIMSIM_ERANGE, "incarnation %lld is not t0 + e*period", (long long)inc_ms);
+    const int64_t q = dlt / h->period;
+    if (q >= (1ll << 29)) return h->fail(SWIMSIM_ERANGE, "incarnation %lld too far from t0", (long long)inc_ms);
+    *e = (uint32_t)q;
+    return 0;
+}
+
+inline int64_t from_e(const swimsim *h, uint32_t e) { return h->t0 + (int64_t)e * h->period; }
+
+}  // namespace
+
+// =============================================================================================
+// C ABI
+// =============================================================================================
+extern "C" {
+
+int swimsim_abi_version(void) { return SWIMSIM_ABI_VERSION; }
+
+const char *swimsim_last_error(swimsim_t *h) { return h ? h->err.c_str() : "null handle"; }
+
+int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
+    if (!cfg || !out) return SWIMSIM_EINVAL;
+    *out = nullptr;
+    swimsim *h = new swimsim();
+    auto bail = [&](int rc) {
+        swimsim_destroy(h);
+        return rc;
+    };
+    static thread_local std::string create_err;
+    h->N = cfg->num_members;
+    if (h->N < 1 || h->N >= (1u << 24)) return bail(SWIMSIM_EINVAL);
+    h->NP = (h->N + 63) & ~63u;
+    h->lo = cfg->observer_begin;
+    const uint32_t hi_o = cfg->observer_end ? cfg->observer_end : h->N;
+    if (h->lo >= hi_o || hi_o > h->N) return bail(SWIMSIM_EINVAL);
+    h->NL = hi_o - h->lo;
+    h->t0 = cfg->t0_ms ? cfg->t0_ms : 1500000000000ll;
+    h->period = cfg->protocol_period_ms ? cfg->protocol_period_ms : 200;
+    const uint32_t ts = cfg->suspect_timeout_ms ? cfg->suspect_timeout_ms : 5000;
+    const uint32_t tf = cfg->faulty_timeout_ms ? cfg->faulty_timeout_ms : 24u * 3600u * 1000u;
+    const uint32_t tt = cfg->tombstone_timeout_ms ? cfg->tombstone_timeout_ms : 60000;
+    if (ts % h->period || tf % h->period || tt % h->period) {
+        h->err = "state timeouts must be multiples of the protocol period";
+        return bail(SWIMSIM_EINVAL);
+    }
+    h->to_susp = ts / h->period;
+    h->to_faulty = tf / h->period;
+    h->to_tomb = tt / h->period;
+    h->K = cfg->ping_request_size ? cfg->ping_request_size : 3;
+    if (h->K > 8) return bail(SWIMSIM_EINVAL);
+    h->maxjobs = cfg->max_reverse_full_sync_jobs ? cfg->max_reverse_full_sync_jobs : 5;
+    h->pfactor = cfg->p_factor ? cfg->p_factor : 15;
+    h->seed = cfg->seed;
+    h->device = (int)cfg->device;
+    // addresses
+    h->addrs.resize(h->N);
+    if (cfg->addresses) {
+        for (uint32_t m = 0; m < h->N; m++) {
+            const char *a = cfg->addresses + (size_t)m * cfg->addr_stride;
+            h->addrs[m] = std::string(a, strnlen(a, cfg->addr_stride));
+        }
+        h->W = (uint32_t)h->addrs[0].size();
+        for (uint32_t m = 0; m < h->N; m++) {
+            if (h->addrs[m].size() != h->W || (m && !(h->addrs[m - 1] < h->addrs[m]))) {
+                h->err = "addresses must be fixed-width and strictly ascending";
+                return bail(SWIMSIM_EINVAL);
+            }
+        }
+    } else {
+        char buf[32];
+        for (uint32_t m = 0; m < h->N; m++) {
+            snprintf(buf, sizeof buf, "10.%03u.%03u.%03u:7000", (m >> 16) & 255, (m >> 8) & 255, m & 255);
+            h->addrs[m] = buf;
+        }
+        h->W = 19;
+    }
+    if (h->W < 13 || h->W > 20) {
+        h->err = "address width must be 13..20 bytes";
+        return bail(SWIMSIM_EINVAL);
+    }
+    if (hipSetDevice(h->device) != hipSuccess) {
+        h->err = "hipSetDevice failed (no usable MI355X device)";
+        return bail(SWIMSIM_EHIP);
+    }
+    if (hipStreamCreateWithFlags(&h->s, hipStreamNonBlocking) != hipSuccess) {
+        h->err = "hipStreamCreate failed";
+        return bail(SWIMSIM_EHIP);
+    }
+    DS &d = h->d;
+    d.N = h->N; d.NP = h->NP; d.NL = h->NL; d.lo = h->lo;
+    d.NB = h->NP / 64;
+    d.NBW = (d.NB + 63) / 64;
+    d.W = h->W; d.pfactor = h->pfactor; d.K = h->K; d.maxjobs = h->maxjobs;
+    d.to_susp = h->to_susp; d.to_faulty = h->to_faulty; d.to_tomb = h->to_tomb;
+    d.seed = h->seed;
+    const size_t rows = (size_t)h->NL * h->NP;
+    int rc = 0;
+    if ((rc = dalloc(h, &d.mw, rows, "member words")) || (rc = dalloc(h, &d.dp, rows, "piggyback counters")) ||
+        (rc = dalloc(h, &d.tst, rows, "timer states")) || (rc = dalloc(h, &d.aux, rows, "aux")) ||
+        (rc = dalloc(h, &d.ping, h->NL, "ping")) || (rc = dalloc(h, &d.maxp, h->NL, "maxp")) ||
+        (rc = dalloc(h, &d.dcnt, h->NL, "dcnt")) || (rc = dalloc(h, &d.dirty, h->NL, "dirty")) ||
+        (rc = dalloc(h, &d.cs, h->NL, "cs")) || (rc = dalloc(h, &d.it_idx, h->NL, "it_idx")) ||
+        (rc = dalloc(h, &d.it_ep, h->NL, "it_ep")) || (rc = dalloc(h, &d.tmin, h->NL, "tmin")) ||
+        (rc = dalloc(h, &d.njobs, h->NL, "njobs")) || (rc = dalloc(h, &d.jobs, (size_t)h->NL * h->maxjobs, "jobs")) ||
+        (rc = dalloc(h, &d.dblk, (size_t)h->NL * d.NBW, "dblk")) || (rc = dalloc(h, &d.tblk, (size_t)h->NL * d.NB, "tblk")) ||
+        (rc = dalloc(h, &d.live, h->N, "live")) || (rc = dalloc(h, &d.part, h->N, "part")) ||
+        (rc = dalloc(h, &d.ctr, 32, "counters")) || (rc = dalloc(h, &d.err, 4, "err")))
+        return bail(rc);
+    // address words
+    {
+        std::vector<uint32_t> aw((size_t)h->N * 6, 0u);
+        for (uint32_t m = 0; m < h->N; m++) {
+            uint8_t b[24] = {0};
+            memcpy(b, h->addrs[m].data(), h->W);
+            for (int w = 0; w < 6; w++)
+                aw[(size_t)m * 6 + w] = (uint32_t)b[4 * w] | ((uint32_t)b[4 * w + 1] << 8) | ((uint32_t)b[4 * w + 2] << 16) |
+                                        ((uint32_t)b[4 * w + 3] << 24);
+        }
+        uint32_t *dev = nullptr;
+        if ((rc = dalloc(h, &dev, aw.size(), "address words"))) return bail(rc);
+        if (hipMemcpy(dev, aw.data(), aw.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return bail(SWIMSIM_EHIP);
+        d.addrw = dev;
+    }
+    if ((rc = build_tail_table(h, cfg->max_rounds ? cfg->max_rounds : 65536))) return bail(rc);
+    // pools
+    const uint64_t want_records = cfg->message_pool_bytes
+                                      ? cfg->message_pool_bytes / 16
+                                      : std::min<uint64_t>(std::max<uint64_t>(4ull * h->NL * h->N, 1ull << 20), (8ull << 30) / 16);
+    d.pool_cap = want_records;
+    if ((rc = dalloc(h, &d.pool, want_records, "message pool")) || (rc = dalloc(h, &d.pool_cur, 1, "pool cursor")))
+        return bail(rc);
+    d.dense_cap = (uint32_t)std::max<uint64_t>(64, std::min<uint64_t>(h->NL + 64, (4ull << 30) / (4ull * h->NP)));
+    if ((rc = dalloc(h, &d.dense, (size_t)d.dense_cap * h->NP, "dense snapshots")) ||
+        (rc = dalloc(h, &d.dense_meta, d.dense_cap, "dense meta")) || (rc = dalloc(h, &d.dense_cur, 1, "dense cursor")))
+        return bail(rc);
+    // work buffers
+    const size_t NLK = (size_t)h->NL * h->K;
+    if ((rc = dalloc(h, &h->tgt, h->NL, "tgt")) || (rc = dalloc(h, &h->failed, h->NL, "failed")) ||
+        (rc = dalloc(h, &h->sdesc, h->NL, "sdesc")) || (rc = dalloc(h, &h->rdesc, h->NL, "rdesc")) ||
+        (rc = dalloc(h, &h->sdesc2, h->NL, "sdesc2")) || (rc = dalloc(h, &h->rdesc2, NLK, "rdesc2")) ||
+        (rc = dalloc(h, &h->snapdesc, h->NL, "snapdesc")) || (rc = dalloc(h, &h->hdesc, 8, "hdesc")) ||
+        (rc = dalloc(h, &h->sI, h->NL, "sI")) || (rc = dalloc(h, &h->sC, h->NL, "sC")) ||
+        (rc = dalloc(h, &h->sI2, h->NL, "sI2")) || (rc = dalloc(h, &h->sC2, h->NL, "sC2")) ||
+        (rc = dalloc(h, &h->H, NLK, "H")) || (rc = dalloc(h, &h->nh, h->NL, "nh")) ||
+        (rc = dalloc(h, &h->keys_in, NLK, "keys_in")) || (rc = dalloc(h, &h->vals_in, NLK, "vals_in")) ||
+        (rc = dalloc(h, &h->keys_out, NLK, "keys_out")) || (rc = dalloc(h, &h->vals_out, NLK, "vals_out")) ||
+        (rc = dalloc(h, &h->ukeys, NLK, "ukeys")) || (rc = dalloc(h, &h->counts, NLK, "counts")) ||
+        (rc = dalloc(h, &h->offs, NLK, "offs")) || (rc = dalloc(h, &h->nruns, 1, "nruns")) ||
+        (rc = dalloc(h, &h->info, 8, "info")) || (rc = dalloc(h, &h->list, NLK + 64, "list")) ||
+        (rc = dalloc(h, &h->cnt, 1, "cnt")) || (rc = dalloc(h, &h->defer, NLK + 64, "defer")) ||
+        (rc = dalloc(h, &h->defer_cnt, 1, "defer_cnt")) || (rc = dalloc(h, &h->exh_list, h->NL, "exh_list")) ||
+        (rc = dalloc(h, &h->exh_cnt, 1, "exh_cnt")) || (rc = dalloc(h, &h->scratch, (size_t)64 * (h->NP / 32), "scratch")) ||
+        (rc = dalloc(h, &h->need, h->NL, "need")) || (rc = dalloc(h, &h->digest_buf, 4, "digest")))
+        return bail(rc);
+    h->evcap = 4 * h->N + 64;
+    if ((rc = dalloc(h, &h->evbuf, h->evcap, "events")) || (rc = dalloc(h, &h->ev_applied, h->evcap, "ev_applied")))
+        return bail(rc);
+    {
+        size_t b1 = 0, b2 = 0, b3 = 0;
+        hipcub::DeviceRadixSort::SortPairs(nullptr, b1, h->keys_in, h->keys_out, h->vals_in, h->vals_out, (int)NLK, 0, 32);
+        hipcub::DeviceRunLengthEncode::Encode(nullptr, b2, h->keys_out, h->ukeys, h->counts, h->nruns, (int)NLK);
+        hipcub::DeviceScan::ExclusiveSum(nullptr, b3, h->counts, h->offs, (int)NLK);
+        h->cub_bytes = std::max(b1, std::max(b2, b3));
+        if ((rc = dalloc(h, (uint8_t **)&h->cub_tmp, h->cub_bytes, "cub temp"))) return bail(rc);
+    }
+    if (hipHostMalloc((void **)&h->hinfo, 64, 0) != hipSuccess) return bail(SWIMSIM_ENOMEM);
+    hipMemset(d.ctr, 0, 32 * 8);
+    hipMemset(d.err, 0, 4);
+    hipMemset(h->need, 0, h->NL);
+    hipMemset(d.njobs, 0, h->NL * 4);
+    h->live.assign(h->N, 1);
+    h->part.assign(h->N, 0);
+    if (upload_topology(h) || hipStreamSynchronize(h->s) != hipSuccess) return bail(SWIMSIM_EHIP);
+    if (hipGetLastError() != hipSuccess) return bail(SWIMSIM_EHIP);
+    *out = h;
+    return SWIMSIM_OK;
+}
+
+int swimsim_destroy(swimsim_t *h) {
+    if (!h) return SWIMSIM_OK;
+    if (h->s) hipStreamSynchronize(h->s);
+    for (auto &t : h->pending) { hipEventDestroy(t.a); hipEventDestroy(t.b); }
+    for (auto e : h->evpool) hipEventDestroy(e);
+    for (void *p : h->allocs) hipFree(p);
+    if (h->hinfo) hipHostFree(h->hinfo);
+    if (h->s) hipStreamDestroy(h->s);
+    delete h;
+    return SWIMSIM_OK;
+}
+
+static int init_rows(swimsim_t *h, int mode) {
+    hipLaunchKernelGGL(k_init_rows, dim3(blocks_for_waves(h->NL)), dim3(256), 0, h->s, h->d, mode, 0u);
+    checksum_dirty(h, 0);
+    return check_err(h);
+}
+
+int swimsim_init_converged(swimsim_t *h) { return h ? init_rows(h, 0) : SWIMSIM_EINVAL; }
+int swimsim_init_self_only(swimsim_t *h) { return h ? init_rows(h, 1) : SWIMSIM_EINVAL; }
+
+static bool own(const swimsim *h, uint32_t o) { return o >= h->lo && o < h->lo + h->NL; }
+
+int swimsim_set_member(swimsim_t *h, uint32_t o, uint32_t m, int32_t status, int64_t inc_ms) {
+    if (!h || !own(h, o) || m >= h->N) return SWIMSIM_EINVAL;
+    if (!(status >= 0 && status <= 4) && status != SWIMSIM_UNKNOWN) return SWIMSIM_EINVAL;
+    uint32_t e = 0;
+    if (status != SWIMSIM_UNKNOWN)
+        if (int rc = to_e(h, inc_ms, &e)) return rc;
+    const uint32_t w = (e << 3) | (uint32_t)status;
+    HIPCHK(h, hipMemcpyAsync(h->d.mw + (size_t)(o - h->lo) * h->NP + m, &w, 4, hipMemcpyHostToDevice, h->s));
+    hipLaunchKernelGGL(k_recount, dim3(1), dim3(64), 0, h->s, h->d, o - h->lo);
+    HIPCHK(h, hipStreamSynchronize(h->s));
+    return SWIMSIM_OK;
+}
+
+int swimsim_make_change(swimsim_t *h, uint32_t o, uint32_t m, int64_t inc_ms, int32_t status) {
+    if (!h || !own(h, o) || m >= h->N || status < 0 || status > 4) return SWIMSIM_EINVAL;
+    uint32_t e;
+    if (int rc = to_e(h, inc_ms, &e)) return rc;
+    std::vector<uint4> b{make_uint4(1, o, m, e | ((uint32_t)status << 29))};
+    if (int rc = flush_events(h, b)) return rc;
+    uint32_t applied = 0;
+    HIPCHK(h, hipMemcpyAsync(&applied, h->ev_applied, 4, hipMemcpyDeviceToHost, h->s));
+    HIPCHK(h, hipStreamSynchronize(h->s));
+    return (int)applied;
+}
+
+int swimsim_clear_changes(swimsim_t *h, uint32_t o) {
+    if (!h || !own(h, o)) return SWIMSIM_EINVAL;
+    hipLaunchKernelGGL(k_clear_changes, dim3(1), dim3(256), 0, h->s, h->d, o - h->lo);
+    HIPCHK(h, hipStreamSynchronize(h->s));
+    return SWIMSIM_OK;
+}
+
+int swimsim_set_live(swimsim_t *h, uint32_t m, int32_t live) {
+    if (!h || m >= h->N) return SWIMSIM_EINVAL;
+    h->live[m] = live ? 1 : 0;
+    return upload_topology(h);
+}
+
+int swimsim_set_partition(swimsim_t *h, uint32_t m, int32_t label) {
+    if (!h || m >= h->N) return SWIMSIM_EINVAL;
+    h->part[m] = label;
+    return upload_topology(h);
+}
+
+int swimsim_set_round(swimsim_t *h, uint32_t r) {
+    if (!h) return SWIMSIM_EINVAL;
+    h->round = r;
+    return ensure_ecap(h, r + 1);
+}
+
+int swimsim_step(swimsim_t *h, uint32_t nrounds, const swimsim_event *events, size_t nevents) {
+    if (!h) return SWIMSIM_EINVAL;
+    for (uint32_t i = 0; i < nrounds; i++) {
+        if (int rc = ensure_ecap(h, h->round + 1)) return rc;
+        if (int rc = step_one(h, events, nevents)) return rc;
+    }
+    if (int rc = check_err(h)) return rc;
+    drain_timing(h);
+    return SWIMSIM_OK;
+}
+
+int swimsim_heal(swimsim_t *h, uint32_t o, int32_t *targets, size_t cap, size_t *ntargets) {
+    if (!h || !own(h, o)) return SWIMSIM_EINVAL;
+    std::vector<int32_t> ret;
+    HIPCHK(h, hipMemsetAsync(h->d.pool_cur, 0, 8, h->s));
+    if (int rc = do_heal(h, o, &ret)) return rc;
+    if (int rc = check_err(h)) return rc;
+    if (targets)
+        for (size_t i = 0; i < ret.size() && i < cap; i++) targets[i] = ret[i];
+    if (ntargets) *ntargets = ret.size();
+    return SWIMSIM_OK;
+}
+
+uint32_t swimsim_round(swimsim_t *h) { return h ? h->round : 0; }
+
+int swimsim_checksums(swimsim_t *h, uint32_t *out) {
+    if (!h || !out) return SWIMSIM_EINVAL;
+    checksum_dirty(h, 0);
+    HIPCHK(h, hipMemcpyAsync(out, h->d.cs, h->NL * 4, hipMemcpyDeviceToHost, h->s));
+    return check_err(h);
+}
+
+int swimsim_row(swimsim_t *h, uint32_t o, uint8_t *status, int64_t *inc_ms) {
+    if (!h || !own(h, o)) return SWIMSIM_EINVAL;
+    std::vector<uint32_t> row(h->NP);
+    HIPCHK(h, hipMemcpyAsync(row.data(), h->d.mw + (size_t)(o - h->lo) * h->NP, h->NP * 4, hipMemcpyDeviceToHost, h->s));
+    HIPCHK(h, hipStreamSynchronize(h->s));
+    for (uint32_t m = 0; m < h->N; m++) {
+        if (status) status[m] = (uint8_t)(row[m] & 7u);
+        if (inc_ms) inc_ms[m] = from_e(h, row[m] >> 3);
+    }
+    return SWIMSIM_OK;
+}
+
+int swimsim_count_reachable(swimsim_t *h, uint32_t o, uint32_t *out) {
+    if (!h || !out) return SWIMSIM_EINVAL;
+    std::vector<uint8_t> st(h->N);
+    if (int rc = swimsim_row(h, o, st.data(), nullptr)) return rc;
+    uint32_t c = 0;
+    for (uint32_t m = 0; m < h->N; m++) c += st[m] <= 1;
+    *out = c;
+    return SWIMSIM_OK;
+}
+
+int swimsim_reachable(swimsim_t *h, uint32_t o, uint32_t *idx, size_t cap, size_t *n) {
+    if (!h) return SWIMSIM_EINVAL;
+    std::vector<uint8_t> st(h->N);
+    if (int rc = swimsim_row(h, o, st.data(), nullptr)) return rc;
+    size_t k = 0;
+    for (uint32_t m = 0; m < h->N; m++)
+        if (st[m] <= 1) {
+            if (idx && k < cap) idx[k] = m;
+            k++;
+        }
+    if (n) *n = k;
+    return SWIMSIM_OK;
+}
+
+int swimsim_node_stats(swimsim_t *h, uint32_t o, int32_t *pingable, int32_t *maxp, int32_t *changes, int32_t *members) {
+    if (!h || !own(h, o)) return SWIMSIM_EINVAL;
+    const uint32_t ol = o - h->lo;
+    int32_t v[3];
+    HIPCHK(h, hipMemcpyAsync(&v[0], h->d.ping + ol, 4, hipMemcpyDeviceToHost, h->s));
+    HIPCHK(h, hipMemcpyAsync(&v[1], h->d.maxp + ol, 4, hipMemcpyDeviceToHost, h->s));
+    HIPCHK(h, hipMemcpyAsync(&v[2], h->d.dcnt + ol, 4, hipMemcpyDeviceToHost, h->s));
+    HIPCHK(h, hipStreamSynchronize(h->s));
+    if (pingable) *pingable = v[0];
+    if (maxp) *maxp = v[1];
+    if (changes) *changes = v[2];
+    if (members) {
+        std::vector<uint8_t> st(h->N);
+        if (int rc = swimsim_row(h, o, st.data(), nullptr)) return rc;
+        int32_t c = 0;
+        for (uint32_t m = 0; m < h->N; m++) c += st[m] != SWIMSIM_UNKNOWN;
+        *members = c;
+    }
+    return SWIMSIM_OK;
+}
+
+int swimsim_changes(swimsim_t *h, uint32_t o, int32_t *member, int32_t *p, int32_t *source, int64_t *source_inc_ms,
+                    size_t cap, size_t *n) {
+    if (!h || !own(h, o)) return SWIMSIM_EINVAL;
+    const size_t base = (size_t)(o - h->lo) * h->NP;
+    std::vector<uint8_t> dp(h->NP);
+    std::vector<uint4> aux(h->NP);
+    HIPCHK(h, hipMemcpyAsync(dp.data(), h->d.dp + base, h->NP, hipMemcpyDeviceToHost, h->s));
+    HIPCHK(h, hipMemcpyAsync(aux.data(), h->d.aux + base, h->NP * 16, hipMemcpyDeviceToHost, h->s));
+    HIPCHK(h, hipStreamSynchronize(h->s));
+    size_t k = 0;
+    for (uint32_t m = 0; m < h->N; m++) {
+        if (dp[m] == DP_NONE) continue;
+        if (k < cap) {
+            if (member) member[k] = (int32_t)m;
+            if (p) p[k] = dp[m];
+            if (source) source[k] = aux[m].x == SRC_NONE ? -1 : (int32_t)aux[m].x;
+            if (source_inc_ms) source_inc_ms[k] = aux[m].x == SRC_NONE ? 0 : from_e(h, aux[m].y);
+        }
+        k++;
+    }
+    if (n) *n = k;
+    return SWIMSIM_OK;
+}
+
+int swimsim_timers(swimsim_t *h, uint32_t o, int32_t *member, int32_t *state, int32_t *fired, int64_t *deadline_ms,
+                   int64_t *subject_inc_ms, size_t cap, size_t *n) {
+    if (!h || !own(h, o)) return SWIMSIM_EINVAL;
+    const size_t base = (size_t)(o - h->lo) * h->NP;
+    std::vector<uint8_t> ts(h->NP);
+    std::vector<uint4> aux(h->NP);
+    HIPCHK(h, hipMemcpyAsync(ts.data(), h->d.tst + base, h->NP, hipMemcpyDeviceToHost, h->s));
+    HIPCHK(h, hipMemcpyAsync(aux.data(), h->d.aux + base, h->NP * 16, hipMemcpyDeviceToHost, h->s));
+    HIPCHK(h, hipStreamSynchronize(h->s));
+    size_t k = 0;
+    for (uint32_t m = 0; m < h->N; m++) {
+        if (!(ts[m] & 7u)) continue;
+        if (k < cap) {
+            if (member) member[k] = (int32_t)m;
+            if (state) state[k] = ts[m] & 7;
+            if (fired) fired[k] = (ts[m] >> 7) & 1;
+            if (deadline_ms) deadline_ms[k] = from_e(h, aux[m].z);
+            if (subject_inc_ms) subject_inc_ms[k] = from_e(h, aux[m].w);
+        }
+        k++;
+    }
+    if (n) *n = k;
+    return SWIMSIM_OK;
+}
+
+int swimsim_iter_state(swimsim_t *h, uint32_t o, int64_t *idx, uint32_t *epoch) {
+    if (!h || !own(h, o)) return SWIMSIM_EINVAL;
+    int32_t i;
+    uint32_t ep;
+    HIPCHK(h, hipMemcpyAsync(&i, h->d.it_idx + (o - h->lo), 4, hipMemcpyDeviceToHost, h->s));
+    HIPCHK(h, hipMemcpyAsync(&ep, h->d.it_ep + (o - h->lo), 4, hipMemcpyDeviceToHost, h->s));
+    HIPCHK(h, hipStreamSynchronize(h->s));
+    if (idx) *idx = i;
+    if (epoch) *epoch = ep;
+    return SWIMSIM_OK;
+}
+
+int swimsim_last_targets(swimsim_t *h, int32_t *out) {
+    if (!h || !out) return SWIMSIM_EINVAL;
+    HIPCHK(h, hipMemcpyAsync(out, h->tgt, h->NL * 4, hipMemcpyDeviceToHost, h->s));
+    HIPCHK(h, hipStreamSynchronize(h->s));
+    return SWIMSIM_OK;
+}
+
+int swimsim_counters(swimsim_t *h, uint64_t *out) {
+    if (!h || !out) return SWIMSIM_EINVAL;
+    uint64_t c[32];
+    HIPCHK(h, hipMemcpyAsync(c, h->d.ctr, sizeof c, hipMemcpyDeviceToHost, h->s));
+    HIPCHK(h, hipStreamSynchronize(h->s));
+    for (int i = 0; i < SWIMSIM_NCOUNTERS; i++) out[i] = c[i] + h->host_ctr[i];
+    return SWIMSIM_OK;
+}
+
+int swimsim_digest(swimsim_t *h, uint64_t *rows, uint64_t *dis, uint64_t *tim) {
+    if (!h) return SWIMSIM_EINVAL;
+    HIPCHK(h, hipMemsetAsync(h->digest_buf, 0, 32, h->s));
+    hipLaunchKernelGGL(k_digest, dim3(blocks_for_waves(h->NL)), dim3(256), 0, h->s, h->d, h->digest_buf, 0u);
+    unsigned long long v[3];
+    HIPCHK(h, hipMemcpyAsync(v, h->digest_buf, 24, hipMemcpyDeviceToHost, h->s));
+    HIPCHK(h, hipStreamSynchronize(h->s));
+    if (rows) *rows = v[0];
+    if (dis) *dis = v[1];
+    if (tim) *tim = v[2];
+    return SWIMSIM_OK;
+}
+
+int swimsim_converged(swimsim_t *h, int32_t *out) {
+    if (!h || !out) return SWIMSIM_EINVAL;
+    std::vector<uint32_t> cs(h->NL);
+    std::vector<int32_t> dc(h->NL);
+    if (int rc = swimsim_checksums(h, cs.data())) return rc;
+    HIPCHK(h, hipMemcpyAsync(dc.data(), h->d.dcnt, h->NL * 4, hipMemcpyDeviceToHost, h->s));
+    HIPCHK(h, hipStreamSynchronize(h->s));
+    bool ok = true, have = false;
+    uint32_t first = 0;
+    for (uint32_t ol = 0; ol < h->NL && ok; ol++) {
+        if (!h->live[h->lo + ol]) continue;
+        if (dc[ol]) ok = false;
+        if (!have) { first = cs[ol]; have = true; }
+        else if (cs[ol] != first) ok = false;
+    }
+    *out = ok ? 1 : 0;
+    return SWIMSIM_OK;
+}
+
+int swimsim_enable_timing(swimsim_t *h, int32_t enable) {
+    if (!h) return SWIMSIM_EINVAL;
+    drain_timing(h);
+    h->timing = enable != 0;
+    for (int f = 0; f < F_NFAM; f++) { h->fam_ms[f] = 0; h->fam_n[f] = 0; }
+    HIPCHK(h, hipMemcpyAsync(h->fam_bytes_base, h->d.ctr, sizeof(h->fam_bytes_base), hipMemcpyDeviceToHost, h->s));
+    HIPCHK(h, hipStreamSynchronize(h->s));
+    return SWIMSIM_OK;
+}
+
+int swimsim_kernel_times(swimsim_t *h, const char **names, double *avg_ms, uint64_t *launches, double *alg_bytes,
+                         size_t cap, size_t *n) {
+    if (!h) return SWIMSIM_EINVAL;
+    drain_timing(h);
+    uint64_t c[32];
+    HIPCHK(h, hipMemcpyAsync(c, h->d.ctr, sizeof c, hipMemcpyDeviceToHost, h->s));
+    HIPCHK(h, hipStreamSynchronize(h->s));
+    const double merged = (double)(c[C_X_MERGED] - h->fam_bytes_base[C_X_MERGED]);
+    const double applied = (double)(c[C_X_APPLIED] - h->fam_bytes_base[C_X_APPLIED]);
+    const double issued = (double)(c[C_X_ISSUED] - h->fam_bytes_base[C_X_ISSUED]);
+    const double csrows = (double)(c[C_X_CS_ROWS] - h->fam_bytes_base[C_X_CS_ROWS]);
+    // algorithmic bytes: merge = 16 B record + 4 B row word read per processed
+    // change; + 4 B row word + 1 B counter + 16 B dissem/timer entry + 1 B timer state per applied change.
+    // checksum = 4 B member word per member per dirty row. issue = 16 B per record written (+ 16 B read).
+    const double merge_bytes = merged * 20.0 + applied * 22.0;
+    for (int f = 0; f < F_NFAM && (size_t)f < cap; f++) {
+        if (names) names[f] = kFamName[f];
+        if (avg_ms) avg_ms[f] = h->fam_n[f] ? h->fam_ms[f] / (double)h->fam_n[f] : 0.0;
+        if (launches) launches[f] = h->fam_n[f];
+        if (alg_bytes) {
+            double b = 0;
+            if (f == F_CHECKSUM) b = csrows * 4.0 * h->N;
+            if (f == F_ISSUE) b = issued * 32.0;
+            if (f == F_RECV) b = merge_bytes;  // merge volume is attributed to the receive waves (the bulk)
+            alg_bytes[f] = b;
+        }
+    }
+    if (n) *n = F_NFAM;
+    return SWIMSIM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,8 @@
+// swimsim_kernels.h — kernel entry points of the engine (defined in swimsim_kernels.hip)
+#pragma once
+#include "swimsim_device.h"
+
+namespace swimdev {
+void launch_checksum(const DS &d, const uint32_t *list, const uint32_t *count, uint32_t maxn, bool fast,
+                     hipStream_t s);
+}

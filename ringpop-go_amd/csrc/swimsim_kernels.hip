@@ -1,0 +1,1061 @@
+// swimsim_kernels.hip — gfx950 kernels of the SWIM protocol-round engine.
+//
+// Every kernel restates one phase of docs/ROUND_SEMANTICS.md. The reference functions they
+// replace are cited at each kernel (maniacs-ops/ringpop-go, package swim/). There is no MFMA:
+// nothing on this path is a dense contraction. The design is one 64-lane wave per observer
+// row for merges and buffer scans (the changes in one message are distinct members, so lanes
+// never conflict), and one lane per row for the FarmHash chain (it is sequential within a row).
+#include "swimsim_kernels.h"
+
+namespace swimdev {
+
+__device__ __forceinline__ int wsum(int v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+__device__ __forceinline__ uint32_t wmin(uint32_t v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, off, 64));
+    return v;
+}
+__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63; }
+__device__ __forceinline__ uint32_t wave_gid() { return (blockIdx.x * blockDim.x + threadIdx.x) >> 6; }
+__device__ __forceinline__ uint64_t lanemask_lt() { return (1ull << lane_id()) - 1ull; }
+
+__device__ __forceinline__ unsigned long long bcast64(unsigned long long v) {
+    uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, 0, 64), hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), 0, 64);
+    return ((unsigned long long)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint32_t timeout_rounds(const DS &d, uint32_t st) {
+    return st == ST_SUSPECT ? d.to_susp : st == ST_FAULTY ? d.to_faulty : d.to_tomb;
+}
+
+__device__ __forceinline__ bool reach(const DS &d, uint32_t a, uint32_t b) {
+    return d.live[a] && d.live[b] && d.part[a] == d.part[b];
+}
+
+// ---------------------------------------------------------------------------------------------
+// memberlist.Update for one change (memberlist.go:310-390, Apply 418-449) + handleChanges per
+// applied change (node.go:424-447: RecordChange, timer schedule/cancel). Row totals are folded
+// by wave_finalize (AdjustMaxPropagations, disseminator.go:75-97).
+// ---------------------------------------------------------------------------------------------
+struct MAcc {
+    int dping, ddc, napp, nref, nproc, evict;
+    __device__ MAcc() : dping(0), ddc(0), napp(0), nref(0), nproc(0), evict(0) {}
+};
+
+__device__ __forceinline__ void merge_change(const DS &d, uint32_t ol, uint32_t o, uint32_t m, uint32_t cst, uint32_t ce,
+                                             uint32_t csrc, uint32_t csinc, uint32_t now_e, uint32_t sched_r, MAcc &acc) {
+    const size_t idx = (size_t)ol * d.NP + m;
+    const uint32_t cur = d.mw[idx];
+    const uint32_t cur_st = cur & 7u;
+    uint32_t nst, ne, nsrc, nsinc;
+    acc.nproc++;
+    if (cur_st == ST_UNKNOWN) {                                    // memberlist.go:329-334
+        if (cst == ST_TOMB) return;                                // memberlist.go:424-426
+        nst = cst; ne = ce; nsrc = csrc; nsinc = csinc;
+    } else if (m == o && ce >= (cur >> 3) && (cst == ST_SUSPECT || cst == ST_FAULTY || cst == ST_TOMB)) {
+        nst = ST_ALIVE; ne = now_e; nsrc = o; nsinc = now_e;       // refute: memberlist.go:337-354
+        acc.nref++;
+    } else if (((ce << 3) | cst) > cur) {                          // nonLocalOverride: member.go:79-93
+        nst = cst; ne = ce; nsrc = csrc; nsinc = csinc;
+    } else {
+        return;
+    }
+    d.mw[idx] = (ne << 3) | nst;
+    if (m != o) acc.dping += (int)is_pingable(nst) - (int)is_pingable(cur_st);
+    // RecordChange (disseminator.go:223-227): entry = {p 0, source, source incarnation}
+    if (d.dp[idx] == DP_NONE) acc.ddc++;
+    d.dp[idx] = 0;
+    uint4 a = d.aux[idx];
+    a.x = nsrc;
+    a.y = nsinc;
+    atomicOr(&d.dblk[(size_t)ol * d.NBW + (m >> 12)], 1ull << ((m >> 6) & 63));
+    if (m != o) {                                                  // no timers for the local member
+        const uint8_t ts = d.tst[idx];
+        const uint32_t tstate = ts & 7u;
+        if (nst == ST_ALIVE || nst == ST_LEAVE) {
+            if (ts) d.tst[idx] = 0;                                // Cancel (state_transitions.go:163-176)
+        } else if (tstate != nst) {                                // same state: no-op (130-136)
+            const uint32_t dl = sched_r + timeout_rounds(d, nst);
+            d.tst[idx] = (uint8_t)nst;
+            a.z = dl;
+            a.w = ne;                                              // subject = the applied change
+            atomicMin(&d.tblk[(size_t)ol * d.NB + (m >> 6)], dl);
+            atomicMin(&d.tmin[ol], dl);
+        }
+    }
+    d.aux[idx] = a;
+    acc.napp++;
+}
+
+__device__ __forceinline__ void fold_row(const DS &d, uint32_t ol, int dping, int ddc, int napp, int nref, int evict) {
+    if (dping) d.ping[ol] += dping;
+    if (ddc) d.dcnt[ol] += ddc;
+    if (napp) {
+        d.maxp[ol] = (int32_t)d.pfactor * digits10(d.ping[ol]);    // AdjustMaxPropagations
+        atomicAdd(&d.ctr[C_APPLIED], (unsigned long long)napp);
+    }
+    if (napp || evict) d.dirty[ol] = 1;                            // ComputeChecksum pending
+    if (nref) atomicAdd(&d.ctr[C_REFUTES], (unsigned long long)nref);
+}
+
+__device__ __forceinline__ void wave_finalize(const DS &d, uint32_t ol, const MAcc &acc) {
+    const int dping = wsum(acc.dping), ddc = wsum(acc.ddc), napp = wsum(acc.napp), nref = wsum(acc.nref);
+    const int ev = wsum(acc.evict), np = wsum(acc.nproc);
+    if (lane_id() == 0) {
+        fold_row(d, ol, dping, ddc, napp, nref, ev);
+        if (np) atomicAdd(&d.ctr[C_X_MERGED], (unsigned long long)np);
+        if (napp) atomicAdd(&d.ctr[C_X_APPLIED], (unsigned long long)napp);
+    }
+    __threadfence_block();
+}
+
+// merge a whole message into row ol (wave-wide; the changes of one message are distinct members)
+__device__ void wave_merge_msg(const DS &d, uint32_t ol, uint32_t o, const MsgDesc &md, uint32_t now_e, uint32_t sched_r) {
+    MAcc acc;
+    if (md.kind == 0) {
+        const unsigned long long off = ((unsigned long long)md.off_hi << 32) | md.off_lo;
+        for (uint32_t i = lane_id(); i < md.len; i += 64) {
+            const uint4 r = d.pool[off + i];
+            merge_change(d, ol, o, r.x & 0xFFFFFFu, r.x >> 24, r.y, r.z, r.w, now_e, sched_r, acc);
+        }
+    } else if (md.kind == 1) {
+        const uint32_t slot = md.off_lo;
+        const uint4 meta = d.dense_meta[slot];
+        const uint32_t *snap = d.dense + (size_t)slot * d.NP;
+        for (uint32_t m = lane_id(); m < d.N; m += 64) {
+            const uint32_t w = snap[m];
+            const uint32_t st = w & 7u;
+            if (st == ST_UNKNOWN) continue;
+            merge_change(d, ol, o, m, st, w >> 3, meta.x, meta.y, now_e, sched_r, acc);
+        }
+    }
+    __threadfence_block();
+    wave_finalize(d, ol, acc);
+}
+
+// bumpPiggybackCounters over a sparse list (disseminator.go:135-149)
+__device__ void wave_bump(const DS &d, uint32_t ol, const MsgDesc &md) {
+    if (md.kind != 0) return;
+    const unsigned long long off = ((unsigned long long)md.off_hi << 32) | md.off_lo;
+    const int maxp = d.maxp[ol];
+    int del = 0;
+    for (uint32_t i = lane_id(); i < md.len; i += 64) {
+        const uint32_t m = d.pool[off + i].x & 0xFFFFFFu;
+        const size_t idx = (size_t)ol * d.NP + m;
+        const uint32_t p = d.dp[idx];
+        if (p == DP_NONE) continue;
+        if ((int)(p + 1) >= maxp) { d.dp[idx] = DP_NONE; del++; }
+        else d.dp[idx] = (uint8_t)(p + 1);
+    }
+    del = wsum(del);
+    if (lane_id() == 0 && del) d.dcnt[ol] -= del;
+    __threadfence_block();
+}
+
+__device__ __forceinline__ unsigned long long pool_alloc(const DS &d, uint32_t n) {
+    unsigned long long off = 0;
+    if (lane_id() == 0 && n) off = atomicAdd(d.pool_cur, (unsigned long long)n);
+    off = bcast64(off);
+    if (off + n > d.pool_cap) {
+        if (lane_id() == 0) atomicOr(d.err, E_POOL);
+        return ~0ull;
+    }
+    return off;
+}
+
+// issueChanges / IssueAsSender (disseminator.go:128-133,201-215): snapshot of every entry
+__device__ void wave_issue(const DS &d, uint32_t ol, MsgDesc &out) {
+    const uint32_t cnt = (uint32_t)d.dcnt[ol];
+    out.kind = 0; out.len = 0; out.off_lo = out.off_hi = 0;
+    if (cnt == 0) return;
+    const unsigned long long off = pool_alloc(d, cnt);
+    if (off == ~0ull) return;
+    uint32_t pos = 0;
+    for (uint32_t w = 0; w < d.NBW; w++) {
+        unsigned long long bits = d.dblk[(size_t)ol * d.NBW + w];
+        while (bits) {
+            const uint32_t b = __ffsll((long long)bits) - 1;
+            bits &= bits - 1;
+            const uint32_t m = ((w * 64 + b) << 6) + lane_id();
+            const size_t idx = (size_t)ol * d.NP + m;
+            const bool present = d.dp[idx] != DP_NONE;
+            const unsigned long long mask = __ballot(present);
+            if (!mask) {
+                if (lane_id() == 0) d.dblk[(size_t)ol * d.NBW + w] &= ~(1ull << b);
+                continue;
+            }
+            if (present) {
+                const uint32_t rank = __popcll(mask & lanemask_lt());
+                const uint32_t wv = d.mw[idx];
+                const uint32_t st = (wv & 7u) == ST_UNKNOWN ? ST_TOMB : (wv & 7u);   // evicted: (tombstone, inc)
+                const uint4 a = d.aux[idx];
+                if (pos + rank < cnt) d.pool[off + pos + rank] = make_uint4(m | (st << 24), wv >> 3, a.x, a.y);
+            }
+            pos += __popcll(mask);
+        }
+    }
+    if (pos != cnt && lane_id() == 0) atomicOr(d.err, E_COUNT);
+    out.off_lo = (uint32_t)off;
+    out.off_hi = (uint32_t)(off >> 32);
+    out.len = min(pos, cnt);
+}
+
+// IssueAsReceiver up to the full-sync decision (disseminator.go:156-199). Returns kept count.
+__device__ uint32_t wave_issue_recv(const DS &d, uint32_t ol, uint32_t sender, uint32_t sinc, MsgDesc &out) {
+    const uint32_t cnt = (uint32_t)d.dcnt[ol];
+    out.kind = 0; out.len = 0; out.off_lo = out.off_hi = 0;
+    if (cnt == 0) return 0;
+    const unsigned long long off = pool_alloc(d, cnt);
+    if (off == ~0ull) return 0;
+    const int maxp = d.maxp[ol];
+    uint32_t pos = 0;
+    int del = 0;
+    for (uint32_t w = 0; w < d.NBW; w++) {
+        unsigned long long bits = d.dblk[(size_t)ol * d.NBW + w];
+        while (bits) {
+            const uint32_t b = __ffsll((long long)bits) - 1;
+            bits &= bits - 1;
+            const uint32_t m = ((w * 64 + b) << 6) + lane_id();
+            const size_t idx = (size_t)ol * d.NP + m;
+            const uint32_t p = d.dp[idx];
+            const bool present = p != DP_NONE;
+            uint4 a = make_uint4(0, 0, 0, 0);
+            if (present) a = d.aux[idx];
+            const bool keep = present && !(a.x == sender && a.y == sinc);   // filterChangesFromSender
+            const unsigned long long kmask = __ballot(keep);
+            bool remain = present;
+            if (keep) {
+                const uint32_t rank = __popcll(kmask & lanemask_lt());
+                const uint32_t wv = d.mw[idx];
+                const uint32_t st = (wv & 7u) == ST_UNKNOWN ? ST_TOMB : (wv & 7u);
+                d.pool[off + pos + rank] = make_uint4(m | (st << 24), wv >> 3, a.x, a.y);
+                if ((int)(p + 1) >= maxp) { d.dp[idx] = DP_NONE; del++; remain = false; }   // bump
+                else d.dp[idx] = (uint8_t)(p + 1);
+            }
+            pos += __popcll(kmask);
+            if (!__ballot(remain) && lane_id() == 0) d.dblk[(size_t)ol * d.NBW + w] &= ~(1ull << b);
+        }
+    }
+    del = wsum(del);
+    if (lane_id() == 0 && del) d.dcnt[ol] -= del;
+    __threadfence_block();
+    out.off_lo = (uint32_t)off;
+    out.off_hi = (uint32_t)(off >> 32);
+    out.len = pos;
+    return pos;
+}
+
+// MembershipAsChanges (disseminator.go:107-123) as a dense snapshot of row ol
+__device__ bool wave_snapshot(const DS &d, uint32_t ol, uint32_t o, MsgDesc &out) {
+    uint32_t slot = 0;
+    if (lane_id() == 0) slot = atomicAdd(d.dense_cur, 1u);
+    slot = (uint32_t)__shfl((int)slot, 0, 64);
+    out.kind = 2; out.len = 0; out.off_lo = out.off_hi = 0;
+    if (slot >= d.dense_cap) {
+        if (lane_id() == 0) atomicOr(d.err, E_DENSE);
+        return false;
+    }
+    const uint4 *src = (const uint4 *)(d.mw + (size_t)ol * d.NP);
+    uint4 *dst = (uint4 *)(d.dense + (size_t)slot * d.NP);
+    int known = 0;
+    for (uint32_t i = lane_id(); i < d.NP / 4; i += 64) {
+        const uint4 v = src[i];
+        dst[i] = v;
+        known += ((v.x & 7u) != ST_UNKNOWN) + ((v.y & 7u) != ST_UNKNOWN) + ((v.z & 7u) != ST_UNKNOWN) + ((v.w & 7u) != ST_UNKNOWN);
+    }
+    known = wsum(known);
+    if (lane_id() == 0) d.dense_meta[slot] = make_uint4(o, d.mw[(size_t)ol * d.NP + o] >> 3, (uint32_t)known, 0);
+    out.kind = 1; out.off_lo = slot; out.len = (uint32_t)known;
+    return true;
+}
+
+// ---------------------------------------------------------------------------------------------
+// initialisation
+// ---------------------------------------------------------------------------------------------
+__global__ void k_init_rows(DS d, int mode, uint32_t e0) {
+    const uint32_t ol = wave_gid();
+    if (ol >= d.NL) return;
+    const uint32_t o = d.lo + ol;
+    for (uint32_t m = lane_id(); m < d.NP; m += 64) {
+        const size_t idx = (size_t)ol * d.NP + m;
+        uint32_t w = ST_UNKNOWN;
+        if (m < d.N && (mode == 0 || m == o)) w = (e0 << 3) | ST_ALIVE;
+        d.mw[idx] = w;
+        d.dp[idx] = DP_NONE;
+        d.tst[idx] = 0;
+        d.aux[idx] = make_uint4(0, 0, NO_DEADLINE, 0);
+    }
+    for (uint32_t b = lane_id(); b < d.NB; b += 64) d.tblk[(size_t)ol * d.NB + b] = NO_DEADLINE;
+    for (uint32_t b = lane_id(); b < d.NBW; b += 64) d.dblk[(size_t)ol * d.NBW + b] = 0;
+    if (lane_id() == 0) {
+        const int32_t p = mode == 0 ? (int32_t)d.N - 1 : 0;
+        d.ping[ol] = p;
+        d.maxp[ol] = mode == 0 ? (int32_t)d.pfactor * digits10(p) : (int32_t)d.pfactor;
+        d.dcnt[ol] = 0;
+        d.dirty[ol] = 1;
+        d.cs[ol] = 0;
+        d.it_idx[ol] = -1;
+        d.it_ep[ol] = 0;
+        d.tmin[ol] = NO_DEADLINE;
+        d.njobs[ol] = 0;
+    }
+}
+
+// recount pingable/changes of one row after raw writes (NumPingableMembers, memberlist.go:188-198)
+__global__ void k_recount(DS d, uint32_t ol) {
+    const uint32_t o = d.lo + ol;
+    int p = 0, c = 0;
+    for (uint32_t m = lane_id(); m < d.N; m += 64) {
+        const size_t idx = (size_t)ol * d.NP + m;
+        if (m != o && is_pingable(d.mw[idx] & 7u)) p++;
+        if (d.dp[idx] != DP_NONE) c++;
+    }
+    p = wsum(p);
+    c = wsum(c);
+    if (lane_id() == 0) { d.ping[ol] = p; d.dcnt[ol] = c; d.dirty[ol] = 1; }
+}
+
+__global__ void k_clear_changes(DS d, uint32_t ol) {
+    for (uint32_t m = threadIdx.x; m < d.NP; m += blockDim.x) d.dp[(size_t)ol * d.NP + m] = DP_NONE;
+    for (uint32_t b = threadIdx.x; b < d.NBW; b += blockDim.x) d.dblk[(size_t)ol * d.NBW + b] = 0;
+    if (threadIdx.x == 0) d.dcnt[ol] = 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// phase E: host events, applied in order by one thread (few per round)
+// ---------------------------------------------------------------------------------------------
+__device__ void thread_make_change(const DS &d, uint32_t ol, uint32_t o, uint32_t m, uint32_t e, uint32_t st, uint32_t r) {
+    MAcc acc;
+    const uint32_t self_e = d.mw[(size_t)ol * d.NP + o] >> 3;   // MakeChange: SourceIncarnation = local inc
+    merge_change(d, ol, o, m, st, e, o, self_e, r, r, acc);
+    fold_row(d, ol, acc.dping, acc.ddc, acc.napp, acc.nref, 0);
+}
+
+__global__ void k_events(DS d, const uint4 *ev, uint32_t nev, uint32_t r, uint32_t *applied_out) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    for (uint32_t i = 0; i < nev; i++) {
+        const uint4 e = ev[i];   // {kind, observer, member, e | status << 29 | label}
+        const uint32_t kind = e.x, o = e.y;
+        if (o < d.lo || o >= d.lo + d.NL) continue;
+        const uint32_t ol = o - d.lo;
+        const unsigned long long before = d.ctr[C_APPLIED];
+        switch (kind) {
+        case 1:  // MakeChange(o, member, e, status)
+            thread_make_change(d, ol, o, e.z, e.w & 0x1FFFFFFFu, e.w >> 29, r);
+            break;
+        case 2:  // Reincarnate: MakeAlive(self, now) (memberlist.go:234-236)
+            thread_make_change(d, ol, o, o, r, ST_ALIVE, r);
+            break;
+        case 3:  // admin leave: MakeLeave(self, local inc) (handlers.go:145-148)
+            thread_make_change(d, ol, o, o, d.mw[(size_t)ol * d.NP + o] >> 3, ST_LEAVE, r);
+            break;
+        case 4:  // reap: faulty → tombstone (handlers.go:154-163)
+            for (uint32_t m = 0; m < d.N; m++) {
+                const uint32_t w = d.mw[(size_t)ol * d.NP + m];
+                if ((w & 7u) == ST_FAULTY) thread_make_change(d, ol, o, m, w >> 3, ST_TOMB, r);
+            }
+            break;
+        }
+        if (applied_out) applied_out[i] = (uint32_t)(d.ctr[C_APPLIED] - before);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// phase T: timers (state_transitions.go:90-160 on the round clock; Mock.Add fires in deadline
+// order with now = deadline, so a follow-up schedule is based at the fired deadline)
+// ---------------------------------------------------------------------------------------------
+__global__ void k_timers(DS d, uint32_t r) {
+    const uint32_t ol = wave_gid();
+    if (ol >= d.NL) return;
+    const uint32_t o = d.lo + ol;
+    if (!d.live[o] || d.tmin[ol] > r) return;
+    const uint32_t self_e = d.mw[(size_t)ol * d.NP + o] >> 3;
+    MAcc acc;
+    uint32_t newmin = NO_DEADLINE;
+    int fired = 0;
+    for (uint32_t b = 0; b < d.NB; b++) {
+        const uint32_t bm = d.tblk[(size_t)ol * d.NB + b];
+        if (bm > r) { newmin = min(newmin, bm); continue; }
+        const uint32_t m = (b << 6) + lane_id();
+        const size_t idx = (size_t)ol * d.NP + m;
+        const uint8_t ts = d.tst[idx];
+        const uint32_t state = ts & 7u;
+        uint4 a = d.aux[idx];
+        if (state && !(ts & 0x80) && a.z <= r) {
+            d.tst[idx] = ts | 0x80;                                 // fired; the entry stays
+            fired++;
+            if (state == ST_SUSPECT) merge_change(d, ol, o, m, ST_FAULTY, a.w, o, self_e, r, a.z, acc);  // MakeFaulty
+            else if (state == ST_FAULTY) merge_change(d, ol, o, m, ST_TOMB, a.w, o, self_e, r, a.z, acc); // MakeTombstone
+            else {                                                  // Evict (memberlist.go:271-279)
+                const uint32_t w = d.mw[idx];
+                if ((w & 7u) != ST_UNKNOWN && m != o) {
+                    if (is_pingable(w & 7u)) acc.dping--;
+                    d.mw[idx] = (w & ~7u) | ST_UNKNOWN;
+                    acc.evict++;
+                }
+            }
+            a = d.aux[idx];
+        }
+        const uint8_t ts2 = d.tst[idx];
+        const uint32_t v = ((ts2 & 7u) && !(ts2 & 0x80)) ? a.z : NO_DEADLINE;
+        const uint32_t bmin = wmin(v);
+        if (lane_id() == 0) d.tblk[(size_t)ol * d.NB + b] = bmin;
+        newmin = min(newmin, bmin);
+    }
+    if (lane_id() == 0) d.tmin[ol] = newmin;
+    fired = wsum(fired);
+    if (lane_id() == 0 && fired) atomicAdd(&d.ctr[C_TIMERS_FIRED], (unsigned long long)fired);
+    __threadfence_block();
+    wave_finalize(d, ol, acc);
+}
+
+// ---------------------------------------------------------------------------------------------
+// phase S: memberlistIter.Next (memberlist_iter.go:50-72) on Philox permutations
+// ---------------------------------------------------------------------------------------------
+__global__ void k_select(DS d, int32_t *tgt, uint32_t *exh_list, uint32_t *exh_cnt) {
+    const uint32_t ol = blockIdx.x * blockDim.x + threadIdx.x;
+    if (ol >= d.NL) return;
+    const uint32_t o = d.lo + ol;
+    int32_t target = -1;
+    if (d.live[o]) {
+        if (d.ping[ol] <= 0) {
+            exh_list[atomicAdd(exh_cnt, 1u)] = ol;                // walks every member: rare path
+        } else {
+            int32_t idx = d.it_idx[ol];
+            uint32_t ep = d.it_ep[ol];
+            Feistel f;
+            f.init(d.seed, o, ep, d.N);
+            const uint32_t *row = d.mw + (size_t)ol * d.NP;
+            for (uint32_t guard = 0; guard < 4 * d.N + 8; guard++) {
+                idx++;
+                if (idx >= (int32_t)d.N) { idx = 0; ep++; f.init(d.seed, o, ep, d.N); }
+                const uint32_t m = f.perm((uint32_t)idx, d.N);
+                const uint32_t st = row[m] & 7u;
+                if (st == ST_UNKNOWN) continue;
+                if (m != o && is_pingable(st)) { target = (int32_t)m; break; }
+            }
+            if (target < 0) atomicOr(d.err, E_ITER);
+            d.it_idx[ol] = idx;
+            d.it_ep[ol] = ep;
+        }
+    }
+    tgt[ol] = target;
+}
+
+// no pingable member: the reference loop visits until every known member was seen, then
+// returns none; replay it literally with a visited bitmap (one thread per exhausted observer)
+__global__ void k_select_exhaust(DS d, const uint32_t *exh_list, const uint32_t *exh_cnt, uint32_t *scratch) {
+    const uint32_t cnt = *exh_cnt;
+    uint32_t *vis = scratch + (size_t)blockIdx.x * (d.NP / 32);
+    for (uint32_t q = blockIdx.x; q < cnt; q += gridDim.x) {
+        const uint32_t ol = exh_list[q], o = d.lo + ol;
+        for (uint32_t i = threadIdx.x; i < d.NP / 32; i += blockDim.x) vis[i] = 0;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const uint32_t *row = d.mw + (size_t)ol * d.NP;
+            uint32_t known = 0;
+            for (uint32_t m = 0; m < d.N; m++) known += (row[m] & 7u) != ST_UNKNOWN;
+            int32_t idx = d.it_idx[ol];
+            uint32_t ep = d.it_ep[ol], nvis = 0;
+            Feistel f;
+            f.init(d.seed, o, ep, d.N);
+            uint64_t guard = 0;
+            while (nvis < known && guard++ < 8ull * d.N + 8) {
+                idx++;
+                if (idx >= (int32_t)d.N) { idx = 0; ep++; f.init(d.seed, o, ep, d.N); }
+                const uint32_t m = f.perm((uint32_t)idx, d.N);
+                if ((row[m] & 7u) == ST_UNKNOWN) continue;
+                if (!(vis[m >> 5] & (1u << (m & 31)))) { vis[m >> 5] |= 1u << (m & 31); nvis++; }
+            }
+            d.it_idx[ol] = idx;
+            d.it_ep[ol] = ep;
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// lists and snapshots
+// ---------------------------------------------------------------------------------------------
+// mode 0: dirty rows; 1: dirty rows of live senders with a target; 2: dirty rows of failed senders
+__global__ void k_list(DS d, int mode, const int32_t *tgt, const uint8_t *failed, uint32_t *list, uint32_t *cnt) {
+    const uint32_t ol = blockIdx.x * blockDim.x + threadIdx.x;
+    if (ol >= d.NL) return;
+    bool take = d.dirty[ol] != 0;
+    if (mode == 1) take = take && tgt[ol] >= 0;
+    if (mode == 2) take = take && failed[ol];
+    if (take) list[atomicAdd(cnt, 1u)] = ol;
+}
+
+__global__ void k_list_one(uint32_t *list, uint32_t *cnt, uint32_t ol, const DS d) {
+    if (threadIdx.x == 0) { *cnt = d.dirty[ol] ? 1u : 0u; list[0] = ol; }
+}
+
+// phase I (ping_sender.go:43-66) / Q1: snapshot S_o, C_o, I_o for the senders of this phase
+__global__ void k_issue(DS d, int mode, const int32_t *tgt, const uint8_t *failed, MsgDesc *sdesc, uint32_t *sI,
+                        uint32_t *sC) {
+    const uint32_t ol = wave_gid();
+    if (ol >= d.NL) return;
+    if (mode == 0 && tgt[ol] < 0) return;
+    if (mode == 1 && !failed[ol]) return;
+    const uint32_t o = d.lo + ol;
+    MsgDesc md;
+    wave_issue(d, ol, md);
+    if (lane_id() == 0) {
+        sdesc[ol] = md;
+        sI[ol] = d.mw[(size_t)ol * d.NP + o] >> 3;
+        sC[ol] = d.cs[ol];
+        if (mode == 0) {
+            atomicAdd(&d.ctr[C_PINGS], 1ull);
+            atomicAdd(&d.ctr[C_MSG_CHANGES], (unsigned long long)md.len);   // counted per helper call in Q2
+        }
+        atomicAdd(&d.ctr[C_X_ISSUED], (unsigned long long)md.len);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// phase D / Q2 inbox construction (sorted by receiver; ascending sender inside a receiver)
+// ---------------------------------------------------------------------------------------------
+__global__ void k_pairs_direct(DS d, const int32_t *tgt, uint32_t *keys, uint32_t *vals, uint8_t *failed,
+                               uint32_t *info) {
+    const uint32_t ol = blockIdx.x * blockDim.x + threadIdx.x;
+    if (ol >= d.NL) return;
+    const uint32_t o = d.lo + ol;
+    const int32_t t = tgt[ol];
+    uint32_t key = d.N;
+    uint8_t f = 0;
+    if (t >= 0) {
+        if (reach(d, o, (uint32_t)t)) key = (uint32_t)t;
+        else { f = 1; atomicAdd(&info[2], 1u); }
+    }
+    keys[ol] = key;
+    vals[ol] = o;
+    failed[ol] = f;
+}
+
+// RandomPingableMembers(k, {target}) (memberlist.go:201-219) with the Philox draw rule
+__global__ void k_helpers(DS d, const int32_t *tgt, const uint8_t *failed, uint32_t *H, uint32_t *nh, uint32_t r) {
+    const uint32_t ol = blockIdx.x * blockDim.x + threadIdx.x;
+    if (ol >= d.NL) return;
+    nh[ol] = 0;
+    if (!failed[ol]) return;
+    const uint32_t o = d.lo + ol, t = (uint32_t)tgt[ol], K = d.K;
+    const uint32_t *row = d.mw + (size_t)ol * d.NP;
+    atomicAdd(&d.ctr[C_PINGREQS], 1ull);
+    const int32_t eligible = d.ping[ol] - (is_pingable(row[t] & 7u) ? 1 : 0);
+    const uint32_t need = (uint32_t)max(0, min((int32_t)K, eligible));
+    uint32_t got = 0, h[8];
+    U4 blk = U4{0, 0, 0, 0};
+    for (uint32_t i = 0; i < 64 && got < need; i++) {
+        if ((i & 3) == 0) blk = philox10(r, o, 2u, i >> 2, d.seed);
+        const uint32_t c = mulhi_n(pick(blk, i), d.N);
+        if (c == o || c == t || !is_pingable(row[c] & 7u)) continue;
+        bool dup = false;
+        for (uint32_t q = 0; q < got; q++) dup |= h[q] == c;
+        if (!dup) h[got++] = c;
+    }
+    if (got < need) {
+        const uint32_t start = mulhi_n(philox10(r, o, 2u, 16u, d.seed).x, d.N);
+        for (uint32_t q = 0; q < d.N && got < need; q++) {
+            uint32_t c = start + q;
+            if (c >= d.N) c -= d.N;
+            if (c == o || c == t || !is_pingable(row[c] & 7u)) continue;
+            bool dup = false;
+            for (uint32_t z = 0; z < got; z++) dup |= h[z] == c;
+            if (!dup) h[got++] = c;
+        }
+    }
+    for (uint32_t q = 0; q < got; q++) H[(size_t)ol * K + q] = h[q];
+    nh[ol] = got;
+}
+
+__global__ void k_pairs_helpers(DS d, const uint8_t *failed, const uint32_t *H, const uint32_t *nh, uint32_t *keys,
+                                uint32_t *vals) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t K = d.K;
+    if (i >= d.NL * K) return;
+    const uint32_t ol = i / K, q = i % K, o = d.lo + ol;
+    uint32_t key = d.N;
+    if (failed[ol] && q < nh[ol]) {
+        const uint32_t h = H[i];
+        if (reach(d, o, h)) key = h;
+    }
+    keys[i] = key;
+    vals[i] = o * K + q;
+}
+
+// runs: number of receivers (excluding the sentinel) and the longest inbox
+__global__ void k_runs_info(const uint32_t *ukeys, const uint32_t *counts, const uint32_t *nruns, uint32_t N,
+                            uint32_t *info) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= *nruns) return;
+    if (ukeys[i] == N) return;
+    atomicMax(&info[1], counts[i]);
+    atomicAdd(&info[0], 1u);
+}
+
+// ---------------------------------------------------------------------------------------------
+// phase D waves / Q2 waves: receiver merges the w-th message of its inbox, then IssueAsReceiver
+// (ping_handler.go:25-58 / ping_request_handler.go:32-76)
+// ---------------------------------------------------------------------------------------------
+struct RecvArgs {
+    const uint32_t *ukeys, *counts, *offs, *vals;   // run-length encoded sorted inbox
+    uint32_t nruns_max;
+    uint32_t w;                                     // wave index
+    int phase;                                      // 0: direct ping (phase D), 1: ping-req (Q2)
+    const MsgDesc *sdesc;                           // sender snapshots (by sender row)
+    const uint32_t *sI, *sC;
+    MsgDesc *rdesc;                                 // responses (by sender row / (row, slot))
+    uint4 *defer;
+    uint32_t *defer_cnt;
+    uint32_t r;
+};
+
+__device__ void recv_one(const DS &d, const RecvArgs &a, uint32_t j, uint32_t sender_row, uint32_t resp_idx) {
+    const uint32_t ol = j - d.lo;
+    const uint32_t sender = d.lo + sender_row;
+    wave_merge_msg(d, ol, j, a.sdesc[sender_row], a.r, a.r);
+    MsgDesc resp;
+    const uint32_t kept = wave_issue_recv(d, ol, sender, a.sI[sender_row], resp);
+    if (kept == 0) {
+        if (d.dirty[ol]) {                                          // checksum needed first
+            if (lane_id() == 0) a.defer[atomicAdd(a.defer_cnt, 1u)] = make_uint4(ol, resp_idx, sender, a.sC[sender_row]);
+            resp.kind = 2;
+        } else if (d.cs[ol] != a.sC[sender_row]) {                  // full sync
+            wave_snapshot(d, ol, j, resp);
+            if (lane_id() == 0) {
+                if (a.phase == 0) {
+                    atomicAdd(&d.ctr[C_FULL_SYNCS], 1ull);
+                    if (d.njobs[ol] < d.maxjobs) d.jobs[(size_t)ol * d.maxjobs + d.njobs[ol]++] = sender;
+                    else atomicAdd(&d.ctr[C_RFS_OMITTED], 1ull);
+                } else {
+                    atomicAdd(&d.ctr[C_FULL_SYNCS_PINGREQ], 1ull);
+                }
+            }
+        }
+    }
+    if (lane_id() == 0) {
+        a.rdesc[resp_idx] = resp;
+        if (resp.kind != 2) atomicAdd(&d.ctr[C_MSG_CHANGES], (unsigned long long)resp.len);
+        if (a.phase == 1) atomicAdd(&d.ctr[C_HELPER_CALLS], 1ull);
+        atomicAdd(&d.ctr[C_MSG_CHANGES], (unsigned long long)a.sdesc[sender_row].len * (a.phase == 1));
+    }
+}
+
+__global__ void k_recv(DS d, RecvArgs a) {
+    const uint32_t u = wave_gid();
+    if (u >= a.nruns_max) return;
+    const uint32_t key = a.ukeys[u];
+    if (key >= d.N || a.counts[u] <= a.w) return;
+    const uint32_t v = a.vals[a.offs[u] + a.w];
+    if (a.phase == 0) recv_one(d, a, key, v - d.lo, v - d.lo);
+    else {
+        const uint32_t o = v / d.K, q = v % d.K;
+        recv_one(d, a, key, o - d.lo, (o - d.lo) * d.K + q);
+    }
+}
+
+// second half of IssueAsReceiver for receivers whose checksum had to be recomputed first
+__global__ void k_recv_finish(DS d, const uint4 *defer, const uint32_t *defer_cnt, MsgDesc *rdesc, int phase) {
+    const uint32_t i = wave_gid();
+    if (i >= *defer_cnt) return;
+    const uint4 e = defer[i];
+    const uint32_t ol = e.x;
+    MsgDesc resp;
+    resp.kind = 0; resp.len = 0; resp.off_lo = resp.off_hi = 0;
+    if (d.cs[ol] != e.w) {
+        wave_snapshot(d, ol, d.lo + ol, resp);
+        if (lane_id() == 0) {
+            if (phase != 1) {
+                atomicAdd(&d.ctr[C_FULL_SYNCS], 1ull);
+                if (d.njobs[ol] < d.maxjobs) d.jobs[(size_t)ol * d.maxjobs + d.njobs[ol]++] = e.z;
+                else atomicAdd(&d.ctr[C_RFS_OMITTED], 1ull);
+            } else {
+                atomicAdd(&d.ctr[C_FULL_SYNCS_PINGREQ], 1ull);
+            }
+        }
+    }
+    if (lane_id() == 0) {
+        rdesc[e.y] = resp;
+        if (phase != 2) atomicAdd(&d.ctr[C_MSG_CHANGES], (unsigned long long)resp.len);
+    }
+}
+
+// phase R: sender bumps its piggyback counters and merges the response (ping_sender.go:52, node.go:488)
+__global__ void k_resp(DS d, const int32_t *tgt, const uint8_t *failed, const MsgDesc *sdesc, const MsgDesc *rdesc,
+                       uint32_t r) {
+    const uint32_t ol = wave_gid();
+    if (ol >= d.NL) return;
+    if (tgt[ol] < 0 || failed[ol]) return;
+    const uint32_t o = d.lo + ol;
+    wave_bump(d, ol, sdesc[ol]);
+    wave_merge_msg(d, ol, o, rdesc[ol], r, r);
+    if (lane_id() == 0) atomicAdd(&d.ctr[C_PINGS_OK], 1ull);
+}
+
+// Q3: resolve indirect pings (ping_request_sender.go:65-138, node.go:494-509)
+__global__ void k_resolve(DS d, const int32_t *tgt, const uint8_t *failed, const uint32_t *H, const uint32_t *nh,
+                          const MsgDesc *sdesc2, const MsgDesc *rdesc2, uint32_t r) {
+    const uint32_t ol = wave_gid();
+    if (ol >= d.NL || !failed[ol]) return;
+    const uint32_t o = d.lo + ol, K = d.K;
+    uint32_t errs = 0;
+    for (uint32_t q = 0; q < nh[ol]; q++) {
+        const uint32_t h = H[(size_t)ol * K + q];
+        if (!reach(d, o, h)) {
+            errs++;
+            wave_bump(d, ol, sdesc2[ol]);                           // bump only on error (105-106)
+        } else {
+            wave_merge_msg(d, ol, o, rdesc2[(size_t)ol * K + q], r, r);
+        }
+    }
+    if (lane_id() == 0) {
+        if (errs) atomicAdd(&d.ctr[C_HELPER_ERRORS], (unsigned long long)errs);
+        if (errs == K) {
+            atomicAdd(&d.ctr[C_INCONCLUSIVE], 1ull);
+        } else {
+            atomicAdd(&d.ctr[C_SUSPECT_DECL], 1ull);
+            const uint32_t t = (uint32_t)tgt[ol];
+            const uint32_t te = d.mw[(size_t)ol * d.NP + t] >> 3;      // member.Incarnation read now (node.go:508)
+            thread_make_change(d, ol, o, t, te, ST_SUSPECT, r);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// phase F: reverse full syncs (disseminator.go:257-304); sources are snapshotted first
+// ---------------------------------------------------------------------------------------------
+__global__ void k_jobs_mark(DS d, uint8_t *need) {
+    const uint32_t ol = blockIdx.x * blockDim.x + threadIdx.x;
+    if (ol >= d.NL) return;
+    for (uint32_t q = 0; q < d.njobs[ol]; q++) need[d.jobs[(size_t)ol * d.maxjobs + q] - d.lo] = 1;
+}
+
+__global__ void k_jobs_snap(DS d, const uint8_t *need, MsgDesc *snapdesc) {
+    const uint32_t ol = wave_gid();
+    if (ol >= d.NL || !need[ol]) return;
+    MsgDesc md;
+    wave_snapshot(d, ol, d.lo + ol, md);
+    if (lane_id() == 0) snapdesc[ol] = md;
+}
+
+__global__ void k_jobs_merge(DS d, uint32_t q, const MsgDesc *snapdesc, uint32_t r) {
+    const uint32_t ol = wave_gid();
+    if (ol >= d.NL || d.njobs[ol] <= q) return;
+    const uint32_t src = d.jobs[(size_t)ol * d.maxjobs + q];
+    wave_merge_msg(d, ol, d.lo + ol, snapdesc[src - d.lo], r, r);
+    if (lane_id() == 0) atomicAdd(&d.ctr[C_RFS_DONE], 1ull);
+}
+
+__global__ void k_jobs_reset(DS d, uint8_t *need) {
+    const uint32_t ol = blockIdx.x * blockDim.x + threadIdx.x;
+    if (ol >= d.NL) return;
+    d.njobs[ol] = 0;
+    need[ol] = 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// phase C: checksum (memberlist.go:83-128) — one lane per row, FarmHash-32 mk chain over the
+// byte stream addr ‖ status ‖ decimal(inc) ‖ ';' of every non-tombstone member in index order
+// (fixed-width ascending addresses make the sort order == index order)
+// ---------------------------------------------------------------------------------------------
+template <int W, int RW>
+__device__ __forceinline__ void build_rec(uint32_t (&R)[RW], const uint32_t *A, const uint32_t (&T)[6]) {
+    constexpr int wW = W / 4, bW = W % 4;
+#pragma unroll
+    for (int i = 0; i < RW; i++) {
+        uint32_t v;
+        if (i < wW) {
+            v = A[i];
+        } else if (bW == 0) {
+            const int k = i - wW;
+            v = k < 6 ? T[k] : 0u;
+        } else if (i == wW) {
+            v = (A[wW] & ((1u << (8 * bW)) - 1u)) | (T[0] << (8 * bW));
+        } else {
+            const int k = i - wW - 1;
+            const uint32_t lo = k < 6 ? (T[k] >> (32 - 8 * bW)) : 0u;
+            const uint32_t hi = (k + 1) < 6 ? (T[k + 1] << (8 * bW)) : 0u;
+            v = lo | hi;
+        }
+        R[i] = v;
+    }
+}
+
+__device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t sh_bits) {
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> sh_bits);
+}
+
+template <int W, int RW, int NBM>
+__global__ void __launch_bounds__(256) k_checksum(DS d, const uint32_t *list, const uint32_t *count) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= *count) return;
+    const uint32_t ol = list[i];
+    const uint32_t *row = d.mw + (size_t)ol * d.NP;
+    const uint32_t *tail = d.tailw;
+    const uint32_t ecap = d.ecap;
+    // pass 1: total length and the last included member
+    uint32_t len = 0;
+    int32_t last = -1;
+    bool bad_e = false;
+    for (uint32_t m = 0; m < d.N; m += 4) {
+        const uint4 w4 = *(const uint4 *)(row + m);
+        const uint32_t ws[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t st = ws[k] & 7u, e = ws[k] >> 3;
+            if (st < 4u && m + k < d.N) {
+                bad_e |= e >= ecap;
+                const uint32_t te = e < ecap ? e : 0u;
+                len += W + tail[((size_t)te * 4 + st) * 8 + 6];
+                last = (int32_t)(m + k);
+            }
+        }
+    }
+    if (bad_e) atomicOr(d.err, E_ECAP);
+    if (len <= 24 || last < 0) {
+        atomicOr(d.err, E_SHORT);
+        d.cs[ol] = 0;
+        d.dirty[ol] = 0;
+        return;
+    }
+    // prologue: the last 20 bytes come from the last record
+    FH fh;
+    {
+        const uint32_t w = row[last], st = w & 7u, e = min(w >> 3, ecap - 1);
+        const uint32_t *tp = tail + ((size_t)e * 4 + st) * 8;
+        uint32_t T[6] = {tp[0], tp[1], tp[2], tp[3], tp[4], tp[5]};
+        uint32_t R[RW + 1];
+        uint32_t Rr[RW];
+        build_rec<W, RW>(Rr, d.addrw + (size_t)last * 6, T);
+#pragma unroll
+        for (int k = 0; k < RW; k++) R[k] = Rr[k];
+        R[RW] = 0;
+        const uint32_t L = W + tp[6], q = L - 20, qw = q >> 2, qb = (q & 3u) * 8u;
+        uint32_t t[5];
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            uint32_t lo = 0, hi = 0;
+#pragma unroll
+            for (int s = 0; s <= RW; s++) {
+                lo = ((uint32_t)s == qw + k) ? R[s] : lo;
+                hi = ((uint32_t)s == qw + k + 1) ? R[s] : hi;
+            }
+            t[k] = funnel(hi, lo, qb);
+        }
+        fh.init(len, t[0], t[1], t[2], t[3], t[4]);
+    }
+    const uint32_t iters = (len - 1) / 20;
+    uint32_t done = 0, c = 0;
+    uint32_t P0 = 0, P1 = 0, P2 = 0, P3 = 0, P4 = 0;
+    constexpr int NS = (RW + 6 > 5 * NBM + 5) ? RW + 6 : 5 * NBM + 5;
+    for (uint32_t m = 0; m < d.N; m += 4) {
+        const uint4 w4 = *(const uint4 *)(row + m);
+        const uint32_t ws[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t mm = m + k;
+            const uint32_t st = ws[k] & 7u, e = ws[k] >> 3;
+            const bool inc = st < 4u && mm < d.N;
+            const uint32_t te = (e < ecap) ? e : 0u;
+            const uint32_t *tp = tail + ((size_t)te * 4 + (st & 3u)) * 8;
+            const uint4 ta = *(const uint4 *)tp;
+            const uint4 tb = *(const uint4 *)(tp + 4);
+            uint32_t T[6] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y};
+            const uint32_t L = inc ? W + tb.z : 0u;
+            uint32_t R[RW];
+            build_rec<W, RW>(R, d.addrw + (size_t)(mm < d.N ? mm : 0) * 6, T);
+            if (!inc) {
+#pragma unroll
+                for (int z = 0; z < RW; z++) R[z] = 0;
+            }
+            // byte shift by c & 3
+            const uint32_t cb = (c & 3u) * 8u;
+            uint32_t S[NS];
+            S[0] = funnel(R[0], 0u, 32u - cb);
+#pragma unroll
+            for (int z = 1; z < RW; z++) S[z] = funnel(R[z], R[z - 1], 32u - cb);
+            S[RW] = funnel(0u, R[RW - 1], 32u - cb);
+#pragma unroll
+            for (int z = RW + 1; z < NS; z++) S[z] = 0u;
+            // word shift by c >> 2 (0..4): 3-stage barrel shifter
+            const uint32_t cw = c >> 2;
+#pragma unroll
+            for (int z = NS - 1; z >= 0; z--) S[z] = (cw & 1u) ? (z >= 1 ? S[z - 1] : 0u) : S[z];
+#pragma unroll
+            for (int z = NS - 1; z >= 0; z--) S[z] = (cw & 2u) ? (z >= 2 ? S[z - 2] : 0u) : S[z];
+#pragma unroll
+            for (int z = NS - 1; z >= 0; z--) S[z] = (cw & 4u) ? (z >= 4 ? S[z - 4] : 0u) : S[z];
+            S[0] |= P0; S[1] |= P1; S[2] |= P2; S[3] |= P3; S[4] |= P4;
+            const uint32_t T2 = c + L;
+            const uint32_t nb = T2 / 20u;
+#pragma unroll
+            for (int bi = 0; bi < NBM; bi++) {
+                if ((uint32_t)bi < nb && done < iters) {
+                    fh.block(S[5 * bi], S[5 * bi + 1], S[5 * bi + 2], S[5 * bi + 3], S[5 * bi + 4]);
+                    done++;
+                }
+            }
+            uint32_t Q0 = S[0], Q1 = S[1], Q2 = S[2], Q3 = S[3], Q4 = S[4];
+#pragma unroll
+            for (int bi = 1; bi <= NBM; bi++) {
+                const bool sel = nb == (uint32_t)bi;
+                Q0 = sel ? S[5 * bi] : Q0;
+                Q1 = sel ? S[5 * bi + 1] : Q1;
+                Q2 = sel ? S[5 * bi + 2] : Q2;
+                Q3 = sel ? S[5 * bi + 3] : Q3;
+                Q4 = sel ? S[5 * bi + 4] : Q4;
+            }
+            P0 = Q0; P1 = Q1; P2 = Q2; P3 = Q3; P4 = Q4;
+            c = T2 - 20u * nb;
+        }
+    }
+    d.cs[ol] = fh.fin();
+    d.dirty[ol] = 0;
+    atomicAdd(&d.ctr[C_X_CS_ROWS], 1ull);
+}
+
+template __global__ void k_checksum<19, 10, 2>(DS, const uint32_t *, const uint32_t *);
+
+#define CS_GENERIC(Wv) template __global__ void k_checksum<Wv, 12, 3>(DS, const uint32_t *, const uint32_t *);
+CS_GENERIC(13) CS_GENERIC(14) CS_GENERIC(15) CS_GENERIC(16) CS_GENERIC(17) CS_GENERIC(18) CS_GENERIC(19)
+CS_GENERIC(20)
+
+void launch_checksum(const DS &d, const uint32_t *list, const uint32_t *count, uint32_t maxn, bool fast, hipStream_t s) {
+    const uint32_t grid = (maxn + 255) / 256;
+    if (grid == 0) return;
+    if (fast && d.W == 19) {
+        hipLaunchKernelGGL((k_checksum<19, 10, 2>), dim3(grid), dim3(256), 0, s, d, list, count);
+        return;
+    }
+    switch (d.W) {
+#define CS_CASE(Wv) case Wv: hipLaunchKernelGGL((k_checksum<Wv, 12, 3>), dim3(grid), dim3(256), 0, s, d, list, count); break;
+        CS_CASE(13) CS_CASE(14) CS_CASE(15) CS_CASE(16) CS_CASE(17) CS_CASE(18) CS_CASE(19) CS_CASE(20)
+    default: break;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// heal helpers (heal_partition.go:33-145)
+// ---------------------------------------------------------------------------------------------
+__global__ void k_snapshot_row(DS d, uint32_t ol, MsgDesc *out) {
+    MsgDesc md;
+    wave_snapshot(d, ol, d.lo + ol, md);
+    if (lane_id() == 0) *out = md;
+}
+
+__device__ __forceinline__ uint32_t outgoing(uint32_t st) { return st == ST_TOMB ? ST_FAULTY : st; }
+
+// nodesThatNeedToReincarnate (heal_partition.go:64-92) over dense snapshots MA (slot a), MB (slot b)
+__global__ void k_heal_diff(DS d, const MsgDesc *ma, const MsgDesc *mb, MsgDesc *outA, MsgDesc *outB) {
+    const uint32_t *A = d.dense + (size_t)ma->off_lo * d.NP;
+    const uint32_t *B = d.dense + (size_t)mb->off_lo * d.NP;
+    // count
+    int na = 0, nb = 0;
+    for (uint32_t m = lane_id(); m < d.N; m += 64) {
+        const uint32_t a = A[m], b = B[m];
+        if ((a & 7u) == ST_UNKNOWN || (b & 7u) == ST_UNKNOWN) continue;
+        const uint32_t as = outgoing(a & 7u), bs = outgoing(b & 7u);
+        const uint32_t ak = ((a >> 3) << 3) | as, bk = ((b >> 3) << 3) | bs;
+        if (is_pingable(bs) && ak > bk && !is_pingable(as)) nb++;
+        if (is_pingable(as) && bk > ak && !is_pingable(bs)) na++;
+    }
+    na = wsum(na);
+    nb = wsum(nb);
+    const unsigned long long oa = pool_alloc(d, (uint32_t)na);
+    const unsigned long long ob = pool_alloc(d, (uint32_t)nb);
+    uint32_t pa = 0, pb = 0;
+    for (uint32_t base = 0; base < d.NP; base += 64) {
+        const uint32_t m = base + lane_id();
+        bool wa = false, wb = false;
+        uint32_t a = 0, b = 0;
+        if (m < d.N) {
+            a = A[m]; b = B[m];
+            if ((a & 7u) != ST_UNKNOWN && (b & 7u) != ST_UNKNOWN) {
+                const uint32_t as = outgoing(a & 7u), bs = outgoing(b & 7u);
+                const uint32_t ak = ((a >> 3) << 3) | as, bk = ((b >> 3) << 3) | bs;
+                wb = is_pingable(bs) && ak > bk && !is_pingable(as);
+                wa = is_pingable(as) && bk > ak && !is_pingable(bs);
+            }
+        }
+        const unsigned long long ma_ = __ballot(wa), mb_ = __ballot(wb);
+        if (wa && oa != ~0ull) d.pool[oa + pa + __popcll(ma_ & lanemask_lt())] = make_uint4(m | (ST_SUSPECT << 24), b >> 3, SRC_NONE, 0);
+        if (wb && ob != ~0ull) d.pool[ob + pb + __popcll(mb_ & lanemask_lt())] = make_uint4(m | (ST_SUSPECT << 24), a >> 3, SRC_NONE, 0);
+        pa += __popcll(ma_);
+        pb += __popcll(mb_);
+    }
+    if (lane_id() == 0) {
+        outA->kind = 0; outA->len = (uint32_t)na; outA->off_lo = (uint32_t)oa; outA->off_hi = (uint32_t)(oa >> 32);
+        outB->kind = 0; outB->len = (uint32_t)nb; outB->off_lo = (uint32_t)ob; outB->off_hi = (uint32_t)(ob >> 32);
+    }
+}
+
+__global__ void k_apply_msg(DS d, uint32_t ol, const MsgDesc *md, uint32_t r) {
+    wave_merge_msg(d, ol, d.lo + ol, *md, r, r);
+}
+
+// sendPingWithChanges o → t whose response is discarded (heal_partition.go:97-124): target runs
+// handlePing: Update, IssueAsReceiver(o, I_o, C_o); a full sync queues a reverse full sync
+__global__ void k_ping_with(DS d, uint32_t tol, uint32_t sender, const MsgDesc *md, uint32_t sinc, uint32_t scs,
+                            MsgDesc *resp_out, uint4 *defer, uint32_t *defer_cnt, uint32_t r) {
+    wave_merge_msg(d, tol, d.lo + tol, *md, r, r);
+    MsgDesc resp;
+    const uint32_t kept = wave_issue_recv(d, tol, sender, sinc, resp);
+    if (kept == 0) {
+        if (d.dirty[tol]) {
+            if (lane_id() == 0) defer[atomicAdd(defer_cnt, 1u)] = make_uint4(tol, 0, sender, scs);
+            resp.kind = 2;
+        } else if (d.cs[tol] != scs) {
+            wave_snapshot(d, tol, d.lo + tol, resp);
+            if (lane_id() == 0) {
+                atomicAdd(&d.ctr[C_FULL_SYNCS], 1ull);
+                if (d.njobs[tol] < d.maxjobs) d.jobs[(size_t)tol * d.maxjobs + d.njobs[tol]++] = sender;
+                else atomicAdd(&d.ctr[C_RFS_OMITTED], 1ull);
+            }
+        }
+    }
+    if (lane_id() == 0) *resp_out = resp;
+}
+
+// ---------------------------------------------------------------------------------------------
+// readback helpers
+// ---------------------------------------------------------------------------------------------
+__global__ void k_digest(DS d, unsigned long long *out, uint32_t period_div) {
+    const uint32_t ol = wave_gid();
+    if (ol >= d.NL) return;
+    const uint32_t o = d.lo + ol;
+    unsigned long long r = 0, dd = 0, t = 0;
+    for (uint32_t m = lane_id(); m < d.N; m += 64) {
+        const size_t idx = (size_t)ol * d.NP + m;
+        const uint32_t w = d.mw[idx];
+        r += mix4(o, m, w & 7u, w >> 3);
+        const uint8_t p = d.dp[idx];
+        const uint4 a = d.aux[idx];
+        if (p != DP_NONE) {
+            const uint64_t se = a.x == SRC_NONE ? 0ull : (uint64_t)a.y;
+            dd += mix4((uint64_t)o | (1ull << 40), m, (uint64_t)p | ((uint64_t)(uint32_t)(a.x + 1u) << 8), se);
+        }
+        const uint8_t ts = d.tst[idx];
+        if (ts & 7u) {
+            const uint64_t state = ts & 7u, fired = (ts >> 7) & 1u;
+            t += mix4((uint64_t)o | (2ull << 40), m, state | (fired << 4) | ((uint64_t)a.z << 8), a.w);
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        r += __shfl_xor(r, off, 64);
+        dd += __shfl_xor(dd, off, 64);
+        t += __shfl_xor(t, off, 64);
+    }
+    if (lane_id() == 0) {
+        atomicAdd(&out[0], r);
+        atomicAdd(&out[1], dd);
+        atomicAdd(&out[2], t);
+    }
+}
+
+}  // namespace swimdev

@@ -1,0 +1,411 @@
+"""swimsim — Python host binding of libswimsim.so, the MI355X SWIM protocol-round engine.
+
+The classes mirror the reference's swim package surface (maniacs-ops/ringpop-go):
+  * ``Cluster``: N simulated ``swim.Node`` processes driven in synchronous protocol rounds.
+  * ``Node``: ``swim.NodeInterface`` (swim/node.go:137-147): GetChecksum, CountReachableMembers,
+    GetReachableMembers, MemberStats, Incarnation, plus ``memberlist`` and ``disseminator`` views.
+  * ``Memberlist``: Checksum, Member, NumMembers, NumPingableMembers, MakeChange...
+    (swim/memberlist.go).
+  * ``Disseminator``: ChangesCount, ChangesByAddress, HasChanges, MaxP, ClearChanges
+    (swim/disseminator.go).
+
+Everything runs through the C ABI of include/swimsim.h and its gfx950 HIP kernels. There is no CPU
+fallback. If the library is missing or no device is usable, construction raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libswimsim.so")
+
+ALIVE, SUSPECT, FAULTY, LEAVE, TOMBSTONE, UNKNOWN = 0, 1, 2, 3, 4, 7
+STATUS_NAMES = {ALIVE: "alive", SUSPECT: "suspect", FAULTY: "faulty", LEAVE: "leave", TOMBSTONE: "tombstone"}
+SOURCE_NONE = -1
+EV_KILL, EV_REVIVE, EV_REINCARNATE, EV_LEAVE, EV_PARTITION, EV_HEAL, EV_REAP = 1, 2, 3, 4, 5, 6, 7
+COUNTER_NAMES = [
+    "rounds", "pings", "pings_ok", "pingreqs", "helper_calls", "helper_errors", "inconclusive",
+    "suspect_decl", "applied", "refutes", "full_syncs", "full_syncs_pingreq", "rfs_done",
+    "rfs_omitted", "timers_fired", "msg_changes", "heal_attempts", "heal_failures",
+]
+T0_MS = 1_500_000_000_000
+ERRORS = {-1: "EINVAL", -2: "ENOMEM", -3: "EHIP", -4: "ECAPACITY", -5: "ERANGE"}
+
+
+class SwimsimError(RuntimeError):
+    pass
+
+
+class Config(C.Structure):
+    _fields_ = [
+        ("num_members", C.c_uint32), ("device", C.c_uint32), ("t0_ms", C.c_int64),
+        ("protocol_period_ms", C.c_uint32), ("suspect_timeout_ms", C.c_uint32), ("faulty_timeout_ms", C.c_uint32),
+        ("tombstone_timeout_ms", C.c_uint32), ("ping_request_size", C.c_uint32),
+        ("max_reverse_full_sync_jobs", C.c_uint32), ("p_factor", C.c_uint32), ("seed", C.c_uint64),
+        ("addresses", C.c_char_p), ("addr_stride", C.c_uint32), ("max_rounds", C.c_uint32),
+        ("message_pool_bytes", C.c_uint64), ("observer_begin", C.c_uint32), ("observer_end", C.c_uint32),
+    ]
+
+
+class Event(C.Structure):
+    _fields_ = [("round", C.c_uint32), ("kind", C.c_uint32), ("a", C.c_int32), ("b", C.c_int32)]
+
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libswimsim.so. Raises loudly when it is absent: the product has no fallback."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise SwimsimError(f"{path} is missing: build it with `make -C ringpop-go_amd` (hipcc, gfx950)")
+    L = C.CDLL(path)
+    P, u32, i32, i64, u64, sz = C.c_void_p, C.c_uint32, C.c_int32, C.c_int64, C.c_uint64, C.c_size_t
+    sigs = {
+        "swimsim_abi_version": (C.c_int, []),
+        "swimsim_create": (C.c_int, [C.POINTER(Config), C.POINTER(P)]),
+        "swimsim_destroy": (C.c_int, [P]),
+        "swimsim_last_error": (C.c_char_p, [P]),
+        "swimsim_init_converged": (C.c_int, [P]),
+        "swimsim_init_self_only": (C.c_int, [P]),
+        "swimsim_set_member": (C.c_int, [P, u32, u32, i32, i64]),
+        "swimsim_make_change": (C.c_int, [P, u32, u32, i64, i32]),
+        "swimsim_clear_changes": (C.c_int, [P, u32]),
+        "swimsim_set_live": (C.c_int, [P, u32, i32]),
+        "swimsim_set_partition": (C.c_int, [P, u32, i32]),
+        "swimsim_set_round": (C.c_int, [P, u32]),
+        "swimsim_step": (C.c_int, [P, u32, C.POINTER(Event), sz]),
+        "swimsim_heal": (C.c_int, [P, u32, P, sz, C.POINTER(sz)]),
+        "swimsim_round": (u32, [P]),
+        "swimsim_checksums": (C.c_int, [P, P]),
+        "swimsim_row": (C.c_int, [P, u32, P, P]),
+        "swimsim_count_reachable": (C.c_int, [P, u32, C.POINTER(u32)]),
+        "swimsim_reachable": (C.c_int, [P, u32, P, sz, C.POINTER(sz)]),
+        "swimsim_node_stats": (C.c_int, [P, u32, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)]),
+        "swimsim_changes": (C.c_int, [P, u32, P, P, P, P, sz, C.POINTER(sz)]),
+        "swimsim_timers": (C.c_int, [P, u32, P, P, P, P, P, sz, C.POINTER(sz)]),
+        "swimsim_iter_state": (C.c_int, [P, u32, C.POINTER(i64), C.POINTER(u32)]),
+        "swimsim_last_targets": (C.c_int, [P, P]),
+        "swimsim_counters": (C.c_int, [P, P]),
+        "swimsim_digest": (C.c_int, [P, C.POINTER(u64), C.POINTER(u64), C.POINTER(u64)]),
+        "swimsim_converged": (C.c_int, [P, C.POINTER(i32)]),
+        "swimsim_kernel_times": (C.c_int, [P, P, P, P, P, sz, C.POINTER(sz)]),
+        "swimsim_enable_timing": (C.c_int, [P, i32]),
+    }
+    for name, (res, args) in sigs.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def _events(events):
+    arr = (Event * max(1, len(events)))()
+    for i, (r, k, a, b) in enumerate(events):
+        arr[i].round, arr[i].kind, arr[i].a, arr[i].b = int(r), int(k), int(a), int(b)
+    return arr
+
+
+class Cluster:
+    """N swim nodes simulated on one MI355X (or one shard of observer rows)."""
+
+    def __init__(self, n, *, t0_ms=T0_MS, period_ms=200, suspect_ms=5000, faulty_ms=24 * 3600 * 1000,
+                 tombstone_ms=60_000, ping_request_size=3, max_rfs_jobs=5, p_factor=15, seed=1, addresses=None,
+                 device=0, init="converged", max_rounds=0, message_pool_bytes=0, observer_range=None):
+        L = load_library()
+        self.n = n
+        self.t0_ms, self.period_ms = t0_ms, period_ms
+        cfg = Config()
+        cfg.num_members, cfg.device, cfg.t0_ms, cfg.protocol_period_ms = n, device, t0_ms, period_ms
+        cfg.suspect_timeout_ms, cfg.faulty_timeout_ms, cfg.tombstone_timeout_ms = suspect_ms, faulty_ms, tombstone_ms
+        cfg.ping_request_size, cfg.max_reverse_full_sync_jobs, cfg.p_factor = ping_request_size, max_rfs_jobs, p_factor
+        cfg.seed, cfg.max_rounds, cfg.message_pool_bytes = seed, max_rounds, message_pool_bytes
+        if observer_range:
+            cfg.observer_begin, cfg.observer_end = observer_range
+        self._addr_buf = None
+        if addresses is not None:
+            stride = max(len(a) for a in addresses)
+            buf = b"".join(a.encode().ljust(stride, b"\0") for a in addresses)
+            self._addr_buf = C.create_string_buffer(buf, len(buf))
+            cfg.addresses = C.cast(self._addr_buf, C.c_char_p)
+            cfg.addr_stride = stride
+        h = C.c_void_p()
+        rc = L.swimsim_create(C.byref(cfg), C.byref(h))
+        if rc != 0:
+            raise SwimsimError(f"swimsim_create failed: {ERRORS.get(rc, rc)}")
+        self.h = h
+        self.lo = observer_range[0] if observer_range else 0
+        self.nl = (observer_range[1] - observer_range[0]) if observer_range else n
+        if init == "converged":
+            self._chk(L.swimsim_init_converged(self.h))
+        elif init == "self":
+            self._chk(L.swimsim_init_self_only(self.h))
+
+    def _chk(self, rc):
+        if rc < 0:
+            msg = load_library().swimsim_last_error(self.h).decode()
+            raise SwimsimError(f"{ERRORS.get(rc, rc)}: {msg}")
+        return rc
+
+    def close(self):
+        if getattr(self, "h", None):
+            load_library().swimsim_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    # ---- driving -------------------------------------------------------------------------
+    def step(self, rounds=1, events=()):
+        ev = _events(events)
+        self._chk(load_library().swimsim_step(self.h, rounds, ev, len(events)))
+
+    def run(self, rounds, events=()):
+        self.step(rounds, events)
+
+    def heal(self, o):
+        out = np.empty(self.n, np.int32)
+        n = C.c_size_t()
+        self._chk(load_library().swimsim_heal(self.h, o, out.ctypes.data, self.n, C.byref(n)))
+        return [int(x) for x in out[: min(n.value, self.n)]]
+
+    @property
+    def round(self):
+        return load_library().swimsim_round(self.h)
+
+    # ---- setup -----------------------------------------------------------------------------
+    def set_member(self, o, m, status, inc):
+        self._chk(load_library().swimsim_set_member(self.h, o, m, status, inc))
+
+    def make_change(self, o, m, inc, status):
+        return self._chk(load_library().swimsim_make_change(self.h, o, m, inc, status))
+
+    def clear_changes(self, o):
+        self._chk(load_library().swimsim_clear_changes(self.h, o))
+
+    def set_live(self, m, live):
+        self._chk(load_library().swimsim_set_live(self.h, m, int(live)))
+
+    def set_partition(self, m, label):
+        self._chk(load_library().swimsim_set_partition(self.h, m, label))
+
+    def set_round(self, r):
+        self._chk(load_library().swimsim_set_round(self.h, r))
+
+    # ---- read-back -------------------------------------------------------------------------
+    def checksums(self):
+        out = np.empty(self.nl, np.uint32)
+        self._chk(load_library().swimsim_checksums(self.h, out.ctypes.data))
+        return out
+
+    def checksum(self, o):
+        return int(self.checksums()[o - self.lo])
+
+    def row(self, o):
+        st = np.empty(self.n, np.uint8)
+        inc = np.empty(self.n, np.int64)
+        self._chk(load_library().swimsim_row(self.h, o, st.ctypes.data, inc.ctypes.data))
+        return st, inc
+
+    def rows(self):
+        st = np.empty((self.nl, self.n), np.uint8)
+        inc = np.empty((self.nl, self.n), np.int64)
+        for i in range(self.nl):
+            st[i], inc[i] = self.row(self.lo + i)
+        return st, inc
+
+    def member(self, o, m):
+        st, inc = self.row(o)
+        return int(st[m]), int(inc[m])
+
+    def node_stats(self, o):
+        p, mx, ch, mem = C.c_int32(), C.c_int32(), C.c_int32(), C.c_int32()
+        self._chk(load_library().swimsim_node_stats(self.h, o, C.byref(p), C.byref(mx), C.byref(ch), C.byref(mem)))
+        return {"pingable": p.value, "maxp": mx.value, "changes": ch.value, "members": mem.value}
+
+    def changes(self, o):
+        cap = self.n
+        m = np.empty(cap, np.int32); p = np.empty(cap, np.int32); s = np.empty(cap, np.int32)
+        si = np.empty(cap, np.int64)
+        n = C.c_size_t()
+        self._chk(load_library().swimsim_changes(self.h, o, m.ctypes.data, p.ctypes.data, s.ctypes.data, si.ctypes.data,
+                                                 cap, C.byref(n)))
+        return {int(m[i]): (int(p[i]), int(s[i]), int(si[i])) for i in range(n.value)}
+
+    def timers(self, o):
+        cap = self.n
+        m = np.empty(cap, np.int32); st = np.empty(cap, np.int32); f = np.empty(cap, np.int32)
+        dl = np.empty(cap, np.int64); sj = np.empty(cap, np.int64)
+        n = C.c_size_t()
+        self._chk(load_library().swimsim_timers(self.h, o, m.ctypes.data, st.ctypes.data, f.ctypes.data,
+                                                dl.ctypes.data, sj.ctypes.data, cap, C.byref(n)))
+        return {int(m[i]): (int(st[i]), int(f[i]), int(dl[i]), int(sj[i])) for i in range(n.value)}
+
+    def iter_state(self, o):
+        idx, ep = C.c_int64(), C.c_uint32()
+        self._chk(load_library().swimsim_iter_state(self.h, o, C.byref(idx), C.byref(ep)))
+        return idx.value, ep.value
+
+    def last_targets(self):
+        out = np.empty(self.nl, np.int32)
+        self._chk(load_library().swimsim_last_targets(self.h, out.ctypes.data))
+        return out
+
+    def counters(self):
+        out = np.zeros(len(COUNTER_NAMES), np.uint64)
+        self._chk(load_library().swimsim_counters(self.h, out.ctypes.data))
+        return dict(zip(COUNTER_NAMES, (int(x) for x in out)))
+
+    def digest(self):
+        a, b, c = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        self._chk(load_library().swimsim_digest(self.h, C.byref(a), C.byref(b), C.byref(c)))
+        return a.value, b.value, c.value
+
+    def converged(self):
+        v = C.c_int32()
+        self._chk(load_library().swimsim_converged(self.h, C.byref(v)))
+        return bool(v.value)
+
+    def count_reachable(self, o):
+        v = C.c_uint32()
+        self._chk(load_library().swimsim_count_reachable(self.h, o, C.byref(v)))
+        return v.value
+
+    def enable_timing(self, on=True):
+        self._chk(load_library().swimsim_enable_timing(self.h, int(on)))
+
+    def kernel_times(self):
+        cap = 32
+        names = (C.c_char_p * cap)()
+        avg = np.zeros(cap, np.float64)
+        n_l = np.zeros(cap, np.uint64)
+        byt = np.zeros(cap, np.float64)
+        n = C.c_size_t()
+        self._chk(load_library().swimsim_kernel_times(self.h, names, avg.ctypes.data, n_l.ctypes.data, byt.ctypes.data,
+                                                      cap, C.byref(n)))
+        return {names[i].decode(): {"avg_ms": float(avg[i]), "launches": int(n_l[i]), "alg_bytes": float(byt[i])}
+                for i in range(n.value)}
+
+    def node(self, o):
+        return Node(self, o)
+
+
+@dataclass
+class MemberView:
+    address: str
+    status: str
+    incarnation: int
+
+
+def address_of(m: int) -> str:
+    return "10.%03d.%03d.%03d:7000" % ((m >> 16) & 255, (m >> 8) & 255, m & 255)
+
+
+class Memberlist:
+    """swim.memberlist view of one observer (swim/memberlist.go)."""
+
+    def __init__(self, cluster: Cluster, o: int):
+        self.c, self.o = cluster, o
+
+    def Checksum(self):                                   # memberlist.go:73-80
+        return self.c.checksum(self.o)
+
+    def Member(self, m):                                  # memberlist.go:131-138
+        st, inc = self.c.member(self.o, m)
+        if st == UNKNOWN:
+            return None, False
+        return MemberView(address_of(m), STATUS_NAMES[st], inc), True
+
+    def NumMembers(self):                                 # memberlist.go:174-179
+        return self.c.node_stats(self.o)["members"]
+
+    def NumPingableMembers(self):                         # memberlist.go:188-198
+        return self.c.node_stats(self.o)["pingable"]
+
+    def MakeChange(self, m, incarnation, status):         # memberlist.go:282-307
+        return self.c.make_change(self.o, m, incarnation, status)
+
+    def MakeAlive(self, m, inc):
+        return self.MakeChange(m, inc, ALIVE)
+
+    def MakeSuspect(self, m, inc):
+        return self.MakeChange(m, inc, SUSPECT)
+
+    def MakeFaulty(self, m, inc):
+        return self.MakeChange(m, inc, FAULTY)
+
+    def MakeLeave(self, m, inc):
+        return self.MakeChange(m, inc, LEAVE)
+
+    def MakeTombstone(self, m, inc):
+        return self.MakeChange(m, inc, TOMBSTONE)
+
+    def GetReachableMembers(self):                        # memberlist.go:471-483
+        st, _ = self.c.row(self.o)
+        return [address_of(m) for m in np.nonzero(st <= SUSPECT)[0]]
+
+    def CountReachableMembers(self):                      # memberlist.go:485-497
+        return self.c.count_reachable(self.o)
+
+
+class Disseminator:
+    """swim.disseminator view of one observer (swim/disseminator.go)."""
+
+    def __init__(self, cluster: Cluster, o: int):
+        self.c, self.o = cluster, o
+
+    def ChangesCount(self):                               # disseminator.go:239-244
+        return self.c.node_stats(self.o)["changes"]
+
+    def HasChanges(self):                                 # disseminator.go:100-105
+        return self.ChangesCount() > 0
+
+    def ChangesByAddress(self, m):                        # disseminator.go:229-237
+        ch = self.c.changes(self.o)
+        return (ch[m], True) if m in ch else (None, False)
+
+    def MaxP(self):                                       # disseminator.go:49
+        return self.c.node_stats(self.o)["maxp"]
+
+    def ClearChanges(self):                               # disseminator.go:217-221
+        self.c.clear_changes(self.o)
+
+
+class Node:
+    """swim.NodeInterface of simulated member o (swim/node.go:137-147)."""
+
+    def __init__(self, cluster: Cluster, o: int):
+        self.c, self.o = cluster, o
+        self.memberlist = Memberlist(cluster, o)
+        self.disseminator = Disseminator(cluster, o)
+
+    def Address(self):
+        return address_of(self.o)
+
+    def GetChecksum(self):
+        return self.memberlist.Checksum()
+
+    def CountReachableMembers(self):
+        return self.memberlist.CountReachableMembers()
+
+    def GetReachableMembers(self):
+        return self.memberlist.GetReachableMembers()
+
+    def Incarnation(self):                                # node.go:256-264
+        return self.c.member(self.o, self.o)[1]
+
+    def MemberStats(self):                                # stats.go:41-52
+        st, inc = self.c.row(self.o)
+        members = [MemberView(address_of(m), STATUS_NAMES[int(st[m])], int(inc[m]))
+                   for m in range(self.c.n) if st[m] != UNKNOWN]
+        return {"checksum": self.GetChecksum(), "members": members}
+
+    def HasChanges(self):
+        return self.disseminator.HasChanges()
