@@ -149,6 +149,9 @@ int swimsim_converged(swimsim_t *h, int32_t *out);
 int swimsim_kernel_times(swimsim_t *h, const char **names, double *avg_ms, uint64_t *launches,
                          double *alg_bytes, size_t cap, size_t *n);
 int swimsim_enable_timing(swimsim_t *h, int32_t enable);
+/* time the checksum kernel alone on the first nrows rows (mode 0 full, 1 hasher only, 2 formatting
+ * only; the last two are diagnostics and leave garbage checksums) — average ms per launch */
+int swimsim_bench_checksum(swimsim_t *h, uint32_t nrows, int32_t mode, int32_t reps, double *ms);
 
 #ifdef __cplusplus
 }

@@ -71,6 +71,13 @@ struct DS {
     uint4 *dense_meta;      // {source, source e, known count, unused}
     uint32_t *dense_cur;
     uint32_t dense_cap;
+    uint32_t *dense_len;    // checksum-string length of each snapshot
+    int32_t *dense_last;    // last included member of each snapshot (-2: rescan)
+    uint32_t *dense_cs;     // checksum of each snapshot (deferred full-sync decisions)
+    uint32_t *clen;         // [NL] checksum-string length of each row
+    int32_t *clast;         // [NL] last included member (-2: rescan)
+    uint32_t dig_d0;          // decimal digits of t0
+    uint32_t dig_thr[8];      // e at which t0 + e*period gains a digit (0xFFFFFFFF = never)
 };
 
 __host__ __device__ inline bool is_pingable(uint32_t st) { return st <= ST_SUSPECT; }

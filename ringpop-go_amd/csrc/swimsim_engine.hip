@@ -66,7 +66,7 @@ struct swimsim {
     uint4 *defer = nullptr;
     uint32_t *defer_cnt = nullptr;
     uint32_t *exh_list = nullptr, *exh_cnt = nullptr, *scratch = nullptr;
-    uint8_t *need = nullptr;
+    uint8_t *need = nullptr, *fsflag = nullptr;
     uint4 *evbuf = nullptr;
     uint32_t *ev_applied = nullptr;
     uint32_t evcap = 0;
@@ -156,8 +156,8 @@ void drain_timing(swimsim *h) {
     h->pending.clear();
 }
 
-inline uint32_t blocks_for_waves(uint32_t waves) { return (waves + 3) / 4; }      // 4 waves per 256-thread block
-inline uint32_t blocks_for_threads(uint32_t n) { return (n + 255) / 256; }
+inline uint32_t blocks_for_waves(uint32_t waves) { return waves ? (waves + 3) / 4 : 1; }  // 4 waves per 256-thread block
+inline uint32_t blocks_for_threads(uint32_t n) { return n ? (n + 255) / 256 : 1; }
 
 int build_tail_table(swimsim *h, uint32_t ecap) {
     std::vector<uint32_t> t((size_t)ecap * 4 * 8, 0u);
@@ -183,6 +183,21 @@ int build_tail_table(swimsim *h, uint32_t ecap) {
     if (int rc = dalloc(h, &dev, t.size(), "tail table")) return rc;
     HIPCHK(h, hipMemcpy(dev, t.data(), t.size() * 4, hipMemcpyHostToDevice));
     h->d.tailw = dev;
+    // digit-count thresholds of t0 + e*period over the table (the checksum record length formula)
+    {
+        uint32_t d0 = t[6] - 6, nthr = 0;   // "alive" + ';' around the digits of e = 0
+        for (int k = 0; k < 8; k++) h->d.dig_thr[k] = 0xFFFFFFFFu;
+        uint32_t prev = d0;
+        for (uint32_t e = 1; e < ecap; e++) {
+            const uint32_t de = t[((size_t)e * 4) * 8 + 6] - 6;
+            if (de != prev) {
+                if (de != prev + 1 || nthr == 8) return h->fail(SWIMSIM_EINVAL, "incarnation digit count changes too often");
+                h->d.dig_thr[nthr++] = e;
+                prev = de;
+            }
+        }
+        h->d.dig_d0 = d0;
+    }
     h->ecap = ecap;
     h->d.ecap = ecap;
     h->max_tl = max_tl;
@@ -233,21 +248,20 @@ void checksum_dirty(swimsim *h, int mode) {
     launch_checksum(h->d, h->list, h->cnt, h->NL, h->fast_cs, h->s);
 }
 
-// defer list holds uint4 {row, ...}: copy rows out and checksum them
-__global__ void k_defer_rows(const uint4 *defer, const uint32_t *defer_cnt, uint32_t *list, uint32_t *cnt) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i == 0) *cnt = *defer_cnt;
-    if (i < *defer_cnt) list[i] = defer[i].x;
+// run the receive waves over a sorted inbox (phase D when phase==0, phase Q2 when phase==1), then
+// resolve the deferred full-sync decisions with one batched checksum of the receivers' snapshots
+void resolve_deferred(swimsim *h, int phase, MsgDesc *rdesc, uint32_t maxn) {
+    {
+        Scope sc(h, F_CHECKSUM);
+        hipLaunchKernelGGL(k_defer_ids, dim3(blocks_for_threads(maxn)), dim3(256), 0, h->s, h->d, h->defer,
+                           h->defer_cnt, h->list, h->cnt);
+        launch_checksum(h->d, h->list, h->cnt, maxn, h->fast_cs, h->s);
+    }
+    Scope sc(h, phase == 1 ? F_PINGREQ : F_RECV);
+    hipLaunchKernelGGL(k_recv_finish, dim3(blocks_for_threads(maxn)), dim3(256), 0, h->s, h->d, h->defer,
+                       h->defer_cnt, rdesc, phase, h->fsflag);
 }
 
-void checksum_deferred(swimsim *h, uint32_t maxn) {
-    Scope sc(h, F_CHECKSUM);
-    hipLaunchKernelGGL(k_defer_rows, dim3(blocks_for_threads(maxn)), dim3(256), 0, h->s, h->defer, h->defer_cnt, h->list,
-                       h->cnt);
-    launch_checksum(h->d, h->list, h->cnt, maxn, h->fast_cs, h->s);
-}
-
-// run the receive waves over a sorted inbox (phase D when phase==0, phase Q2 when phase==1)
 void run_waves(swimsim *h, int phase, uint32_t nruns_valid, uint32_t maxcount) {
     RecvArgs a{};
     a.ukeys = h->ukeys; a.counts = h->counts; a.offs = h->offs; a.vals = h->vals_out;
@@ -259,20 +273,20 @@ void run_waves(swimsim *h, int phase, uint32_t nruns_valid, uint32_t maxcount) {
     a.rdesc = phase == 0 ? h->rdesc : h->rdesc2;
     a.defer = h->defer;
     a.defer_cnt = h->defer_cnt;
+    a.fsflag = h->fsflag;
     a.r = h->round;
+    hipMemsetAsync(h->defer_cnt, 0, 4, h->s);
     for (uint32_t w = 0; w < maxcount; w++) {
         a.w = w;
-        {
-            Scope sc(h, phase == 0 ? F_RECV : F_PINGREQ);
-            hipMemsetAsync(h->defer_cnt, 0, 4, h->s);
-            hipLaunchKernelGGL(k_recv, dim3(blocks_for_waves(nruns_valid)), dim3(256), 0, h->s, h->d, a);
-        }
-        checksum_deferred(h, nruns_valid);
-        {
-            Scope sc(h, phase == 0 ? F_RECV : F_PINGREQ);
-            hipLaunchKernelGGL(k_recv_finish, dim3(blocks_for_waves(nruns_valid)), dim3(256), 0, h->s, h->d, h->defer,
-                               h->defer_cnt, a.rdesc, phase);
-        }
+        Scope sc(h, phase == 0 ? F_RECV : F_PINGREQ);
+        hipLaunchKernelGGL(k_recv, dim3(blocks_for_waves(nruns_valid)), dim3(256), 0, h->s, h->d, a);
+    }
+    const uint32_t maxdefer = std::min<uint64_t>((uint64_t)nruns_valid * maxcount, h->d.dense_cap);
+    resolve_deferred(h, phase, a.rdesc, maxdefer);
+    if (phase == 0) {
+        Scope sc(h, F_RECV);
+        hipLaunchKernelGGL(k_build_jobs, dim3(blocks_for_threads(nruns_valid)), dim3(256), 0, h->s, h->d, h->ukeys,
+                           h->counts, h->offs, h->vals_out, nruns_valid, h->fsflag);
     }
 }
 
@@ -312,8 +326,7 @@ int ping_with(swimsim *h, uint32_t o, uint32_t t, const MsgDesc *md_dev) {
     hipMemsetAsync(h->defer_cnt, 0, 4, h->s);
     hipLaunchKernelGGL(k_ping_with, dim3(1), dim3(64), 0, h->s, h->d, t - h->lo, o, md_dev, sinc_cs[0], sinc_cs[1],
                        h->hdesc + 7, h->defer, h->defer_cnt, h->round);
-    checksum_deferred(h, 1);
-    hipLaunchKernelGGL(k_recv_finish, dim3(1), dim3(64), 0, h->s, h->d, h->defer, h->defer_cnt, h->hdesc + 6, 2);
+    resolve_deferred(h, 2, h->hdesc + 6, 1);
     return 0;
 }
 
@@ -609,7 +622,8 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
         (rc = dalloc(h, &d.njobs, h->NL, "njobs")) || (rc = dalloc(h, &d.jobs, (size_t)h->NL * h->maxjobs, "jobs")) ||
         (rc = dalloc(h, &d.dblk, (size_t)h->NL * d.NBW, "dblk")) || (rc = dalloc(h, &d.tblk, (size_t)h->NL * d.NB, "tblk")) ||
         (rc = dalloc(h, &d.live, h->N, "live")) || (rc = dalloc(h, &d.part, h->N, "part")) ||
-        (rc = dalloc(h, &d.ctr, 32, "counters")) || (rc = dalloc(h, &d.err, 4, "err")))
+        (rc = dalloc(h, &d.ctr, 32, "counters")) || (rc = dalloc(h, &d.err, 4, "err")) ||
+        (rc = dalloc(h, &d.clen, h->NL, "clen")) || (rc = dalloc(h, &d.clast, h->NL, "clast")))
         return bail(rc);
     // address words
     {
@@ -634,9 +648,18 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
     d.pool_cap = want_records;
     if ((rc = dalloc(h, &d.pool, want_records, "message pool")) || (rc = dalloc(h, &d.pool_cur, 1, "pool cursor")))
         return bail(rc);
-    d.dense_cap = (uint32_t)std::max<uint64_t>(64, std::min<uint64_t>(h->NL + 64, (4ull << 30) / (4ull * h->NP)));
+    {
+        // dense snapshots (full-sync payloads, deferred full-sync decisions, reverse-full-sync sources):
+        // up to 2 per observer row, bounded by a third of the free HBM
+        size_t freeb = 0, totalb = 0;
+        hipMemGetInfo(&freeb, &totalb);
+        const uint64_t by_mem = (uint64_t)(freeb / 3) / (4ull * h->NP);
+        d.dense_cap = (uint32_t)std::max<uint64_t>(64, std::min<uint64_t>(2ull * h->NL + 64, by_mem));
+    }
     if ((rc = dalloc(h, &d.dense, (size_t)d.dense_cap * h->NP, "dense snapshots")) ||
-        (rc = dalloc(h, &d.dense_meta, d.dense_cap, "dense meta")) || (rc = dalloc(h, &d.dense_cur, 1, "dense cursor")))
+        (rc = dalloc(h, &d.dense_meta, d.dense_cap, "dense meta")) || (rc = dalloc(h, &d.dense_cur, 1, "dense cursor")) ||
+        (rc = dalloc(h, &d.dense_len, d.dense_cap, "dense len")) || (rc = dalloc(h, &d.dense_last, d.dense_cap, "dense last")) ||
+        (rc = dalloc(h, &d.dense_cs, d.dense_cap, "dense cs")))
         return bail(rc);
     // work buffers
     const size_t NLK = (size_t)h->NL * h->K;
@@ -651,11 +674,12 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
         (rc = dalloc(h, &h->keys_out, NLK, "keys_out")) || (rc = dalloc(h, &h->vals_out, NLK, "vals_out")) ||
         (rc = dalloc(h, &h->ukeys, NLK, "ukeys")) || (rc = dalloc(h, &h->counts, NLK, "counts")) ||
         (rc = dalloc(h, &h->offs, NLK, "offs")) || (rc = dalloc(h, &h->nruns, 1, "nruns")) ||
-        (rc = dalloc(h, &h->info, 8, "info")) || (rc = dalloc(h, &h->list, NLK + 64, "list")) ||
-        (rc = dalloc(h, &h->cnt, 1, "cnt")) || (rc = dalloc(h, &h->defer, NLK + 64, "defer")) ||
+        (rc = dalloc(h, &h->info, 8, "info")) || (rc = dalloc(h, &h->list, NLK + 2 * (size_t)h->NL + 64, "list")) ||
+        (rc = dalloc(h, &h->cnt, 1, "cnt")) || (rc = dalloc(h, &h->defer, NLK + 2 * (size_t)h->NL + 64, "defer")) ||
         (rc = dalloc(h, &h->defer_cnt, 1, "defer_cnt")) || (rc = dalloc(h, &h->exh_list, h->NL, "exh_list")) ||
         (rc = dalloc(h, &h->exh_cnt, 1, "exh_cnt")) || (rc = dalloc(h, &h->scratch, (size_t)64 * (h->NP / 32), "scratch")) ||
-        (rc = dalloc(h, &h->need, h->NL, "need")) || (rc = dalloc(h, &h->digest_buf, 4, "digest")))
+        (rc = dalloc(h, &h->need, h->NL, "need")) || (rc = dalloc(h, &h->digest_buf, 4, "digest")) ||
+        (rc = dalloc(h, &h->fsflag, NLK, "fsflag")))
         return bail(rc);
     h->evcap = 4 * h->N + 64;
     if ((rc = dalloc(h, &h->evbuf, h->evcap, "events")) || (rc = dalloc(h, &h->ev_applied, h->evcap, "ev_applied")))
@@ -672,6 +696,7 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
     hipMemset(d.ctr, 0, 32 * 8);
     hipMemset(d.err, 0, 4);
     hipMemset(h->need, 0, h->NL);
+    hipMemset(h->fsflag, 0, NLK);
     hipMemset(d.njobs, 0, h->NL * 4);
     h->live.assign(h->N, 1);
     h->part.assign(h->N, 0);
@@ -950,6 +975,31 @@ int swimsim_converged(swimsim_t *h, int32_t *out) {
     }
     *out = ok ? 1 : 0;
     return SWIMSIM_OK;
+}
+
+__global__ void k_iota(uint32_t *list, uint32_t *cnt, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) *cnt = n;
+    if (i < n) list[i] = i;
+}
+
+int swimsim_bench_checksum(swimsim_t *h, uint32_t nrows, int32_t mode, int32_t reps, double *ms) {
+    if (!h || !ms || nrows == 0 || nrows > h->NL || reps < 1) return SWIMSIM_EINVAL;
+    hipLaunchKernelGGL(k_iota, dim3(blocks_for_threads(nrows)), dim3(256), 0, h->s, h->list, h->cnt, nrows);
+    hipEvent_t a, b;
+    HIPCHK(h, hipEventCreate(&a));
+    HIPCHK(h, hipEventCreate(&b));
+    launch_checksum_mode(h->d, h->list, h->cnt, nrows, mode, h->s);   // warm-up
+    HIPCHK(h, hipEventRecord(a, h->s));
+    for (int i = 0; i < reps; i++) launch_checksum_mode(h->d, h->list, h->cnt, nrows, mode, h->s);
+    HIPCHK(h, hipEventRecord(b, h->s));
+    HIPCHK(h, hipEventSynchronize(b));
+    float t = 0;
+    hipEventElapsedTime(&t, a, b);
+    *ms = t / reps;
+    hipEventDestroy(a);
+    hipEventDestroy(b);
+    return check_err(h);
 }
 
 int swimsim_enable_timing(swimsim_t *h, int32_t enable) {

@@ -5,4 +5,6 @@
 namespace swimdev {
 void launch_checksum(const DS &d, const uint32_t *list, const uint32_t *count, uint32_t maxn, bool fast,
                      hipStream_t s);
+void launch_checksum_mode(const DS &d, const uint32_t *list, const uint32_t *count, uint32_t maxn, int mode,
+                          hipStream_t s);
 }

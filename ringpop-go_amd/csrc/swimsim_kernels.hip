@@ -42,9 +42,28 @@ __device__ __forceinline__ bool reach(const DS &d, uint32_t a, uint32_t b) {
 // by wave_finalize (AdjustMaxPropagations, disseminator.go:75-97).
 // ---------------------------------------------------------------------------------------------
 struct MAcc {
-    int dping, ddc, napp, nref, nproc, evict;
-    __device__ MAcc() : dping(0), ddc(0), napp(0), nref(0), nproc(0), evict(0) {}
+    int dping, ddc, napp, nref, nproc, evict, dlen, maxlast, inval;
+    __device__ MAcc() : dping(0), ddc(0), napp(0), nref(0), nproc(0), evict(0), dlen(0), maxlast(-1), inval(0) {}
 };
+
+// bytes of one member's checksum record addr ‖ status ‖ decimal(inc) ‖ ';' (memberlist.go:115-121);
+// tombstones and unknown members contribute nothing (memberlist.go:112-114)
+__device__ __forceinline__ int reclen(const DS &d, uint32_t st, uint32_t e) {
+    if (st >= 4u) return 0;
+    uint32_t dl = d.dig_d0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) dl += e >= d.dig_thr[k] ? 1u : 0u;
+    return (int)(d.W + 5u + (st == ST_SUSPECT ? 2u : 0u) + (st == ST_FAULTY ? 1u : 0u) + dl + 1u);
+}
+
+// keep the per-row checksum-string length and last included member current (the FarmHash
+// prologue needs both before the chain starts)
+__device__ __forceinline__ void track_len(const DS &d, uint32_t ol, uint32_t m, uint32_t old_w, uint32_t new_w, MAcc &acc) {
+    const uint32_t os = old_w & 7u, ns = new_w & 7u;
+    acc.dlen += reclen(d, ns, new_w >> 3) - reclen(d, os, old_w >> 3);
+    if (ns < 4u) acc.maxlast = max(acc.maxlast, (int)m);
+    else if (os < 4u && (int)m == d.clast[ol]) acc.inval = 1;
+}
 
 __device__ __forceinline__ void merge_change(const DS &d, uint32_t ol, uint32_t o, uint32_t m, uint32_t cst, uint32_t ce,
                                              uint32_t csrc, uint32_t csinc, uint32_t now_e, uint32_t sched_r, MAcc &acc) {
@@ -65,6 +84,7 @@ __device__ __forceinline__ void merge_change(const DS &d, uint32_t ol, uint32_t 
         return;
     }
     d.mw[idx] = (ne << 3) | nst;
+    track_len(d, ol, m, cur, (ne << 3) | nst, acc);
     if (m != o) acc.dping += (int)is_pingable(nst) - (int)is_pingable(cur_st);
     // RecordChange (disseminator.go:223-227): entry = {p 0, source, source incarnation}
     if (d.dp[idx] == DP_NONE) acc.ddc++;
@@ -91,7 +111,8 @@ __device__ __forceinline__ void merge_change(const DS &d, uint32_t ol, uint32_t 
     acc.napp++;
 }
 
-__device__ __forceinline__ void fold_row(const DS &d, uint32_t ol, int dping, int ddc, int napp, int nref, int evict) {
+__device__ __forceinline__ void fold_row(const DS &d, uint32_t ol, int dping, int ddc, int napp, int nref, int evict,
+                                         int dlen, int maxlast, int inval) {
     if (dping) d.ping[ol] += dping;
     if (ddc) d.dcnt[ol] += ddc;
     if (napp) {
@@ -99,14 +120,24 @@ __device__ __forceinline__ void fold_row(const DS &d, uint32_t ol, int dping, in
         atomicAdd(&d.ctr[C_APPLIED], (unsigned long long)napp);
     }
     if (napp || evict) d.dirty[ol] = 1;                            // ComputeChecksum pending
+    if (dlen) d.clen[ol] += dlen;
+    if (maxlast > d.clast[ol]) d.clast[ol] = maxlast;
+    else if (inval) d.clast[ol] = -2;                              // rescanned by the checksum kernel
     if (nref) atomicAdd(&d.ctr[C_REFUTES], (unsigned long long)nref);
+}
+
+__device__ __forceinline__ int wmax(int v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off, 64));
+    return v;
 }
 
 __device__ __forceinline__ void wave_finalize(const DS &d, uint32_t ol, const MAcc &acc) {
     const int dping = wsum(acc.dping), ddc = wsum(acc.ddc), napp = wsum(acc.napp), nref = wsum(acc.nref);
-    const int ev = wsum(acc.evict), np = wsum(acc.nproc);
+    const int ev = wsum(acc.evict), np = wsum(acc.nproc), dl = wsum(acc.dlen), ml = wmax(acc.maxlast);
+    const int inv = wmax(acc.inval);
     if (lane_id() == 0) {
-        fold_row(d, ol, dping, ddc, napp, nref, ev);
+        fold_row(d, ol, dping, ddc, napp, nref, ev, dl, ml, inv);
         if (np) atomicAdd(&d.ctr[C_X_MERGED], (unsigned long long)np);
         if (napp) atomicAdd(&d.ctr[C_X_APPLIED], (unsigned long long)napp);
     }
@@ -268,7 +299,11 @@ __device__ bool wave_snapshot(const DS &d, uint32_t ol, uint32_t o, MsgDesc &out
         known += ((v.x & 7u) != ST_UNKNOWN) + ((v.y & 7u) != ST_UNKNOWN) + ((v.z & 7u) != ST_UNKNOWN) + ((v.w & 7u) != ST_UNKNOWN);
     }
     known = wsum(known);
-    if (lane_id() == 0) d.dense_meta[slot] = make_uint4(o, d.mw[(size_t)ol * d.NP + o] >> 3, (uint32_t)known, 0);
+    if (lane_id() == 0) {
+        d.dense_meta[slot] = make_uint4(o, d.mw[(size_t)ol * d.NP + o] >> 3, (uint32_t)known, 0);
+        d.dense_len[slot] = d.clen[ol];
+        d.dense_last[slot] = d.clast[ol];
+    }
     out.kind = 1; out.off_lo = slot; out.len = (uint32_t)known;
     return true;
 }
@@ -293,6 +328,9 @@ __global__ void k_init_rows(DS d, int mode, uint32_t e0) {
     for (uint32_t b = lane_id(); b < d.NBW; b += 64) d.dblk[(size_t)ol * d.NBW + b] = 0;
     if (lane_id() == 0) {
         const int32_t p = mode == 0 ? (int32_t)d.N - 1 : 0;
+        const uint32_t rl = (uint32_t)reclen(d, ST_ALIVE, e0);
+        d.clen[ol] = mode == 0 ? rl * d.N : rl;
+        d.clast[ol] = mode == 0 ? (int32_t)d.N - 1 : (int32_t)o;
         d.ping[ol] = p;
         d.maxp[ol] = mode == 0 ? (int32_t)d.pfactor * digits10(p) : (int32_t)d.pfactor;
         d.dcnt[ol] = 0;
@@ -308,15 +346,20 @@ __global__ void k_init_rows(DS d, int mode, uint32_t e0) {
 // recount pingable/changes of one row after raw writes (NumPingableMembers, memberlist.go:188-198)
 __global__ void k_recount(DS d, uint32_t ol) {
     const uint32_t o = d.lo + ol;
-    int p = 0, c = 0;
+    int p = 0, c = 0, len = 0, last = -1;
     for (uint32_t m = lane_id(); m < d.N; m += 64) {
         const size_t idx = (size_t)ol * d.NP + m;
-        if (m != o && is_pingable(d.mw[idx] & 7u)) p++;
+        const uint32_t w = d.mw[idx];
+        if (m != o && is_pingable(w & 7u)) p++;
         if (d.dp[idx] != DP_NONE) c++;
+        len += reclen(d, w & 7u, w >> 3);
+        if ((w & 7u) < 4u) last = (int)m;
     }
     p = wsum(p);
     c = wsum(c);
-    if (lane_id() == 0) { d.ping[ol] = p; d.dcnt[ol] = c; d.dirty[ol] = 1; }
+    len = wsum(len);
+    last = wmax(last);
+    if (lane_id() == 0) { d.ping[ol] = p; d.dcnt[ol] = c; d.dirty[ol] = 1; d.clen[ol] = (uint32_t)len; d.clast[ol] = last; }
 }
 
 __global__ void k_clear_changes(DS d, uint32_t ol) {
@@ -332,7 +375,7 @@ __device__ void thread_make_change(const DS &d, uint32_t ol, uint32_t o, uint32_
     MAcc acc;
     const uint32_t self_e = d.mw[(size_t)ol * d.NP + o] >> 3;   // MakeChange: SourceIncarnation = local inc
     merge_change(d, ol, o, m, st, e, o, self_e, r, r, acc);
-    fold_row(d, ol, acc.dping, acc.ddc, acc.napp, acc.nref, 0);
+    fold_row(d, ol, acc.dping, acc.ddc, acc.napp, acc.nref, 0, acc.dlen, acc.maxlast, acc.inval);
 }
 
 __global__ void k_events(DS d, const uint4 *ev, uint32_t nev, uint32_t r, uint32_t *applied_out) {
@@ -375,37 +418,47 @@ __global__ void k_timers(DS d, uint32_t r) {
     if (!d.live[o] || d.tmin[ol] > r) return;
     const uint32_t self_e = d.mw[(size_t)ol * d.NP + o] >> 3;
     MAcc acc;
-    uint32_t newmin = NO_DEADLINE;
+    uint32_t newmin = NO_DEADLINE;   // per-lane partial minimum, reduced at the end
     int fired = 0;
-    for (uint32_t b = 0; b < d.NB; b++) {
-        const uint32_t bm = d.tblk[(size_t)ol * d.NB + b];
-        if (bm > r) { newmin = min(newmin, bm); continue; }
-        const uint32_t m = (b << 6) + lane_id();
-        const size_t idx = (size_t)ol * d.NP + m;
-        const uint8_t ts = d.tst[idx];
-        const uint32_t state = ts & 7u;
-        uint4 a = d.aux[idx];
-        if (state && !(ts & 0x80) && a.z <= r) {
-            d.tst[idx] = ts | 0x80;                                 // fired; the entry stays
-            fired++;
-            if (state == ST_SUSPECT) merge_change(d, ol, o, m, ST_FAULTY, a.w, o, self_e, r, a.z, acc);  // MakeFaulty
-            else if (state == ST_FAULTY) merge_change(d, ol, o, m, ST_TOMB, a.w, o, self_e, r, a.z, acc); // MakeTombstone
-            else {                                                  // Evict (memberlist.go:271-279)
-                const uint32_t w = d.mw[idx];
-                if ((w & 7u) != ST_UNKNOWN && m != o) {
-                    if (is_pingable(w & 7u)) acc.dping--;
-                    d.mw[idx] = (w & ~7u) | ST_UNKNOWN;
-                    acc.evict++;
+    for (uint32_t b0 = 0; b0 < d.NB; b0 += 64) {
+        // 64 block lower bounds per wave-instruction; only blocks with a due deadline are scanned
+        const uint32_t bl = b0 + lane_id();
+        const uint32_t bm = bl < d.NB ? d.tblk[(size_t)ol * d.NB + bl] : NO_DEADLINE;
+        unsigned long long due = __ballot(bm <= r);
+        if (bm > r) newmin = min(newmin, bm);
+        while (due) {
+            const uint32_t bb = __ffsll((long long)due) - 1;
+            due &= due - 1;
+            const uint32_t b = b0 + bb;
+            const uint32_t m = (b << 6) + lane_id();
+            const size_t idx = (size_t)ol * d.NP + m;
+            const uint8_t ts = d.tst[idx];
+            const uint32_t state = ts & 7u;
+            uint4 a = d.aux[idx];
+            if (state && !(ts & 0x80) && a.z <= r) {
+                d.tst[idx] = ts | 0x80;                             // fired; the entry stays
+                fired++;
+                if (state == ST_SUSPECT) merge_change(d, ol, o, m, ST_FAULTY, a.w, o, self_e, r, a.z, acc);   // MakeFaulty
+                else if (state == ST_FAULTY) merge_change(d, ol, o, m, ST_TOMB, a.w, o, self_e, r, a.z, acc); // MakeTombstone
+                else {                                              // Evict (memberlist.go:271-279)
+                    const uint32_t w = d.mw[idx];
+                    if ((w & 7u) != ST_UNKNOWN && m != o) {
+                        if (is_pingable(w & 7u)) acc.dping--;
+                        d.mw[idx] = (w & ~7u) | ST_UNKNOWN;
+                        track_len(d, ol, m, w, (w & ~7u) | ST_UNKNOWN, acc);
+                        acc.evict++;
+                    }
                 }
+                a = d.aux[idx];
             }
-            a = d.aux[idx];
+            const uint8_t ts2 = d.tst[idx];
+            const uint32_t v = ((ts2 & 7u) && !(ts2 & 0x80)) ? a.z : NO_DEADLINE;
+            const uint32_t bmin = wmin(v);
+            if (lane_id() == 0) d.tblk[(size_t)ol * d.NB + b] = bmin;
+            newmin = min(newmin, bmin);
         }
-        const uint8_t ts2 = d.tst[idx];
-        const uint32_t v = ((ts2 & 7u) && !(ts2 & 0x80)) ? a.z : NO_DEADLINE;
-        const uint32_t bmin = wmin(v);
-        if (lane_id() == 0) d.tblk[(size_t)ol * d.NB + b] = bmin;
-        newmin = min(newmin, bmin);
     }
+    newmin = wmin(newmin);
     if (lane_id() == 0) d.tmin[ol] = newmin;
     fired = wsum(fired);
     if (lane_id() == 0 && fired) atomicAdd(&d.ctr[C_TIMERS_FIRED], (unsigned long long)fired);
@@ -610,39 +663,44 @@ struct RecvArgs {
     const MsgDesc *sdesc;                           // sender snapshots (by sender row)
     const uint32_t *sI, *sC;
     MsgDesc *rdesc;                                 // responses (by sender row / (row, slot))
-    uint4 *defer;
+    uint4 *defer;                                   // {resp index, dense slot, sender checksum, pair index}
     uint32_t *defer_cnt;
+    uint8_t *fsflag;                                // per inbox pair: the receiver answered with a full sync
     uint32_t r;
 };
 
-__device__ void recv_one(const DS &d, const RecvArgs &a, uint32_t j, uint32_t sender_row, uint32_t resp_idx) {
+// the full-sync branch of IssueAsReceiver (disseminator.go:161-180): taken iff the filtered list is
+// empty and checksums differ. A dirty receiver snapshots its row (the full-sync payload) and the
+// decision waits for one batched checksum of all snapshots after the last wave. Reverse full syncs
+// are queued afterwards in inbox order (k_build_jobs).
+__device__ void recv_one(const DS &d, const RecvArgs &a, uint32_t j, uint32_t sender_row, uint32_t resp_idx,
+                         uint32_t pair) {
     const uint32_t ol = j - d.lo;
     const uint32_t sender = d.lo + sender_row;
     wave_merge_msg(d, ol, j, a.sdesc[sender_row], a.r, a.r);
     MsgDesc resp;
     const uint32_t kept = wave_issue_recv(d, ol, sender, a.sI[sender_row], resp);
     if (kept == 0) {
-        if (d.dirty[ol]) {                                          // checksum needed first
-            if (lane_id() == 0) a.defer[atomicAdd(a.defer_cnt, 1u)] = make_uint4(ol, resp_idx, sender, a.sC[sender_row]);
+        const uint32_t scs = a.sC[sender_row];
+        if (d.dirty[ol]) {
+            if (wave_snapshot(d, ol, j, resp) && lane_id() == 0)
+                a.defer[atomicAdd(a.defer_cnt, 1u)] = make_uint4(resp_idx, resp.off_lo, scs, pair);
             resp.kind = 2;
-        } else if (d.cs[ol] != a.sC[sender_row]) {                  // full sync
+        } else if (d.cs[ol] != scs) {
             wave_snapshot(d, ol, j, resp);
             if (lane_id() == 0) {
-                if (a.phase == 0) {
-                    atomicAdd(&d.ctr[C_FULL_SYNCS], 1ull);
-                    if (d.njobs[ol] < d.maxjobs) d.jobs[(size_t)ol * d.maxjobs + d.njobs[ol]++] = sender;
-                    else atomicAdd(&d.ctr[C_RFS_OMITTED], 1ull);
-                } else {
-                    atomicAdd(&d.ctr[C_FULL_SYNCS_PINGREQ], 1ull);
-                }
+                if (a.phase == 0) a.fsflag[pair] = 1;
+                atomicAdd(&d.ctr[a.phase == 0 ? C_FULL_SYNCS : C_FULL_SYNCS_PINGREQ], 1ull);
             }
         }
     }
     if (lane_id() == 0) {
         a.rdesc[resp_idx] = resp;
         if (resp.kind != 2) atomicAdd(&d.ctr[C_MSG_CHANGES], (unsigned long long)resp.len);
-        if (a.phase == 1) atomicAdd(&d.ctr[C_HELPER_CALLS], 1ull);
-        atomicAdd(&d.ctr[C_MSG_CHANGES], (unsigned long long)a.sdesc[sender_row].len * (a.phase == 1));
+        if (a.phase == 1) {
+            atomicAdd(&d.ctr[C_HELPER_CALLS], 1ull);
+            atomicAdd(&d.ctr[C_MSG_CHANGES], (unsigned long long)a.sdesc[sender_row].len);
+        }
     }
 }
 
@@ -651,37 +709,60 @@ __global__ void k_recv(DS d, RecvArgs a) {
     if (u >= a.nruns_max) return;
     const uint32_t key = a.ukeys[u];
     if (key >= d.N || a.counts[u] <= a.w) return;
-    const uint32_t v = a.vals[a.offs[u] + a.w];
-    if (a.phase == 0) recv_one(d, a, key, v - d.lo, v - d.lo);
+    const uint32_t pair = a.offs[u] + a.w;
+    const uint32_t v = a.vals[pair];
+    if (a.phase == 0) recv_one(d, a, key, v - d.lo, v - d.lo, pair);
     else {
         const uint32_t o = v / d.K, q = v % d.K;
-        recv_one(d, a, key, o - d.lo, (o - d.lo) * d.K + q);
+        recv_one(d, a, key, o - d.lo, (o - d.lo) * d.K + q, pair);
     }
 }
 
-// second half of IssueAsReceiver for receivers whose checksum had to be recomputed first
-__global__ void k_recv_finish(DS d, const uint4 *defer, const uint32_t *defer_cnt, MsgDesc *rdesc, int phase) {
-    const uint32_t i = wave_gid();
+// resolve deferred full-sync decisions once the snapshot checksums exist (phase 2 = heal ping:
+// the job is queued at once; heal runs in phase E, before any phase-D job of the round)
+__global__ void k_recv_finish(DS d, const uint4 *defer, const uint32_t *defer_cnt, MsgDesc *rdesc, int phase,
+                              uint8_t *fsflag) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= *defer_cnt) return;
     const uint4 e = defer[i];
-    const uint32_t ol = e.x;
+    const uint32_t slot = e.y;
     MsgDesc resp;
     resp.kind = 0; resp.len = 0; resp.off_lo = resp.off_hi = 0;
-    if (d.cs[ol] != e.w) {
-        wave_snapshot(d, ol, d.lo + ol, resp);
-        if (lane_id() == 0) {
-            if (phase != 1) {
-                atomicAdd(&d.ctr[C_FULL_SYNCS], 1ull);
-                if (d.njobs[ol] < d.maxjobs) d.jobs[(size_t)ol * d.maxjobs + d.njobs[ol]++] = e.z;
-                else atomicAdd(&d.ctr[C_RFS_OMITTED], 1ull);
-            } else {
-                atomicAdd(&d.ctr[C_FULL_SYNCS_PINGREQ], 1ull);
-            }
+    if (d.dense_cs[slot] != e.z) {
+        resp.kind = 1; resp.off_lo = slot; resp.len = d.dense_meta[slot].z;
+        atomicAdd(&d.ctr[phase == 1 ? C_FULL_SYNCS_PINGREQ : C_FULL_SYNCS], 1ull);
+        if (phase == 2) {
+            const uint32_t ol = d.dense_meta[slot].x - d.lo;
+            if (d.njobs[ol] < d.maxjobs) d.jobs[(size_t)ol * d.maxjobs + d.njobs[ol]++] = e.w;
+            else atomicAdd(&d.ctr[C_RFS_OMITTED], 1ull);
+        } else if (phase == 0) {
+            fsflag[e.w] = 1;
         }
     }
-    if (lane_id() == 0) {
-        rdesc[e.y] = resp;
-        if (phase != 2) atomicAdd(&d.ctr[C_MSG_CHANGES], (unsigned long long)resp.len);
+    rdesc[e.x] = resp;
+    if (phase != 2) atomicAdd(&d.ctr[C_MSG_CHANGES], (unsigned long long)resp.len);
+}
+
+// defer list → checksum list of dense-snapshot ids (NL + slot)
+__global__ void k_defer_ids(DS d, const uint4 *defer, const uint32_t *defer_cnt, uint32_t *list, uint32_t *cnt) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t n = *defer_cnt;
+    if (i == 0) *cnt = n;
+    if (i < n) list[i] = d.NL + defer[i].y;
+}
+
+// tryStartReverseFullSync (disseminator.go:257-278) in inbox order: at most maxjobs per receiver
+__global__ void k_build_jobs(DS d, const uint32_t *ukeys, const uint32_t *counts, const uint32_t *offs,
+                             const uint32_t *vals, uint32_t nruns, uint8_t *fsflag) {
+    const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= nruns || ukeys[u] >= d.N) return;
+    const uint32_t ol = ukeys[u] - d.lo;
+    for (uint32_t w = 0; w < counts[u]; w++) {
+        const uint32_t p = offs[u] + w;
+        if (!fsflag[p]) continue;
+        fsflag[p] = 0;
+        if (d.njobs[ol] < d.maxjobs) d.jobs[(size_t)ol * d.maxjobs + d.njobs[ol]++] = vals[p];
+        else atomicAdd(&d.ctr[C_RFS_OMITTED], 1ull);
     }
 }
 
@@ -759,10 +840,25 @@ __global__ void k_jobs_reset(DS d, uint8_t *need) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// phase C: checksum (memberlist.go:83-128) — one lane per row, FarmHash-32 mk chain over the
-// byte stream addr ‖ status ‖ decimal(inc) ‖ ';' of every non-tombstone member in index order
-// (fixed-width ascending addresses make the sort order == index order)
+// phase C: checksum (memberlist.go:83-128): FarmHash-32 mk (go-farm Fingerprint32) over the byte
+// stream addr ‖ status ‖ decimal(inc) ‖ ';' of every non-tombstone member in index order (fixed-width
+// ascending addresses make the sorted order the index order).
+//
+// The chain is sequential within a row, so its latency sets the time of a launch. One
+// workgroup takes 64 rows. Wave 0 is the hasher: one lane per row, and it does only the FarmHash
+// block function on 20-byte blocks read from LDS. Waves 1-4 are formatters: they build the byte
+// stream of the same 64 rows into a per-row LDS ring, CS_CHUNK members ahead of the hasher, with one
+// workgroup barrier per chunk. The string length and the last record (the hash prologue) come
+// from per-row values maintained by the merges.
 // ---------------------------------------------------------------------------------------------
+constexpr int CS_ROWS = 64;                     // rows per workgroup (one lane per row in every wave)
+constexpr int CS_RPL = 4;                       // records per formatter lane per chunk
+constexpr int CS_CHUNK = 2 * CS_RPL;            // members per chunk (2 formatter waves)
+constexpr int CS_SUPER = 32;                    // members per staged superchunk (4 chunks)
+constexpr int CS_STG = 36;                      // staged words per row (32 + pad: conflict-free ds_read_b128)
+constexpr int CS_RING = 185;                    // ring words per row: >= 2 chunks + a block; a multiple of 5
+constexpr int CS_RW = 11;                       // record words (<= 44 bytes: 20 B address + 24 B tail)
+
 template <int W, int RW>
 __device__ __forceinline__ void build_rec(uint32_t (&R)[RW], const uint32_t *A, const uint32_t (&T)[6]) {
     constexpr int wW = W / 4, bW = W % 4;
@@ -790,153 +886,249 @@ __device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t sh
     return (uint32_t)((((uint64_t)hi << 32) | lo) >> sh_bits);
 }
 
-template <int W, int RW, int NBM>
-__global__ void __launch_bounds__(256) k_checksum(DS d, const uint32_t *list, const uint32_t *count) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= *count) return;
-    const uint32_t ol = list[i];
-    const uint32_t *row = d.mw + (size_t)ol * d.NP;
-    const uint32_t *tail = d.tailw;
-    const uint32_t ecap = d.ecap;
-    // pass 1: total length and the last included member
-    uint32_t len = 0;
-    int32_t last = -1;
-    bool bad_e = false;
-    for (uint32_t m = 0; m < d.N; m += 4) {
-        const uint4 w4 = *(const uint4 *)(row + m);
-        const uint32_t ws[4] = {w4.x, w4.y, w4.z, w4.w};
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint32_t st = ws[k] & 7u, e = ws[k] >> 3;
-            if (st < 4u && m + k < d.N) {
-                bad_e |= e >= ecap;
-                const uint32_t te = e < ecap ? e : 0u;
-                len += W + tail[((size_t)te * 4 + st) * 8 + 6];
-                last = (int32_t)(m + k);
-            }
-        }
-    }
-    if (bad_e) atomicOr(d.err, E_ECAP);
-    if (len <= 24 || last < 0) {
-        atomicOr(d.err, E_SHORT);
-        d.cs[ol] = 0;
-        d.dirty[ol] = 0;
-        return;
-    }
-    // prologue: the last 20 bytes come from the last record
-    FH fh;
-    {
-        const uint32_t w = row[last], st = w & 7u, e = min(w >> 3, ecap - 1);
-        const uint32_t *tp = tail + ((size_t)e * 4 + st) * 8;
-        uint32_t T[6] = {tp[0], tp[1], tp[2], tp[3], tp[4], tp[5]};
-        uint32_t R[RW + 1];
-        uint32_t Rr[RW];
-        build_rec<W, RW>(Rr, d.addrw + (size_t)last * 6, T);
-#pragma unroll
-        for (int k = 0; k < RW; k++) R[k] = Rr[k];
-        R[RW] = 0;
-        const uint32_t L = W + tp[6], q = L - 20, qw = q >> 2, qb = (q & 3u) * 8u;
-        uint32_t t[5];
-#pragma unroll
-        for (int k = 0; k < 5; k++) {
-            uint32_t lo = 0, hi = 0;
-#pragma unroll
-            for (int s = 0; s <= RW; s++) {
-                lo = ((uint32_t)s == qw + k) ? R[s] : lo;
-                hi = ((uint32_t)s == qw + k + 1) ? R[s] : hi;
-            }
-            t[k] = funnel(hi, lo, qb);
-        }
-        fh.init(len, t[0], t[1], t[2], t[3], t[4]);
-    }
-    const uint32_t iters = (len - 1) / 20;
-    uint32_t done = 0, c = 0;
-    uint32_t P0 = 0, P1 = 0, P2 = 0, P3 = 0, P4 = 0;
-    constexpr int NS = (RW + 6 > 5 * NBM + 5) ? RW + 6 : 5 * NBM + 5;
-    for (uint32_t m = 0; m < d.N; m += 4) {
-        const uint4 w4 = *(const uint4 *)(row + m);
-        const uint32_t ws[4] = {w4.x, w4.y, w4.z, w4.w};
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint32_t mm = m + k;
-            const uint32_t st = ws[k] & 7u, e = ws[k] >> 3;
-            const bool inc = st < 4u && mm < d.N;
-            const uint32_t te = (e < ecap) ? e : 0u;
-            const uint32_t *tp = tail + ((size_t)te * 4 + (st & 3u)) * 8;
-            const uint4 ta = *(const uint4 *)tp;
-            const uint4 tb = *(const uint4 *)(tp + 4);
-            uint32_t T[6] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y};
-            const uint32_t L = inc ? W + tb.z : 0u;
-            uint32_t R[RW];
-            build_rec<W, RW>(R, d.addrw + (size_t)(mm < d.N ? mm : 0) * 6, T);
-            if (!inc) {
-#pragma unroll
-                for (int z = 0; z < RW; z++) R[z] = 0;
-            }
-            // byte shift by c & 3
-            const uint32_t cb = (c & 3u) * 8u;
-            uint32_t S[NS];
-            S[0] = funnel(R[0], 0u, 32u - cb);
-#pragma unroll
-            for (int z = 1; z < RW; z++) S[z] = funnel(R[z], R[z - 1], 32u - cb);
-            S[RW] = funnel(0u, R[RW - 1], 32u - cb);
-#pragma unroll
-            for (int z = RW + 1; z < NS; z++) S[z] = 0u;
-            // word shift by c >> 2 (0..4): 3-stage barrel shifter
-            const uint32_t cw = c >> 2;
-#pragma unroll
-            for (int z = NS - 1; z >= 0; z--) S[z] = (cw & 1u) ? (z >= 1 ? S[z - 1] : 0u) : S[z];
-#pragma unroll
-            for (int z = NS - 1; z >= 0; z--) S[z] = (cw & 2u) ? (z >= 2 ? S[z - 2] : 0u) : S[z];
-#pragma unroll
-            for (int z = NS - 1; z >= 0; z--) S[z] = (cw & 4u) ? (z >= 4 ? S[z - 4] : 0u) : S[z];
-            S[0] |= P0; S[1] |= P1; S[2] |= P2; S[3] |= P3; S[4] |= P4;
-            const uint32_t T2 = c + L;
-            const uint32_t nb = T2 / 20u;
-#pragma unroll
-            for (int bi = 0; bi < NBM; bi++) {
-                if ((uint32_t)bi < nb && done < iters) {
-                    fh.block(S[5 * bi], S[5 * bi + 1], S[5 * bi + 2], S[5 * bi + 3], S[5 * bi + 4]);
-                    done++;
-                }
-            }
-            uint32_t Q0 = S[0], Q1 = S[1], Q2 = S[2], Q3 = S[3], Q4 = S[4];
-#pragma unroll
-            for (int bi = 1; bi <= NBM; bi++) {
-                const bool sel = nb == (uint32_t)bi;
-                Q0 = sel ? S[5 * bi] : Q0;
-                Q1 = sel ? S[5 * bi + 1] : Q1;
-                Q2 = sel ? S[5 * bi + 2] : Q2;
-                Q3 = sel ? S[5 * bi + 3] : Q3;
-                Q4 = sel ? S[5 * bi + 4] : Q4;
-            }
-            P0 = Q0; P1 = Q1; P2 = Q2; P3 = Q3; P4 = Q4;
-            c = T2 - 20u * nb;
-        }
-    }
-    d.cs[ol] = fh.fin();
-    d.dirty[ol] = 0;
-    atomicAdd(&d.ctr[C_X_CS_ROWS], 1ull);
+// record words of member m (member word w); returns the record length (0 = not in the string)
+template <int W>
+__device__ __forceinline__ uint32_t record(const DS &d, uint32_t m, uint32_t w, uint32_t (&R)[CS_RW]) {
+    const uint32_t st = w & 7u, e = min(w >> 3, d.ecap - 1);
+    const uint32_t *tp = d.tailw + ((size_t)e * 4 + (st & 3u)) * 8;
+    const uint4 ta = *(const uint4 *)tp;
+    const uint4 tb = *(const uint4 *)(tp + 4);
+    const uint32_t T[6] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y};
+    build_rec<W, CS_RW>(R, d.addrw + (size_t)m * 6, T);
+    return (st < 4u && m < d.N) ? W + tb.z : 0u;
 }
 
-template __global__ void k_checksum<19, 10, 2>(DS, const uint32_t *, const uint32_t *);
+// write one record at stream byte position pos into the row's ring (aligned b32 stores; the two
+// partial edge words, shared with the neighbouring records, are written bytewise)
+__device__ __forceinline__ void put_record(uint32_t *ring, const uint32_t (&R)[CS_RW], uint32_t L, uint32_t pos) {
+    if (L == 0) return;
+    const uint32_t b = pos & 3u, rb = (4u - b) & 3u, q0 = (pos + 3u) >> 2;
+    uint32_t wq = q0 % CS_RING;
+    if (rb) {
+        uint8_t *p = (uint8_t *)(ring + (wq == 0 ? CS_RING - 1 : wq - 1)) + b;
+        for (uint32_t i = 0; i < rb; i++) p[i] = (uint8_t)(R[0] >> (8 * i));
+    }
+    const uint32_t nfull = (L - rb) >> 2, sh = rb * 8u;
+    uint32_t tailw = 0;
+#pragma unroll
+    for (int i = 0; i < CS_RW; i++) {
+        const uint32_t v = funnel(i + 1 < CS_RW ? R[i + 1] : 0u, R[i], sh);
+        if ((uint32_t)i < nfull) {
+            ring[wq] = v;
+            wq = (wq + 1 == CS_RING) ? 0u : wq + 1;
+        }
+        tailw = ((uint32_t)i == nfull) ? v : tailw;
+    }
+    const uint32_t rl = L - rb - 4u * nfull;
+    uint8_t *p = (uint8_t *)(ring + wq);
+    for (uint32_t i = 0; i < rl; i++) p[i] = (uint8_t)(tailw >> (8 * i));
+}
 
-#define CS_GENERIC(Wv) template __global__ void k_checksum<Wv, 12, 3>(DS, const uint32_t *, const uint32_t *);
-CS_GENERIC(13) CS_GENERIC(14) CS_GENERIC(15) CS_GENERIC(16) CS_GENERIC(17) CS_GENERIC(18) CS_GENERIC(19)
-CS_GENERIC(20)
+// h-chain and (g,f)-chain halves of the FarmHash-32 mk block function; h never reads g or f
+__device__ __forceinline__ void fh_block_h(uint32_t &h, uint32_t a, uint32_t dd, uint32_t e) {
+    h += a;
+    h = fh_mur(dd, h) + e;
+}
+__device__ __forceinline__ void fh_block_gf(uint32_t &g, uint32_t &f, uint32_t a, uint32_t b, uint32_t c, uint32_t dd,
+                                            uint32_t e) {
+    g += b; f += c;
+    g = fh_mur(c, g) + a;
+    f = fh_mur(b + e * FH_C1, f) + dd;
+    f += g; g += f;
+}
+
+// MODE 0: normal; 1: hashers only (formatters stage but do not write the ring); 2: formatters only
+template <int W, int MODE>
+__global__ void __launch_bounds__(256) k_checksum(DS d, const uint32_t *list, const uint32_t *count) {
+    __shared__ uint32_t ring[CS_ROWS * CS_RING];
+    __shared__ __attribute__((aligned(16))) uint32_t stage[2][CS_ROWS * CS_STG];
+    __shared__ uint32_t wp[2][CS_ROWS];
+    __shared__ uint32_t xgf[2][CS_ROWS];
+    const uint32_t cnt = *count;
+    if (blockIdx.x * CS_ROWS >= cnt) return;                       // uniform per workgroup
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t gi = blockIdx.x * CS_ROWS + lane;
+    const bool valid = gi < cnt;
+    const uint32_t id = list[valid ? gi : blockIdx.x * CS_ROWS];
+    const bool is_row = id < d.NL;
+    const uint32_t *row = is_row ? d.mw + (size_t)id * d.NP : d.dense + (size_t)(id - d.NL) * d.NP;
+    uint32_t *myring = ring + lane * CS_RING;
+    const uint32_t nch = (d.N + CS_CHUNK - 1) / CS_CHUNK;
+    const uint32_t nsup = (d.N + CS_SUPER - 1) / CS_SUPER;
+
+    // formatter lanes cooperatively stage 32-member superchunks of all 64 rows (coalesced 16 B pieces:
+    // 8 consecutive lanes cover one row's 128 B); the next superchunk is in flight in registers
+    const uint32_t fl = threadIdx.x - 128;                         // formatter lane 0..127
+    uint4 pre[4];
+    auto stage_rows = [&](uint32_t sup, uint4 (&v)[4]) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t q = fl + 128u * k, r = q >> 3, part = q & 7u;
+            const uint32_t gr = blockIdx.x * CS_ROWS + r;
+            const uint32_t rid = list[gr < cnt ? gr : blockIdx.x * CS_ROWS];
+            const uint32_t *rp = rid < d.NL ? d.mw + (size_t)rid * d.NP : d.dense + (size_t)(rid - d.NL) * d.NP;
+            const uint32_t m0 = sup * CS_SUPER + part * 4;
+            v[k] = m0 < d.NP ? *(const uint4 *)(rp + m0) : make_uint4(ST_UNKNOWN, ST_UNKNOWN, ST_UNKNOWN, ST_UNKNOWN);
+        }
+    };
+    auto stage_store = [&](uint32_t buf, const uint4 (&v)[4]) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t q = fl + 128u * k, r = q >> 3, part = q & 7u;
+            *(uint4 *)&stage[buf][r * CS_STG + part * 4] = v[k];
+        }
+    };
+    if (wave >= 2) {
+        stage_rows(0, pre);
+        stage_store(0, pre);
+        if (nsup > 1) stage_rows(1, pre);
+    }
+    __syncthreads();
+
+    if (wave <= 1) {
+        // ---------------- hashers: wave 0 runs the h chain, wave 1 the (g, f) chains ----------------
+        const uint32_t len = is_row ? d.clen[id] : d.dense_len[id - d.NL];
+        int32_t last = is_row ? d.clast[id] : d.dense_last[id - d.NL];
+        if (last < 0) {                                            // invalidated: rescan from the end
+            last = -1;
+            for (int32_t m = (int32_t)d.N - 1; m >= 0; m--)
+                if ((row[m] & 7u) < 4u) { last = m; break; }
+        }
+        const bool ok = len > 24 && last >= 0;
+        if (!ok && valid && wave == 0) atomicOr(d.err, E_SHORT);
+        FH fh{0, 0, 0};
+        {
+            uint32_t R[CS_RW];
+            const uint32_t L = record<W>(d, (uint32_t)max(last, 0), row[max(last, 0)], R);
+            const uint32_t q = L >= 20 ? L - 20 : 0, qw = q >> 2, qb = (q & 3u) * 8u;
+            uint32_t t[5];
+#pragma unroll
+            for (int k = 0; k < 5; k++) {
+                uint32_t lo = 0, hi = 0;
+#pragma unroll
+                for (int s = 0; s < CS_RW; s++) {
+                    lo = ((uint32_t)s == qw + k) ? R[s] : lo;
+                    hi = ((uint32_t)s == qw + k + 1) ? R[s] : hi;
+                }
+                t[k] = funnel(hi, lo, qb);
+            }
+            fh.init(len, t[0], t[1], t[2], t[3], t[4]);
+        }
+        uint32_t h = fh.h, g = fh.g, f = fh.f;
+        const uint32_t iters = ok ? (len - 1) / 20 : 0;
+        uint32_t done = 0, rq = 0, avail = 0;
+        for (uint32_t t = 0; t <= nch; t++) {
+            const uint32_t lim = MODE == 2 ? 0u : (MODE == 1 ? min(iters, t * 15u) : min(iters, avail));
+            if (wave == 0) {
+                while (__any(done < lim)) {
+                    if (done < lim) {
+                        const uint32_t *p = myring + rq;
+                        fh_block_h(h, p[0], p[3], p[4]);
+                        done++;
+                        rq = (rq + 5 == CS_RING) ? 0u : rq + 5;
+                    }
+                }
+            } else {
+                while (__any(done < lim)) {
+                    if (done < lim) {
+                        const uint32_t *p = myring + rq;
+                        fh_block_gf(g, f, p[0], p[1], p[2], p[3], p[4]);
+                        done++;
+                        rq = (rq + 5 == CS_RING) ? 0u : rq + 5;
+                    }
+                }
+            }
+            __syncthreads();
+            avail = wp[t & 1][lane] / 20;
+        }
+        const uint32_t fin_lim = MODE == 2 ? 0u : iters;
+        while (__any(done < fin_lim)) {
+            if (done < fin_lim) {
+                const uint32_t *p = myring + rq;
+                if (wave == 0) fh_block_h(h, p[0], p[3], p[4]);
+                else fh_block_gf(g, f, p[0], p[1], p[2], p[3], p[4]);
+                done++;
+                rq = (rq + 5 == CS_RING) ? 0u : rq + 5;
+            }
+        }
+        if (wave == 1) { xgf[0][lane] = g; xgf[1][lane] = f; }
+        __syncthreads();
+        if (wave == 0 && valid) {
+            fh.h = h; fh.g = xgf[0][lane]; fh.f = xgf[1][lane];
+            const uint32_t hv = ok ? fh.fin() : 0u;
+            if (is_row) {
+                d.cs[id] = hv;
+                d.dirty[id] = 0;
+                atomicAdd(&d.ctr[C_X_CS_ROWS], 1ull);
+            } else {
+                d.dense_cs[id - d.NL] = hv;
+            }
+        }
+    } else {
+        // ---------------- formatters: wave 2 takes records 0-3 of each chunk, wave 3 records 4-7 ----------------
+        const uint32_t fw = wave - 2;
+        uint32_t S = 0;                                            // stream bytes before this chunk
+        for (uint32_t t = 0; t <= nch; t++) {
+            if (t < nch) {
+                const uint32_t sup = t / (CS_SUPER / CS_CHUNK), cs_ = t % (CS_SUPER / CS_CHUNK);
+                const uint32_t *sp = &stage[sup & 1][lane * CS_STG + cs_ * CS_CHUNK];
+                const uint4 va = *(const uint4 *)sp, vb = *(const uint4 *)(sp + 4);
+                const uint32_t ws[CS_CHUNK] = {va.x, va.y, va.z, va.w, vb.x, vb.y, vb.z, vb.w};
+                const uint32_t mb = t * CS_CHUNK;
+                uint32_t pre_len = 0, tot = 0;
+#pragma unroll
+                for (int k = 0; k < CS_CHUNK; k++) {
+                    const uint32_t l = (mb + k < d.N) ? (uint32_t)reclen(d, ws[k] & 7u, ws[k] >> 3) : 0u;
+                    pre_len += ((uint32_t)k < fw * CS_RPL) ? l : 0u;
+                    tot += l;
+                }
+                uint32_t pos = S + pre_len;
+                uint32_t R[CS_RPL][CS_RW], L[CS_RPL];
+#pragma unroll
+                for (int j = 0; j < CS_RPL; j++) {
+                    const uint32_t wk = fw ? ws[CS_RPL + j] : ws[j];
+                    L[j] = record<W>(d, mb + fw * CS_RPL + j, wk, R[j]);
+                }
+#pragma unroll
+                for (int j = 0; j < CS_RPL; j++) {
+                    if (MODE != 1) put_record(myring, R[j], L[j], pos);
+                    pos += L[j];
+                }
+                S += tot;
+                if (fw == 0) wp[t & 1][lane] = S;
+                // double-buffered staging: store the prefetched superchunk at the end of this one
+                if (cs_ == CS_SUPER / CS_CHUNK - 1 && sup + 1 < nsup) {
+                    stage_store((sup + 1) & 1, pre);
+                    if (sup + 2 < nsup) stage_rows(sup + 2, pre);
+                }
+            }
+            __syncthreads();
+        }
+        __syncthreads();
+    }
+}
+
+#define CS_INST(Wv) template __global__ void k_checksum<Wv, 0>(DS, const uint32_t *, const uint32_t *);
+CS_INST(13) CS_INST(14) CS_INST(15) CS_INST(16) CS_INST(17) CS_INST(18) CS_INST(19) CS_INST(20)
 
 void launch_checksum(const DS &d, const uint32_t *list, const uint32_t *count, uint32_t maxn, bool fast, hipStream_t s) {
-    const uint32_t grid = (maxn + 255) / 256;
+    (void)fast;
+    const uint32_t grid = (maxn + CS_ROWS - 1) / CS_ROWS;
     if (grid == 0) return;
-    if (fast && d.W == 19) {
-        hipLaunchKernelGGL((k_checksum<19, 10, 2>), dim3(grid), dim3(256), 0, s, d, list, count);
-        return;
-    }
     switch (d.W) {
-#define CS_CASE(Wv) case Wv: hipLaunchKernelGGL((k_checksum<Wv, 12, 3>), dim3(grid), dim3(256), 0, s, d, list, count); break;
+#define CS_CASE(Wv) case Wv: hipLaunchKernelGGL((k_checksum<Wv, 0>), dim3(grid), dim3(256), 0, s, d, list, count); break;
         CS_CASE(13) CS_CASE(14) CS_CASE(15) CS_CASE(16) CS_CASE(17) CS_CASE(18) CS_CASE(19) CS_CASE(20)
     default: break;
     }
+}
+
+// measurement variants (swimsim_bench_checksum): W = 19 only
+void launch_checksum_mode(const DS &d, const uint32_t *list, const uint32_t *count, uint32_t maxn, int mode, hipStream_t s) {
+    const uint32_t grid = (maxn + CS_ROWS - 1) / CS_ROWS;
+    if (grid == 0 || d.W != 19) return;
+    if (mode == 1) hipLaunchKernelGGL((k_checksum<19, 1>), dim3(grid), dim3(256), 0, s, d, list, count);
+    else if (mode == 2) hipLaunchKernelGGL((k_checksum<19, 2>), dim3(grid), dim3(256), 0, s, d, list, count);
+    else hipLaunchKernelGGL((k_checksum<19, 0>), dim3(grid), dim3(256), 0, s, d, list, count);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1007,7 +1199,8 @@ __global__ void k_ping_with(DS d, uint32_t tol, uint32_t sender, const MsgDesc *
     const uint32_t kept = wave_issue_recv(d, tol, sender, sinc, resp);
     if (kept == 0) {
         if (d.dirty[tol]) {
-            if (lane_id() == 0) defer[atomicAdd(defer_cnt, 1u)] = make_uint4(tol, 0, sender, scs);
+            if (wave_snapshot(d, tol, d.lo + tol, resp) && lane_id() == 0)
+                defer[atomicAdd(defer_cnt, 1u)] = make_uint4(0, resp.off_lo, scs, sender);
             resp.kind = 2;
         } else if (d.cs[tol] != scs) {
             wave_snapshot(d, tol, d.lo + tol, resp);

@@ -97,6 +97,7 @@ def load_library(path: str = LIB_PATH):
         "swimsim_converged": (C.c_int, [P, C.POINTER(i32)]),
         "swimsim_kernel_times": (C.c_int, [P, P, P, P, P, sz, C.POINTER(sz)]),
         "swimsim_enable_timing": (C.c_int, [P, i32]),
+        "swimsim_bench_checksum": (C.c_int, [P, u32, i32, i32, C.POINTER(C.c_double)]),
     }
     for name, (res, args) in sigs.items():
         f = getattr(L, name)
@@ -292,6 +293,11 @@ class Cluster:
                                                       cap, C.byref(n)))
         return {names[i].decode(): {"avg_ms": float(avg[i]), "launches": int(n_l[i]), "alg_bytes": float(byt[i])}
                 for i in range(n.value)}
+
+    def bench_checksum(self, nrows, mode=0, reps=3):
+        ms = C.c_double()
+        self._chk(load_library().swimsim_bench_checksum(self.h, nrows, mode, reps, C.byref(ms)))
+        return ms.value
 
     def node(self, o):
         return Node(self, o)
