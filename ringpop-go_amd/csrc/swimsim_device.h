@@ -61,7 +61,9 @@ struct DS {
     uint8_t *live;
     int32_t *part;
     const uint32_t *addrw;  // [N][6]
-    const uint32_t *tailw;  // [ecap*4][8]
+    const uint32_t *tailw;  // [ecap*4][8]: tail bytes status‖digits‖';' as words, word 6 = tail length
+    const uint32_t *rtail;  // [ecap*4][8]: record words W/4.. of addr‖tail with the address bytes zeroed
+                            // (tail pre-shifted by W%4 bytes), word 7 = record length W + tail length
     unsigned long long *ctr;
     uint32_t *err;
     uint4 *pool;

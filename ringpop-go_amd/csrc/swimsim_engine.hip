@@ -179,10 +179,33 @@ int build_tail_table(swimsim *h, uint32_t ecap) {
             max_tl = std::max(max_tl, (uint32_t)n);
         }
     }
-    uint32_t *dev = nullptr;
+    // record-tail table of the checksum formatter: record bytes [4*(W/4), 4*(W/4) + 28) with the
+    // address bytes zeroed, so that record word W/4 = address word W/4 | rt[0] and word W/4+k = rt[k]
+    std::vector<uint32_t> rt((size_t)ecap * 4 * 8, 0u);
+    const uint32_t q = h->W / 4, r = h->W % 4;
+    for (size_t i = 0; i < (size_t)ecap * 4; i++) {
+        uint8_t bytes[32] = {0};
+        const uint32_t n = t[i * 8 + 6];
+        memcpy(bytes + r, &t[i * 8], n);                   // tail words are little-endian byte strings
+        for (int w = 0; w < 7; w++)
+            rt[i * 8 + w] = (uint32_t)bytes[4 * w] | ((uint32_t)bytes[4 * w + 1] << 8) | ((uint32_t)bytes[4 * w + 2] << 16) |
+                            ((uint32_t)bytes[4 * w + 3] << 24);
+        // word 7: the record's last 4 bytes (the carried partial word of the stream after this record)
+        const uint32_t L = h->W + n;
+        const uint8_t *tb = (const uint8_t *)&t[i * 8];       // tails are >= 7 bytes: the last 4 are tail bytes
+        rt[i * 8 + 7] = (uint32_t)tb[n - 4] | ((uint32_t)tb[n - 3] << 8) | ((uint32_t)tb[n - 2] << 16) |
+                        ((uint32_t)tb[n - 1] << 24);
+        // record length in the low byte of word 0 (the address bytes' slot; masked off by the kernel)
+        if (r) rt[i * 8] |= L;
+    }
+    (void)q;
+    uint32_t *dev = nullptr, *rdev = nullptr;
     if (int rc = dalloc(h, &dev, t.size(), "tail table")) return rc;
+    if (int rc = dalloc(h, &rdev, rt.size(), "record tail table")) return rc;
     HIPCHK(h, hipMemcpy(dev, t.data(), t.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemcpy(rdev, rt.data(), rt.size() * 4, hipMemcpyHostToDevice));
     h->d.tailw = dev;
+    h->d.rtail = rdev;
     // digit-count thresholds of t0 + e*period over the table (the checksum record length formula)
     {
         uint32_t d0 = t[6] - 6, nthr = 0;   // "alive" + ';' around the digits of e = 0

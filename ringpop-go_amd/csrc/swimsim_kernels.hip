@@ -851,13 +851,13 @@ __global__ void k_jobs_reset(DS d, uint8_t *need) {
 // workgroup barrier per chunk. The string length and the last record (the hash prologue) come
 // from per-row values maintained by the merges.
 // ---------------------------------------------------------------------------------------------
-constexpr int CS_ROWS = 64;                     // rows per workgroup (one lane per row in every wave)
-constexpr int CS_RPL = 4;                       // records per formatter lane per chunk
-constexpr int CS_CHUNK = 2 * CS_RPL;            // members per chunk (2 formatter waves)
-constexpr int CS_SUPER = 32;                    // members per staged superchunk (4 chunks)
-constexpr int CS_STG = 36;                      // staged words per row (32 + pad: conflict-free ds_read_b128)
-constexpr int CS_RING = 185;                    // ring words per row: >= 2 chunks + a block; a multiple of 5
-constexpr int CS_RW = 11;                       // record words (<= 44 bytes: 20 B address + 24 B tail)
+constexpr int CS_ROWS = 64;                     // rows per workgroup: one lane per row in each of the 3 waves
+constexpr int CS_IT = 4;                        // members formatted per pipeline step
+constexpr int CS_SUP = 16;                      // members per register prefetch (4 steps)
+constexpr int CS_RING = 110;                    // ring words per row (22 blocks); holds 2 steps + a block + slack
+constexpr int CS_PRE = 13, CS_POST = 13;        // write spill areas in front of / behind the ring
+constexpr int CS_PHYS = CS_PRE + CS_RING + CS_POST;
+constexpr int CS_RW = 11;                       // record words of the prologue record (<= 44 bytes)
 
 template <int W, int RW>
 __device__ __forceinline__ void build_rec(uint32_t (&R)[RW], const uint32_t *A, const uint32_t (&T)[6]) {
@@ -898,52 +898,39 @@ __device__ __forceinline__ uint32_t record(const DS &d, uint32_t m, uint32_t w, 
     return (st < 4u && m < d.N) ? W + tb.z : 0u;
 }
 
-// write one record at stream byte position pos into the row's ring (aligned b32 stores; the two
-// partial edge words, shared with the neighbouring records, are written bytewise)
-__device__ __forceinline__ void put_record(uint32_t *ring, const uint32_t (&R)[CS_RW], uint32_t L, uint32_t pos) {
-    if (L == 0) return;
-    const uint32_t b = pos & 3u, rb = (4u - b) & 3u, q0 = (pos + 3u) >> 2;
-    uint32_t wq = q0 % CS_RING;
-    if (rb) {
-        uint8_t *p = (uint8_t *)(ring + (wq == 0 ? CS_RING - 1 : wq - 1)) + b;
-        for (uint32_t i = 0; i < rb; i++) p[i] = (uint8_t)(R[0] >> (8 * i));
-    }
-    const uint32_t nfull = (L - rb) >> 2, sh = rb * 8u;
-    uint32_t tailw = 0;
-#pragma unroll
-    for (int i = 0; i < CS_RW; i++) {
-        const uint32_t v = funnel(i + 1 < CS_RW ? R[i + 1] : 0u, R[i], sh);
-        if ((uint32_t)i < nfull) {
-            ring[wq] = v;
-            wq = (wq + 1 == CS_RING) ? 0u : wq + 1;
-        }
-        tailw = ((uint32_t)i == nfull) ? v : tailw;
-    }
-    const uint32_t rl = L - rb - 4u * nfull;
-    uint8_t *p = (uint8_t *)(ring + wq);
-    for (uint32_t i = 0; i < rl; i++) p[i] = (uint8_t)(tailw >> (8 * i));
+// M(x) = mur's data-only half: ror(x * c1, 17) * c2. mur(x, h) = ror(h ^ M(x), 19) * 5 + 0xe6546b64.
+__device__ __forceinline__ uint32_t fh_m(uint32_t x) { return ror32(x * FH_C1, 17) * FH_C2; }
+__device__ __forceinline__ uint32_t x5(uint32_t h) {          // h * 5 as one full-rate v_lshl_add_u32
+    uint32_t r;                                              // (LLVM would re-fold a C shift-add into a
+    asm("v_lshl_add_u32 %0, %1, 2, %1" : "=v"(r) : "v"(h)); //  quarter-rate multiply)
+    return r;
+}
+// mur(x, h) + add with M(x) precomputed: ror(h ^ M(x), 19) * 5 + 0xe6546b64 + add
+__device__ __forceinline__ uint32_t fh_fold(uint32_t h, uint32_t mx, uint32_t add) {
+    return x5(ror32(h ^ mx, 19)) + 0xe6546b64u + add;
 }
 
-// h-chain and (g,f)-chain halves of the FarmHash-32 mk block function; h never reads g or f
-__device__ __forceinline__ void fh_block_h(uint32_t &h, uint32_t a, uint32_t dd, uint32_t e) {
-    h += a;
-    h = fh_mur(dd, h) + e;
-}
-__device__ __forceinline__ void fh_block_gf(uint32_t &g, uint32_t &f, uint32_t a, uint32_t b, uint32_t c, uint32_t dd,
-                                            uint32_t e) {
-    g += b; f += c;
-    g = fh_mur(c, g) + a;
-    f = fh_mur(b + e * FH_C1, f) + dd;
-    f += g; g += f;
-}
-
-// MODE 0: normal; 1: hashers only (formatters stage but do not write the ring); 2: formatters only
+// The byte stream addr(m) ‖ status ‖ decimal(inc) ‖ ';' of one row goes through a per-row ring in LDS
+// (word-major: word q of row l at ring[q*64 + l], so every per-lane access is bank-conflict free):
+//   wave 2 (formatter): CS_IT members per step; each record is assembled from the row's member word
+//                       (register-prefetched), the member's address words (uniform loads one step
+//                       ahead) and a pre-shifted record tail (per-lane LDS cache keyed by incarnation,
+//                       read for the next step before the step barrier), and written as whole words
+//                       with v_perm byte alignment against the carried partial word;
+//   wave 0 (h chain)  : FarmHash-mk h-lane of each 20-byte block of the previous steps;
+//   wave 1 (g/f chain): the coupled g and f lanes of the same blocks.
+// One barrier per step; the hashers trail the formatter by one step.
+// MODE 0: normal; 1: hashers only (formatter skips its stores); 2: formatter only.
 template <int W, int MODE>
-__global__ void __launch_bounds__(256) k_checksum(DS d, const uint32_t *list, const uint32_t *count) {
-    __shared__ uint32_t ring[CS_ROWS * CS_RING];
-    __shared__ __attribute__((aligned(16))) uint32_t stage[2][CS_ROWS * CS_STG];
+__global__ void __launch_bounds__(192) k_checksum(DS d, const uint32_t *list, const uint32_t *count) {
+    __shared__ uint32_t ring[CS_PHYS * CS_ROWS];
+    __shared__ uint4 tcache[4 * 2 * CS_ROWS];     // [status][half][row]: record-tail words for the cached e
     __shared__ uint32_t wp[2][CS_ROWS];
     __shared__ uint32_t xgf[2][CS_ROWS];
+    constexpr int Q = W / 4;                      // record words that are pure address words
+    constexpr int NR = Q + 7;                     // record words
+    constexpr int NO = NR + 1;                    // ring words one record can touch
+    static_assert(NO <= CS_PRE && NO <= CS_POST, "spill areas too small");
     const uint32_t cnt = *count;
     if (blockIdx.x * CS_ROWS >= cnt) return;                       // uniform per workgroup
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
@@ -952,159 +939,218 @@ __global__ void __launch_bounds__(256) k_checksum(DS d, const uint32_t *list, co
     const uint32_t id = list[valid ? gi : blockIdx.x * CS_ROWS];
     const bool is_row = id < d.NL;
     const uint32_t *row = is_row ? d.mw + (size_t)id * d.NP : d.dense + (size_t)(id - d.NL) * d.NP;
-    uint32_t *myring = ring + lane * CS_RING;
-    const uint32_t nch = (d.N + CS_CHUNK - 1) / CS_CHUNK;
-    const uint32_t nsup = (d.N + CS_SUPER - 1) / CS_SUPER;
+    const uint32_t nsup = (d.N + CS_SUP - 1) / CS_SUP;
+    const uint32_t nit = nsup * (CS_SUP / CS_IT);
 
-    // formatter lanes cooperatively stage 32-member superchunks of all 64 rows (coalesced 16 B pieces:
-    // 8 consecutive lanes cover one row's 128 B); the next superchunk is in flight in registers
-    const uint32_t fl = threadIdx.x - 128;                         // formatter lane 0..127
-    uint4 pre[4];
-    auto stage_rows = [&](uint32_t sup, uint4 (&v)[4]) {
+    if (wave == 2) {
+        // ------------------------------- formatter -------------------------------
+        // The carried partial word after a record is its last 4 bytes (tail table word 7).
+        uint4 *tc = tcache;
+        uint32_t pos = 0, phys = 0, hc = 0, ce = 0xFFFFFFFFu;
+        uint4 pre[4], cur[4];
+        uint4 c0[CS_IT], c1[CS_IT];
+        uint32_t Lk[CS_IT];                                        // record lengths (0 = not in the string)
+        uint32_t An[CS_IT][Q + 1];
+        auto load_addr = [&](uint32_t m0) {                        // uniform addresses: one line per load
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint32_t q = fl + 128u * k, r = q >> 3, part = q & 7u;
-            const uint32_t gr = blockIdx.x * CS_ROWS + r;
-            const uint32_t rid = list[gr < cnt ? gr : blockIdx.x * CS_ROWS];
-            const uint32_t *rp = rid < d.NL ? d.mw + (size_t)rid * d.NP : d.dense + (size_t)(rid - d.NL) * d.NP;
-            const uint32_t m0 = sup * CS_SUPER + part * 4;
-            v[k] = m0 < d.NP ? *(const uint4 *)(rp + m0) : make_uint4(ST_UNKNOWN, ST_UNKNOWN, ST_UNKNOWN, ST_UNKNOWN);
-        }
-    };
-    auto stage_store = [&](uint32_t buf, const uint4 (&v)[4]) {
+            for (int k = 0; k < CS_IT; k++) {
+                const uint32_t *ap = d.addrw + (size_t)min(m0 + k, d.N - 1) * 6;
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint32_t q = fl + 128u * k, r = q >> 3, part = q & 7u;
-            *(uint4 *)&stage[buf][r * CS_STG + part * 4] = v[k];
+                for (int i = 0; i <= Q; i++) An[k][i] = ap[i];
+            }
+        };
+        // tails of the members of one step (cache refills are rare: mostly one incarnation per row)
+        auto prep = [&](const uint4 &q4, uint32_t mb) {
+            const uint32_t ws[4] = {q4.x, q4.y, q4.z, q4.w};
+#pragma unroll
+            for (int k = 0; k < CS_IT; k++) {
+                const uint32_t st = ws[k] & 7u, e = min(ws[k] >> 3, d.ecap - 1);
+                const bool ok = st < 4u && mb + k < d.N;
+                if (ok && e != ce) {
+                    const uint4 *tp = (const uint4 *)(d.rtail + (size_t)e * 32);
+#pragma unroll
+                    for (int q = 0; q < 8; q++) tc[q * CS_ROWS + lane] = tp[q];
+                    ce = e;
+                }
+                c0[k] = tc[((st & 3u) * 2) * CS_ROWS + lane];
+                c1[k] = tc[((st & 3u) * 2 + 1) * CS_ROWS + lane];
+                // W % 4 != 0: the length rides in the low byte of word 0 (an address byte slot)
+                Lk[k] = ok ? (W % 4 ? (c0[k].x & 0xFFu) : (uint32_t)reclen(d, st, e)) : 0u;
+            }
+        };
+#pragma unroll
+        for (int k = 0; k < 4; k++) pre[k] = *(const uint4 *)(row + 4 * k);
+        load_addr(0);
+        prep(pre[0], 0);
+        for (uint32_t sc = 0; sc < nsup; sc++) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) cur[k] = pre[k];
+            if (sc + 1 < nsup) {
+#pragma unroll
+                for (int k = 0; k < 4; k++) pre[k] = *(const uint4 *)(row + (sc + 1) * CS_SUP + 4 * k);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint32_t mb = sc * CS_SUP + u * CS_IT;
+                uint32_t A[CS_IT][Q + 1];
+#pragma unroll
+                for (int k = 0; k < CS_IT; k++)
+#pragma unroll
+                    for (int i = 0; i <= Q; i++) A[k][i] = An[k][i];
+                load_addr(mb + CS_IT);                             // one step ahead
+#pragma unroll
+                for (int k = 0; k < CS_IT; k++) {
+                    const uint32_t C[8] = {c0[k].x, c0[k].y, c0[k].z, c0[k].w, c1[k].x, c1[k].y, c1[k].z, c1[k].w};
+                    const uint32_t L = Lk[k];
+                    const uint32_t c0w = W % 4 ? (C[0] & 0xFFFFFF00u) : C[0];
+                    uint32_t R[NR + 1];
+#pragma unroll
+                    for (int i = 0; i < NR; i++) R[i] = i < Q ? A[k][i] : (i == Q ? (A[k][Q] | c0w) : C[i - Q]);
+                    R[NR] = 0u;
+                    const uint32_t s = pos & 3u;
+                    const uint32_t s2b = s | (s << 8);
+                    const uint32_t sel = 0x07060504u - (s2b | (s2b << 16));
+                    if (L) {
+                        if (MODE != 1) {
+                            // words past the record end are garbage that the next record overwrites (program order)
+                            const uint32_t i0 = (CS_PRE + phys) * CS_ROWS + lane;
+#pragma unroll
+                            for (int j = 0; j < NO; j++) ring[i0 + j * CS_ROWS] = __builtin_amdgcn_perm(R[j], j ? R[j - 1] : hc, sel);
+                            if (phys + NO > CS_RING) {                 // words past the ring end: also at the front
+                                const uint32_t i1 = (CS_PRE + phys - CS_RING) * CS_ROWS + lane;
+#pragma unroll
+                                for (int j = 0; j < NO; j++)
+                                    ring[i1 + j * CS_ROWS] = __builtin_amdgcn_perm(R[j], j ? R[j - 1] : hc, sel);
+                            }
+                        }
+                        hc = C[7];
+                        phys += (s + L) >> 2;
+                        phys = phys >= CS_RING ? phys - CS_RING : phys;
+                        pos += L;
+                    }
+                }
+                wp[(sc * 4 + u) & 1][lane] = pos;
+                prep(u < 3 ? cur[u + 1] : pre[0], mb + CS_IT);     // next step's tails, before the barrier
+                __syncthreads();
+            }
         }
-    };
-    if (wave >= 2) {
-        stage_rows(0, pre);
-        stage_store(0, pre);
-        if (nsup > 1) stage_rows(1, pre);
+        __syncthreads();
+        return;
     }
-    __syncthreads();
 
-    if (wave <= 1) {
-        // ---------------- hashers: wave 0 runs the h chain, wave 1 the (g, f) chains ----------------
-        const uint32_t len = is_row ? d.clen[id] : d.dense_len[id - d.NL];
-        int32_t last = is_row ? d.clast[id] : d.dense_last[id - d.NL];
-        if (last < 0) {                                            // invalidated: rescan from the end
-            last = -1;
-            for (int32_t m = (int32_t)d.N - 1; m >= 0; m--)
-                if ((row[m] & 7u) < 4u) { last = m; break; }
-        }
-        const bool ok = len > 24 && last >= 0;
-        if (!ok && valid && wave == 0) atomicOr(d.err, E_SHORT);
-        FH fh{0, 0, 0};
-        {
-            uint32_t R[CS_RW];
-            const uint32_t L = record<W>(d, (uint32_t)max(last, 0), row[max(last, 0)], R);
-            const uint32_t q = L >= 20 ? L - 20 : 0, qw = q >> 2, qb = (q & 3u) * 8u;
-            uint32_t t[5];
+    // ------------------------------- hashers -------------------------------
+    const uint32_t len = is_row ? d.clen[id] : d.dense_len[id - d.NL];
+    int32_t last = is_row ? d.clast[id] : d.dense_last[id - d.NL];
+    if (last < 0) {                                                // invalidated: rescan from the end
+        last = -1;
+        for (int32_t m = (int32_t)d.N - 1; m >= 0; m--)
+            if ((row[m] & 7u) < 4u) { last = m; break; }
+    }
+    const bool ok = len > 24 && last >= 0;
+    if (!ok && valid && wave == 0) atomicOr(d.err, E_SHORT);
+    FH fh{0, 0, 0};
+    {
+        uint32_t R[CS_RW];
+        const uint32_t L = record<W>(d, (uint32_t)max(last, 0), row[max(last, 0)], R);
+        const uint32_t q = L >= 20 ? L - 20 : 0, qw = q >> 2, qb = (q & 3u) * 8u;
+        uint32_t t[5];
 #pragma unroll
-            for (int k = 0; k < 5; k++) {
-                uint32_t lo = 0, hi = 0;
+        for (int k = 0; k < 5; k++) {
+            uint32_t lo = 0, hi = 0;
 #pragma unroll
-                for (int s = 0; s < CS_RW; s++) {
-                    lo = ((uint32_t)s == qw + k) ? R[s] : lo;
-                    hi = ((uint32_t)s == qw + k + 1) ? R[s] : hi;
-                }
-                t[k] = funnel(hi, lo, qb);
+            for (int s = 0; s < CS_RW; s++) {
+                lo = ((uint32_t)s == qw + k) ? R[s] : lo;
+                hi = ((uint32_t)s == qw + k + 1) ? R[s] : hi;
             }
-            fh.init(len, t[0], t[1], t[2], t[3], t[4]);
+            t[k] = funnel(hi, lo, qb);
         }
-        uint32_t h = fh.h, g = fh.g, f = fh.f;
-        const uint32_t iters = ok ? (len - 1) / 20 : 0;
-        uint32_t done = 0, rq = 0, avail = 0;
-        for (uint32_t t = 0; t <= nch; t++) {
-            const uint32_t lim = MODE == 2 ? 0u : (MODE == 1 ? min(iters, t * 15u) : min(iters, avail));
-            if (wave == 0) {
-                while (__any(done < lim)) {
-                    if (done < lim) {
-                        const uint32_t *p = myring + rq;
-                        fh_block_h(h, p[0], p[3], p[4]);
-                        done++;
-                        rq = (rq + 5 == CS_RING) ? 0u : rq + 5;
-                    }
-                }
-            } else {
-                while (__any(done < lim)) {
-                    if (done < lim) {
-                        const uint32_t *p = myring + rq;
-                        fh_block_gf(g, f, p[0], p[1], p[2], p[3], p[4]);
-                        done++;
-                        rq = (rq + 5 == CS_RING) ? 0u : rq + 5;
-                    }
-                }
+        fh.init(len, t[0], t[1], t[2], t[3], t[4]);
+    }
+    uint32_t h = fh.h, g = fh.g, f = fh.f;
+    const uint32_t iters = ok ? (len - 1) / 20 : 0;
+    const uint32_t *rb = ring + CS_PRE * CS_ROWS + lane;
+    uint32_t done = 0, rq = 0;
+    // hash blocks [done, lim) in groups of 4: all loads of a group first, then the arithmetic with
+    // branch-free predication (lanes have different limits); the role test is wave-uniform
+    const uint32_t role = __builtin_amdgcn_readfirstlane(wave);
+    auto advance = [&](uint32_t lim) {
+        const uint32_t n = done < lim ? min(lim - done, 4u) : 0u;
+        done += n;
+        rq += 5u * n;
+        rq = rq >= CS_RING ? rq - CS_RING : rq;
+    };
+    auto run_h = [&](uint32_t lim) {
+        while (__any(done < lim)) {
+            uint32_t a[4], dd[4], e[4];
+            uint32_t q = rq;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t *p = rb + q * CS_ROWS;
+                a[k] = p[0]; dd[k] = p[3 * CS_ROWS]; e[k] = p[4 * CS_ROWS];
+                q += 5;
+                q = q >= CS_RING ? q - CS_RING : q;
             }
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t hn = fh_fold(h + a[k], fh_m(dd[k]), e[k]);
+                h = done + k < lim ? hn : h;
+            }
+            advance(lim);
+        }
+    };
+    auto run_gf = [&](uint32_t lim) {
+        while (__any(done < lim)) {
+            uint32_t v[4][5];
+            uint32_t q = rq;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t *p = rb + q * CS_ROWS;
+#pragma unroll
+                for (int i = 0; i < 5; i++) v[k][i] = p[i * CS_ROWS];
+                q += 5;
+                q = q >= CS_RING ? q - CS_RING : q;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t a = v[k][0], b = v[k][1], c = v[k][2], dd = v[k][3], e = v[k][4];
+                uint32_t gn = fh_fold(g + b, fh_m(c), a);
+                uint32_t fn = fh_fold(f + c, fh_m(b + e * FH_C1), dd);
+                fn += gn; gn += fn;
+                const bool act = done + k < lim;
+                g = act ? gn : g;
+                f = act ? fn : f;
+            }
+            advance(lim);
+        }
+    };
+    uint32_t avail = 0;
+    if (role == 0) {
+        for (uint32_t t = 0; t < nit; t++) {
+            if (MODE != 2) run_h(MODE == 1 ? min(iters, t * 8u) : min(iters, avail));
             __syncthreads();
             avail = wp[t & 1][lane] / 20;
         }
-        const uint32_t fin_lim = MODE == 2 ? 0u : iters;
-        while (__any(done < fin_lim)) {
-            if (done < fin_lim) {
-                const uint32_t *p = myring + rq;
-                if (wave == 0) fh_block_h(h, p[0], p[3], p[4]);
-                else fh_block_gf(g, f, p[0], p[1], p[2], p[3], p[4]);
-                done++;
-                rq = (rq + 5 == CS_RING) ? 0u : rq + 5;
-            }
-        }
-        if (wave == 1) { xgf[0][lane] = g; xgf[1][lane] = f; }
-        __syncthreads();
-        if (wave == 0 && valid) {
-            fh.h = h; fh.g = xgf[0][lane]; fh.f = xgf[1][lane];
-            const uint32_t hv = ok ? fh.fin() : 0u;
-            if (is_row) {
-                d.cs[id] = hv;
-                d.dirty[id] = 0;
-                atomicAdd(&d.ctr[C_X_CS_ROWS], 1ull);
-            } else {
-                d.dense_cs[id - d.NL] = hv;
-            }
-        }
+        if (MODE != 2) run_h(iters);
     } else {
-        // ---------------- formatters: wave 2 takes records 0-3 of each chunk, wave 3 records 4-7 ----------------
-        const uint32_t fw = wave - 2;
-        uint32_t S = 0;                                            // stream bytes before this chunk
-        for (uint32_t t = 0; t <= nch; t++) {
-            if (t < nch) {
-                const uint32_t sup = t / (CS_SUPER / CS_CHUNK), cs_ = t % (CS_SUPER / CS_CHUNK);
-                const uint32_t *sp = &stage[sup & 1][lane * CS_STG + cs_ * CS_CHUNK];
-                const uint4 va = *(const uint4 *)sp, vb = *(const uint4 *)(sp + 4);
-                const uint32_t ws[CS_CHUNK] = {va.x, va.y, va.z, va.w, vb.x, vb.y, vb.z, vb.w};
-                const uint32_t mb = t * CS_CHUNK;
-                uint32_t pre_len = 0, tot = 0;
-#pragma unroll
-                for (int k = 0; k < CS_CHUNK; k++) {
-                    const uint32_t l = (mb + k < d.N) ? (uint32_t)reclen(d, ws[k] & 7u, ws[k] >> 3) : 0u;
-                    pre_len += ((uint32_t)k < fw * CS_RPL) ? l : 0u;
-                    tot += l;
-                }
-                uint32_t pos = S + pre_len;
-                uint32_t R[CS_RPL][CS_RW], L[CS_RPL];
-#pragma unroll
-                for (int j = 0; j < CS_RPL; j++) {
-                    const uint32_t wk = fw ? ws[CS_RPL + j] : ws[j];
-                    L[j] = record<W>(d, mb + fw * CS_RPL + j, wk, R[j]);
-                }
-#pragma unroll
-                for (int j = 0; j < CS_RPL; j++) {
-                    if (MODE != 1) put_record(myring, R[j], L[j], pos);
-                    pos += L[j];
-                }
-                S += tot;
-                if (fw == 0) wp[t & 1][lane] = S;
-                // double-buffered staging: store the prefetched superchunk at the end of this one
-                if (cs_ == CS_SUPER / CS_CHUNK - 1 && sup + 1 < nsup) {
-                    stage_store((sup + 1) & 1, pre);
-                    if (sup + 2 < nsup) stage_rows(sup + 2, pre);
-                }
-            }
+        for (uint32_t t = 0; t < nit; t++) {
+            if (MODE != 2) run_gf(MODE == 1 ? min(iters, t * 8u) : min(iters, avail));
             __syncthreads();
+            avail = wp[t & 1][lane] / 20;
         }
-        __syncthreads();
+        if (MODE != 2) run_gf(iters);
+    }
+    if (wave == 1) { xgf[0][lane] = g; xgf[1][lane] = f; }
+    __syncthreads();
+    if (wave == 0 && valid) {
+        fh.h = h; fh.g = xgf[0][lane]; fh.f = xgf[1][lane];
+        const uint32_t hv = ok ? fh.fin() : 0u;
+        if (is_row) {
+            d.cs[id] = hv;
+            d.dirty[id] = 0;
+            atomicAdd(&d.ctr[C_X_CS_ROWS], 1ull);
+        } else {
+            d.dense_cs[id - d.NL] = hv;
+        }
     }
 }
 
@@ -1116,7 +1162,7 @@ void launch_checksum(const DS &d, const uint32_t *list, const uint32_t *count, u
     const uint32_t grid = (maxn + CS_ROWS - 1) / CS_ROWS;
     if (grid == 0) return;
     switch (d.W) {
-#define CS_CASE(Wv) case Wv: hipLaunchKernelGGL((k_checksum<Wv, 0>), dim3(grid), dim3(256), 0, s, d, list, count); break;
+#define CS_CASE(Wv) case Wv: hipLaunchKernelGGL((k_checksum<Wv, 0>), dim3(grid), dim3(192), 0, s, d, list, count); break;
         CS_CASE(13) CS_CASE(14) CS_CASE(15) CS_CASE(16) CS_CASE(17) CS_CASE(18) CS_CASE(19) CS_CASE(20)
     default: break;
     }
@@ -1126,9 +1172,9 @@ void launch_checksum(const DS &d, const uint32_t *list, const uint32_t *count, u
 void launch_checksum_mode(const DS &d, const uint32_t *list, const uint32_t *count, uint32_t maxn, int mode, hipStream_t s) {
     const uint32_t grid = (maxn + CS_ROWS - 1) / CS_ROWS;
     if (grid == 0 || d.W != 19) return;
-    if (mode == 1) hipLaunchKernelGGL((k_checksum<19, 1>), dim3(grid), dim3(256), 0, s, d, list, count);
-    else if (mode == 2) hipLaunchKernelGGL((k_checksum<19, 2>), dim3(grid), dim3(256), 0, s, d, list, count);
-    else hipLaunchKernelGGL((k_checksum<19, 0>), dim3(grid), dim3(256), 0, s, d, list, count);
+    if (mode == 1) hipLaunchKernelGGL((k_checksum<19, 1>), dim3(grid), dim3(192), 0, s, d, list, count);
+    else if (mode == 2) hipLaunchKernelGGL((k_checksum<19, 2>), dim3(grid), dim3(192), 0, s, d, list, count);
+    else hipLaunchKernelGGL((k_checksum<19, 0>), dim3(grid), dim3(192), 0, s, d, list, count);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -18,4 +18,14 @@ if [ "$mode" = prof ]; then
   rc=$?; echo "rocprof rc=$rc" >> gpurun_out/prof.log
   [ $rc -eq 0 ] || exit $rc
 fi
+if [ "$mode" = pmc ]; then
+  export TMPDIR=/tmp
+  SQ="SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS"
+  timeout -k 10 300 rocprofv3 --pmc $SQ --kernel-trace -d gpurun_out/pmc_sq -o run --output-format csv -- python3 tools_cs_bench.py 65536 16384 1 > gpurun_out/pmc_sq.log 2>&1
+  rc=$?; echo "pmc sq rc=$rc" >> gpurun_out/pmc_sq.log; [ $rc -eq 0 ] || exit $rc
+  timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --no-cpu-baseline --steps 30 > gpurun_out/pmc_fetch.log 2>&1
+  rc=$?; echo "pmc fetch rc=$rc" >> gpurun_out/pmc_fetch.log; [ $rc -eq 0 ] || exit $rc
+  timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --no-cpu-baseline --steps 30 > gpurun_out/pmc_write.log 2>&1
+  rc=$?; echo "pmc write rc=$rc" >> gpurun_out/pmc_write.log; [ $rc -eq 0 ] || exit $rc
+fi
 exit 0

@@ -1,12 +1,18 @@
-import sys, json
+"""Checksum-kernel microbench (diagnostic, not the bench): average ms per launch of k_checksum over the
+first `rows` observer rows of a converged N-member cluster, mode 0 = full kernel, 1 = hash waves only,
+2 = formatter wave only (modes 1/2 leave garbage checksums)."""
+import json
+import sys
+
 sys.path.insert(0, "ringpop-go_amd")
-import swimsim
+import swimsim  # noqa: E402
+
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
-c = swimsim.Cluster(n, observer_range=(0, min(n, 16384)))
+rows_list = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [64, 1024, 4096, 16384]
+reps = int(sys.argv[3]) if len(sys.argv) > 3 else 2
+c = swimsim.Cluster(n, observer_range=(0, min(n, max(rows_list))))
 out = {}
-for rows in (64, 1024, 4096, 16384):
-    if rows > c.nl:
-        continue
+for rows in rows_list:
     for mode in (0, 1, 2):
-        out[f"rows{rows}_mode{mode}"] = round(c.bench_checksum(rows, mode, reps=2), 3)
+        out[f"rows{rows}_mode{mode}"] = round(c.bench_checksum(rows, mode, reps=reps), 3)
 print(json.dumps(out))
