@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SWIMSIM_ABI_VERSION 1
+#define SWIMSIM_ABI_VERSION 2
 
 enum {
     SWIMSIM_OK = 0,
@@ -152,6 +152,24 @@ int swimsim_enable_timing(swimsim_t *h, int32_t enable);
 /* time the checksum kernel alone on the first nrows rows (mode 0 full, 1 hasher only, 2 formatting
  * only; the last two are diagnostics and leave garbage checksums) — average ms per launch */
 int swimsim_bench_checksum(swimsim_t *h, uint32_t nrows, int32_t mode, int32_t reps, double *ms);
+
+/* ---- shards: one cluster's observer rows split over G shards ----
+ * The reference runs one swim.Node per process; here a shard owns observer rows
+ * [N*r/G, N*(r+1)/G) of one simulated cluster and exchanges every cross-shard message (ping
+ * requests and responses, ping-req relays, reverse-full-sync and heal memberships) with the other
+ * shards at fixed points of the round. With G > 1 swimsim_step() is collective: every shard calls
+ * it with the same events. Results stay bit-identical to G = 1. */
+/* G shards in this process (one thread each in swimsim_group_step), all on cfg->device or on
+ * devices[i]; copies between shards are device-to-device (peer copies across GPUs) */
+int swimsim_group_create(const swimsim_config *cfg, uint32_t nshards, const int32_t *devices, swimsim_t **out);
+int swimsim_group_step(swimsim_t *const *handles, uint32_t nshards, uint32_t nrounds, const swimsim_event *events,
+                       size_t nevents);
+/* one process per GPU: rank 0 makes an id, the launcher broadcasts it, every rank attaches its
+ * handle (created with observer_begin/end = its canonical shard); exchanges use RCCL send/recv */
+int swimsim_comm_unique_id(uint8_t *out, size_t cap);   /* returns the id length (128) */
+int swimsim_comm_attach(swimsim_t *h, uint32_t nranks, uint32_t rank, const uint8_t *id, size_t len);
+int swimsim_shard_info(swimsim_t *h, uint32_t *nshards, uint32_t *rank, uint32_t *lo, uint32_t *hi,
+                       uint64_t *exchanged_bytes, uint64_t *exchanges);
 
 #ifdef __cplusplus
 }

@@ -32,7 +32,7 @@ enum Counter {
 };
 
 enum ErrBits : uint32_t {
-    E_POOL = 1, E_DENSE = 2, E_ECAP = 4, E_SHORT = 8, E_ITER = 16, E_COUNT = 32
+    E_POOL = 1, E_DENSE = 2, E_ECAP = 4, E_SHORT = 8, E_ITER = 16, E_COUNT = 32, E_XCAP = 64
 };
 
 struct MsgDesc {        // a change list in flight
@@ -63,7 +63,8 @@ struct DS {
     const uint32_t *addrw;  // [N][6]
     const uint32_t *tailw;  // [ecap*4][8]: tail bytes status‖digits‖';' as words, word 6 = tail length
     const uint32_t *rtail;  // [ecap*4][8]: record words W/4.. of addr‖tail with the address bytes zeroed
-                            // (tail pre-shifted by W%4 bytes), word 7 = record length W + tail length
+                            // (tail pre-shifted by W%4 bytes); word 0's low byte = record length when
+                            // W%4 != 0; word 7 = the record's last 4 bytes
     unsigned long long *ctr;
     uint32_t *err;
     uint4 *pool;
@@ -79,10 +80,19 @@ struct DS {
     uint32_t *clen;         // [NL] checksum-string length of each row
     int32_t *clast;         // [NL] last included member (-2: rescan)
     uint32_t dig_d0;          // decimal digits of t0
+    uint32_t G, rank;         // observer-row shards of the cluster and this handle's shard
+    const uint32_t *shard_lo; // [G+1] first observer of each shard (ascending, shard_lo[G] = N)
     uint32_t dig_thr[8];      // e at which t0 + e*period gains a digit (0xFFFFFFFF = never)
 };
 
 __host__ __device__ inline bool is_pingable(uint32_t st) { return st <= ST_SUSPECT; }
+
+// shard that owns observer row o (G is small: a linear scan over the shard boundaries)
+__device__ __forceinline__ uint32_t owner_of(const DS &d, uint32_t o) {
+    uint32_t r = 0;
+    while (r + 1 < d.G && o >= d.shard_lo[r + 1]) r++;
+    return r;
+}
 
 __host__ __device__ inline int32_t digits10(int32_t n) {
     int32_t d = 0;

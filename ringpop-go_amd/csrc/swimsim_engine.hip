@@ -5,14 +5,20 @@
 // member-state computation runs in the gfx950 kernels of swimsim_kernels.hip. There is no
 // CPU fallback: if the device is unusable, swimsim_create() fails.
 #include "swimsim_kernels.hip"
+#include "swimsim_xchg.hip"
 
 #include <hipcub/hipcub.hpp>
+#include <rccl/rccl.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/swimsim.h"
@@ -28,9 +34,144 @@ struct Timed {
     hipEvent_t a, b;
 };
 
-enum Fam { F_TIMERS, F_SELECT, F_ISSUE, F_SORT, F_RECV, F_RESP, F_PINGREQ, F_JOBS, F_CHECKSUM, F_EVENTS, F_NFAM };
+enum Fam { F_TIMERS, F_SELECT, F_ISSUE, F_SORT, F_RECV, F_RESP, F_PINGREQ, F_JOBS, F_CHECKSUM, F_EVENTS, F_XCHG,
+           F_NFAM };
 const char *kFamName[F_NFAM] = {"timers", "select", "issue", "sort", "recv_merge", "resp_merge", "pingreq",
-                                "rfs_jobs", "checksum", "events"};
+                                "rfs_jobs", "checksum", "events", "exchange"};
+
+// ---------------------------------------------------------------------------------------------
+// shard transports: how parcels move between the shards of one cluster
+// ---------------------------------------------------------------------------------------------
+struct Transport {
+    uint32_t G = 1, rank = 0;
+    virtual ~Transport() {}
+    // send[G*k] → recv[G*k], recv[s*k + i] = shard s's send[rank*k + i] (host arrays)
+    virtual int sizes(const uint64_t *send, uint64_t *recv, int k) = 0;
+    // one variable-size device segment to and from every shard (own segment included)
+    virtual int data(const uint8_t *sbuf, const uint64_t *soff, const uint64_t *sbytes, uint8_t *rbuf,
+                     const uint64_t *roff, const uint64_t *rbytes, hipStream_t st) = 0;
+    // host bytes of shard root to every shard
+    virtual int bcast(void *buf, size_t bytes, uint32_t root) = 0;
+    virtual const char *name() const = 0;
+};
+
+// shards of one process (threads): device-to-device (peer) copies between the shards' buffers
+struct LocalHub {
+    uint32_t G;
+    std::mutex m;
+    std::condition_variable cv;
+    uint32_t arrived = 0, gen = 0;
+    bool aborted = false;
+    std::vector<const void *> ptr;
+    std::vector<const uint64_t *> off, len;
+    std::vector<int> dev;
+    explicit LocalHub(uint32_t g) : G(g), ptr(g), off(g), len(g), dev(g, 0) {}
+    bool barrier() {
+        std::unique_lock<std::mutex> lk(m);
+        if (aborted) return false;
+        const uint32_t my = gen;
+        if (++arrived == G) {
+            arrived = 0;
+            gen++;
+            cv.notify_all();
+        } else {
+            cv.wait(lk, [&] { return gen != my || aborted; });
+        }
+        return !aborted;
+    }
+    void abort() {
+        std::lock_guard<std::mutex> lk(m);
+        aborted = true;
+        cv.notify_all();
+    }
+};
+
+struct LocalPort : Transport {
+    std::shared_ptr<LocalHub> hub;
+    int device = 0;
+    const char *name() const override { return "local"; }
+    int sizes(const uint64_t *send, uint64_t *recv, int k) override {
+        hub->ptr[rank] = send;
+        if (!hub->barrier()) return SWIMSIM_EHIP;
+        for (uint32_t s = 0; s < G; s++)
+            for (int i = 0; i < k; i++) recv[s * k + i] = ((const uint64_t *)hub->ptr[s])[rank * k + i];
+        return hub->barrier() ? 0 : SWIMSIM_EHIP;
+    }
+    int data(const uint8_t *sbuf, const uint64_t *soff, const uint64_t *sbytes, uint8_t *rbuf, const uint64_t *roff,
+             const uint64_t *rbytes, hipStream_t st) override {
+        hub->ptr[rank] = sbuf;
+        hub->off[rank] = soff;
+        hub->len[rank] = sbytes;
+        hub->dev[rank] = device;
+        if (!hub->barrier()) return SWIMSIM_EHIP;
+        hipError_t e = hipSuccess;
+        for (uint32_t s = 0; s < G && e == hipSuccess; s++) {
+            if (!rbytes[s]) continue;
+            const uint8_t *src = (const uint8_t *)hub->ptr[s] + hub->off[s][rank];
+            e = hub->dev[s] == device ? hipMemcpyAsync(rbuf + roff[s], src, rbytes[s], hipMemcpyDeviceToDevice, st)
+                                      : hipMemcpyPeerAsync(rbuf + roff[s], device, src, hub->dev[s], rbytes[s], st);
+        }
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) { hub->abort(); return SWIMSIM_EHIP; }
+        return hub->barrier() ? 0 : SWIMSIM_EHIP;            // sources stay untouched until every copy is done
+    }
+    int bcast(void *buf, size_t bytes, uint32_t root) override {
+        hub->ptr[rank] = buf;
+        if (!hub->barrier()) return SWIMSIM_EHIP;
+        if (rank != root) memcpy(buf, hub->ptr[root], bytes);
+        return hub->barrier() ? 0 : SWIMSIM_EHIP;
+    }
+};
+
+// one process per GPU: RCCL point-to-point over xGMI, grouped so every pair moves concurrently
+struct RcclPort : Transport {
+    ncclComm_t comm = nullptr;
+    hipStream_t st = nullptr;
+    uint64_t *dsz = nullptr;      // device staging for sizes / broadcasts
+    size_t dsz_cap = 0;
+    const char *name() const override { return "rccl"; }
+    ~RcclPort() override {
+        if (comm) ncclCommDestroy(comm);
+        if (dsz) hipFree(dsz);
+    }
+    int stage(size_t bytes) {
+        if (bytes <= dsz_cap) return 0;
+        if (dsz) hipFree(dsz);
+        dsz_cap = std::max<size_t>(bytes, 4096);
+        return hipMalloc(&dsz, dsz_cap) == hipSuccess ? 0 : SWIMSIM_ENOMEM;
+    }
+    int sizes(const uint64_t *send, uint64_t *recv, int k) override {
+        const size_t n = (size_t)G * k;
+        if (int rc = stage(2 * n * 8)) return rc;
+        uint64_t *ds = dsz, *dr = dsz + n;
+        if (hipMemcpyAsync(ds, send, n * 8, hipMemcpyHostToDevice, st) != hipSuccess) return SWIMSIM_EHIP;
+        ncclGroupStart();
+        for (uint32_t p = 0; p < G; p++) {
+            ncclSend(ds + (size_t)p * k, k, ncclUint64, (int)p, comm, st);
+            ncclRecv(dr + (size_t)p * k, k, ncclUint64, (int)p, comm, st);
+        }
+        if (ncclGroupEnd() != ncclSuccess) return SWIMSIM_EHIP;
+        if (hipMemcpyAsync(recv, dr, n * 8, hipMemcpyDeviceToHost, st) != hipSuccess) return SWIMSIM_EHIP;
+        return hipStreamSynchronize(st) == hipSuccess ? 0 : SWIMSIM_EHIP;
+    }
+    int data(const uint8_t *sbuf, const uint64_t *soff, const uint64_t *sbytes, uint8_t *rbuf, const uint64_t *roff,
+             const uint64_t *rbytes, hipStream_t s) override {
+        ncclGroupStart();
+        for (uint32_t p = 0; p < G; p++) {
+            if (sbytes[p]) ncclSend(sbuf + soff[p], sbytes[p], ncclUint8, (int)p, comm, s);
+            if (rbytes[p]) ncclRecv(rbuf + roff[p], rbytes[p], ncclUint8, (int)p, comm, s);
+        }
+        if (ncclGroupEnd() != ncclSuccess) return SWIMSIM_EHIP;
+        return hipStreamSynchronize(s) == hipSuccess ? 0 : SWIMSIM_EHIP;
+    }
+    int bcast(void *buf, size_t bytes, uint32_t root) override {
+        if (int rc = stage(bytes)) return rc;
+        if (hipMemcpyAsync(dsz, buf, bytes, hipMemcpyHostToDevice, st) != hipSuccess) return SWIMSIM_EHIP;
+        if (ncclBroadcast(dsz, dsz, bytes, ncclUint8, (int)root, comm, st) != ncclSuccess) return SWIMSIM_EHIP;
+        if (hipMemcpyAsync(buf, dsz, bytes, hipMemcpyDeviceToHost, st) != hipSuccess) return SWIMSIM_EHIP;
+        return hipStreamSynchronize(st) == hipSuccess ? 0 : SWIMSIM_EHIP;
+    }
+};
 
 }  // namespace
 
@@ -52,13 +193,29 @@ struct swimsim {
     std::vector<std::string> addrs;
     uint32_t round = 0;
     uint64_t host_ctr[SWIMSIM_NCOUNTERS] = {0};
+    // shards: observer rows [lo, lo + NL) of a cluster split over G shards
+    uint32_t G = 1, rank = 0;
+    std::vector<uint32_t> shard_lo;           // [G+1]
+    std::unique_ptr<Transport> xp;
+    uint4 *xitems = nullptr;
+    uint32_t *xcnt = nullptr, xcap = 0;
+    unsigned long long *xsz = nullptr, *xseg = nullptr, *xtcur = nullptr, *xdcur = nullptr;
+    ulonglong2 *xsrcs = nullptr;
+    uint8_t *sbuf = nullptr, *rbuf = nullptr;
+    size_t sbuf_cap = 0, rbuf_cap = 0;
+    uint2 *needlist = nullptr;
+    uint32_t *needcnt = nullptr, needcap = 0;
+    uint32_t *hsics = nullptr, *npairs = nullptr;
+    unsigned long long *keys = nullptr, *keys_sorted = nullptr;
+    uint32_t keycap = 0;
+    uint64_t x_bytes = 0, x_calls = 0;        // exchanged bytes / exchanges (measurement)
     // work buffers
     int32_t *tgt = nullptr;
     uint8_t *failed = nullptr;
     MsgDesc *sdesc = nullptr, *rdesc = nullptr, *sdesc2 = nullptr, *rdesc2 = nullptr, *snapdesc = nullptr, *hdesc = nullptr;
     uint32_t *sI = nullptr, *sC = nullptr, *sI2 = nullptr, *sC2 = nullptr;
     uint32_t *H = nullptr, *nh = nullptr;
-    uint32_t *keys_in = nullptr, *vals_in = nullptr, *keys_out = nullptr, *vals_out = nullptr;
+    uint32_t *keys_in = nullptr, *vals_out = nullptr;    // sorted inbox: receiver column, sender-value column
     uint32_t *ukeys = nullptr, *counts = nullptr, *offs = nullptr, *nruns = nullptr, *info = nullptr;
     void *cub_tmp = nullptr;
     size_t cub_bytes = 0;
@@ -242,16 +399,17 @@ int check_err(swimsim *h) {
     return h->fail(SWIMSIM_EINVAL, "dissemination count mismatch (internal error %u)", e);
 }
 
-// --- sorting a (key, value) inbox and run-length encoding it ---
+// --- sorting the (receiver << 32 | sender value) inbox keys and run-length encoding by receiver ---
 int sort_inbox(swimsim *h, uint32_t n, uint32_t *host_info) {
     Scope sc(h, F_SORT);
     int endbit = 1;
     while ((1u << endbit) <= h->N) endbit++;
     size_t bytes = h->cub_bytes;
-    HIPCHK(h, hipcub::DeviceRadixSort::SortPairs(h->cub_tmp, bytes, h->keys_in, h->keys_out, h->vals_in, h->vals_out,
-                                                 (int)n, 0, endbit, h->s));
+    HIPCHK(h, hipcub::DeviceRadixSort::SortKeys(h->cub_tmp, bytes, h->keys, h->keys_sorted, (int)n, 0, 32 + endbit, h->s));
+    hipLaunchKernelGGL(k_split_keys, dim3(blocks_for_threads(n)), dim3(256), 0, h->s, h->keys_sorted, n, h->keys_in,
+                       h->vals_out);
     bytes = h->cub_bytes;
-    HIPCHK(h, hipcub::DeviceRunLengthEncode::Encode(h->cub_tmp, bytes, h->keys_out, h->ukeys, h->counts, h->nruns,
+    HIPCHK(h, hipcub::DeviceRunLengthEncode::Encode(h->cub_tmp, bytes, h->keys_in, h->ukeys, h->counts, h->nruns,
                                                     (int)n, h->s));
     bytes = h->cub_bytes;
     HIPCHK(h, hipcub::DeviceScan::ExclusiveSum(h->cub_tmp, bytes, h->counts, h->offs, (int)n, h->s));
@@ -260,6 +418,102 @@ int sort_inbox(swimsim *h, uint32_t n, uint32_t *host_info) {
                        h->info);
     HIPCHK(h, hipMemcpyAsync(host_info, h->info, 16, hipMemcpyDeviceToHost, h->s));
     HIPCHK(h, hipStreamSynchronize(h->s));
+    return 0;
+}
+
+inline uint32_t owner_host(const swimsim *h, uint32_t o) {
+    uint32_t r = 0;
+    while (r + 1 < h->G && o >= h->shard_lo[r + 1]) r++;
+    return r;
+}
+
+XArgs xargs(swimsim *h) {
+    XArgs x{};
+    x.sdesc = h->sdesc; x.sdesc2 = h->sdesc2; x.rdesc = h->rdesc; x.rdesc2 = h->rdesc2; x.snapdesc = h->snapdesc;
+    x.hdesc = h->hdesc;
+    x.sI = h->sI; x.sC = h->sC; x.sI2 = h->sI2; x.sC2 = h->sC2;
+    x.hsics = h->hsics;
+    x.need = h->need;
+    x.keys = h->keys; x.npairs = h->npairs; x.keycap = h->keycap;
+    x.needlist = h->needlist; x.needcnt = h->needcnt; x.needcap = h->needcap;
+    return x;
+}
+
+// one collective exchange of the queued items' parcels between all shards (every shard calls it)
+int xchg(swimsim *h) {
+    Scope sc(h, F_XCHG);
+    const uint32_t G = h->G;
+    const XArgs x = xargs(h);
+    HIPCHK(h, hipMemsetAsync(h->xsz, 0, 2 * G * 8, h->s));
+    hipLaunchKernelGGL(k_x_size, dim3(blocks_for_threads(h->xcap)), dim3(256), 0, h->s, h->d, x, h->xitems, h->xcnt,
+                       h->xcap, h->xsz);
+    std::vector<uint64_t> sz(2 * G);
+    uint32_t nitems = 0;
+    HIPCHK(h, hipMemcpyAsync(sz.data(), h->xsz, 2 * G * 8, hipMemcpyDeviceToHost, h->s));
+    HIPCHK(h, hipMemcpyAsync(&nitems, h->xcnt, 4, hipMemcpyDeviceToHost, h->s));
+    HIPCHK(h, hipStreamSynchronize(h->s));
+    if (nitems > h->xcap) return h->fail(SWIMSIM_ECAPACITY, "exchange item list overflow (%u items)", nitems);
+    // send segments: [parcel offset table][parcels], 16-byte aligned
+    std::vector<uint64_t> soff(G), sbytes(G), tbl(G), cur(3 * G), sendsz(2 * G), recvsz(2 * G);
+    uint64_t total = 0;
+    for (uint32_t p = 0; p < G; p++) {
+        tbl[p] = (sz[2 * p + 1] * 4 + 15) & ~15ull;
+        sbytes[p] = sz[2 * p + 1] ? tbl[p] + sz[2 * p] : 0;
+        soff[p] = total;
+        total += (sbytes[p] + 15) & ~15ull;
+        cur[p] = soff[p];            // xseg
+        cur[G + p] = 0;              // table cursor
+        cur[2 * G + p] = tbl[p];     // parcel cursor
+        sendsz[2 * p] = sbytes[p];
+        sendsz[2 * p + 1] = sz[2 * p + 1];
+    }
+    if (total > h->sbuf_cap) {
+        if (h->sbuf) hipFree(h->sbuf);
+        h->sbuf_cap = std::max<uint64_t>(total + total / 2, 1 << 20);
+        HIPCHK(h, hipMalloc(&h->sbuf, h->sbuf_cap));
+    }
+    HIPCHK(h, hipMemcpyAsync(h->xseg, cur.data(), 3 * G * 8, hipMemcpyHostToDevice, h->s));
+    if (nitems)
+        hipLaunchKernelGGL(k_x_pack, dim3(blocks_for_waves(nitems)), dim3(256), 0, h->s, h->d, x, h->xitems, h->xcnt,
+                           h->xcap, h->sbuf, h->xseg, h->xtcur, h->xdcur);
+    HIPCHK(h, hipStreamSynchronize(h->s));
+    if (int rc = h->xp->sizes(sendsz.data(), recvsz.data(), 2)) return h->fail(rc, "shard size exchange failed (%s)", h->xp->name());
+    std::vector<uint64_t> roff(G), rbytes(G);
+    std::vector<ulonglong2> srcs(G);
+    uint64_t rtotal = 0, nparc = 0;
+    for (uint32_t p = 0; p < G; p++) {
+        rbytes[p] = recvsz[2 * p];
+        roff[p] = rtotal;
+        srcs[p] = make_ulonglong2(rtotal, nparc);
+        rtotal += (rbytes[p] + 15) & ~15ull;
+        nparc += recvsz[2 * p + 1];
+    }
+    if (rtotal > h->rbuf_cap) {
+        if (h->rbuf) hipFree(h->rbuf);
+        h->rbuf_cap = std::max<uint64_t>(rtotal + rtotal / 2, 1 << 20);
+        HIPCHK(h, hipMalloc(&h->rbuf, h->rbuf_cap));
+    }
+    if (int rc = h->xp->data(h->sbuf, soff.data(), sbytes.data(), h->rbuf, roff.data(), rbytes.data(), h->s))
+        return h->fail(rc, "shard data exchange failed (%s)", h->xp->name());
+    if (nparc) {
+        HIPCHK(h, hipMemcpyAsync(h->xsrcs, srcs.data(), G * sizeof(ulonglong2), hipMemcpyHostToDevice, h->s));
+        hipLaunchKernelGGL(k_x_unpack, dim3(blocks_for_waves((uint32_t)nparc)), dim3(256), 0, h->s, h->d, x, h->rbuf,
+                           h->xsrcs, G, (uint32_t)nparc);
+    }
+    HIPCHK(h, hipMemsetAsync(h->xcnt, 0, 4, h->s));
+    h->x_bytes += total;
+    h->x_calls++;
+    return 0;
+}
+
+// sum of a host value over all shards (G small: through the size exchange)
+int shard_sum(swimsim *h, uint64_t v, uint64_t *out) {
+    if (h->G == 1) { *out = v; return 0; }
+    std::vector<uint64_t> send(h->G, v), recv(h->G);
+    if (int rc = h->xp->sizes(send.data(), recv.data(), 1)) return h->fail(rc, "shard reduction failed");
+    uint64_t t = 0;
+    for (uint64_t x : recv) t += x;
+    *out = t;
     return 0;
 }
 
@@ -337,34 +591,59 @@ int ensure_clean_checksum(swimsim *h, uint32_t ol) {
     return 0;
 }
 
-// sendPingWithChanges o → t, response discarded (heal_partition.go:97-124)
-int ping_with(swimsim *h, uint32_t o, uint32_t t, const MsgDesc *md_dev) {
-    ensure_clean_checksum(h, o - h->lo);
-    uint32_t sinc_cs[2];
-    uint32_t w;
-    HIPCHK(h, hipMemcpyAsync(&w, h->d.mw + (size_t)(o - h->lo) * h->NP + o, 4, hipMemcpyDeviceToHost, h->s));
-    HIPCHK(h, hipMemcpyAsync(&sinc_cs[1], h->d.cs + (o - h->lo), 4, hipMemcpyDeviceToHost, h->s));
-    HIPCHK(h, hipStreamSynchronize(h->s));
-    sinc_cs[0] = w >> 3;
-    hipMemsetAsync(h->defer_cnt, 0, 4, h->s);
-    hipLaunchKernelGGL(k_ping_with, dim3(1), dim3(64), 0, h->s, h->d, t - h->lo, o, md_dev, sinc_cs[0], sinc_cs[1],
-                       h->hdesc + 7, h->defer, h->defer_cnt, h->round);
-    resolve_deferred(h, 2, h->hdesc + 6, 1);
+inline bool own(const swimsim *h, uint32_t o) { return o >= h->lo && o < h->lo + h->NL; }
+
+int push_item(swimsim *h, uint4 it) {
+    hipLaunchKernelGGL(k_x_item, dim3(1), dim3(64), 0, h->s, h->d, it, h->xitems, h->xcnt, h->xcap);
     return 0;
 }
 
+// sendPingWithChanges o → t, response discarded (heal_partition.go:97-124); the message sits in
+// hdesc[slot] of o's shard. Collective when the cluster is sharded.
+int ping_with(swimsim *h, uint32_t o, uint32_t t, int slot) {
+    const uint32_t root = owner_host(h, o), ot = owner_host(h, t);
+    if (h->rank == root) {
+        ensure_clean_checksum(h, o - h->lo);
+        hipLaunchKernelGGL(k_sender_info, dim3(1), dim3(64), 0, h->s, h->d, o - h->lo, h->hsics);
+    }
+    const MsgDesc *md = h->hdesc + slot;
+    const uint32_t *sics = h->hsics;
+    if (h->G > 1) {
+        if (h->rank == root) {
+            HIPCHK(h, hipMemcpyAsync(h->hdesc + 7, h->hdesc + slot, sizeof(MsgDesc), hipMemcpyDeviceToDevice, h->s));
+            push_item(h, make_uint4(ot, P_PING, t, o));
+        }
+        if (int rc = xchg(h)) return rc;
+        md = h->hdesc + 5;
+        sics = h->hsics + 2;
+    }
+    if (h->rank == ot) {
+        hipMemsetAsync(h->defer_cnt, 0, 4, h->s);
+        hipLaunchKernelGGL(k_ping_with, dim3(1), dim3(64), 0, h->s, h->d, t - h->lo, o, md, sics, h->hdesc + 8,
+                           h->defer, h->defer_cnt, h->round);
+        resolve_deferred(h, 2, h->hdesc + 9, 1);
+    }
+    return 0;
+}
+
+// discoverProviderHealer.Heal on observer o (heal_via_discover_provider.go:120-177). o's shard
+// decides; the target's membership comes from the target's shard. Collective when sharded.
 int do_heal(swimsim *h, uint32_t o, std::vector<int32_t> *ret) {
+    const uint32_t root = owner_host(h, o);
+    const bool me = h->rank == root;
     const uint32_t ol = o - h->lo;
-    std::vector<uint32_t> row(h->NP);
-    HIPCHK(h, hipMemcpyAsync(row.data(), h->d.mw + (size_t)ol * h->NP, h->NP * 4, hipMemcpyDeviceToHost, h->s));
-    HIPCHK(h, hipStreamSynchronize(h->s));
     std::vector<int32_t> targets;
-    for (uint32_t m = 0; m < h->N; m++)                                      // heal_via_discover_provider.go:136-142
-        if ((row[m] & 7u) >= ST_FAULTY) targets.push_back((int32_t)m);
-    for (uint32_t i = 0; i < targets.size(); i++) {                          // ShuffleStringsInPlace (util.go:189-194)
-        const U4 v = philox10(h->round, o, 3u, i >> 2, h->seed);
-        const uint32_t j = mulhi_n(pick(v, i), i + 1);
-        std::swap(targets[i], targets[j]);
+    if (me) {
+        std::vector<uint32_t> row(h->NP);
+        HIPCHK(h, hipMemcpyAsync(row.data(), h->d.mw + (size_t)ol * h->NP, h->NP * 4, hipMemcpyDeviceToHost, h->s));
+        HIPCHK(h, hipStreamSynchronize(h->s));
+        for (uint32_t m = 0; m < h->N; m++)                                  // heal_via_discover_provider.go:136-142
+            if ((row[m] & 7u) >= ST_FAULTY) targets.push_back((int32_t)m);
+        for (uint32_t i = 0; i < targets.size(); i++) {                      // ShuffleStringsInPlace (util.go:189-194)
+            const U4 v = philox10(h->round, o, 3u, i >> 2, h->seed);
+            const uint32_t j = mulhi_n(pick(v, i), i + 1);
+            std::swap(targets[i], targets[j]);
+        }
     }
     auto del = [](std::vector<int32_t> &t, int32_t v) {                      // del (…:181-191)
         for (size_t i = 0; i < t.size(); i++) {
@@ -375,52 +654,81 @@ int do_heal(swimsim *h, uint32_t o, std::vector<int32_t> *ret) {
         }
     };
     int failures = 0;
-    while (!targets.empty() && failures < 10) {
-        const int32_t target = targets[0];
-        del(targets, target);
-        h->host_ctr[SWIMSIM_C_HEAL_ATTEMPTS]++;
-        if (!host_reach(h, o, (uint32_t)target)) {                           // sendJoinRequest fails
-            failures++;
-            h->host_ctr[SWIMSIM_C_HEAL_FAILURES]++;
+    for (;;) {
+        int32_t cmd = (me && !targets.empty() && failures < 10) ? targets[0] : -1;
+        if (h->G > 1)
+            if (int rc = h->xp->bcast(&cmd, sizeof cmd, root)) return h->fail(rc, "heal broadcast failed");
+        if (cmd < 0) break;
+        const uint32_t target = (uint32_t)cmd;
+        if (me) {
+            del(targets, cmd);
+            h->host_ctr[SWIMSIM_C_HEAL_ATTEMPTS]++;
+        }
+        if (!host_reach(h, o, target)) {                                     // sendJoinRequest fails
+            if (me) {
+                failures++;
+                h->host_ctr[SWIMSIM_C_HEAL_FAILURES]++;
+            }
             continue;
         }
-        const uint32_t tol = (uint32_t)target - h->lo;
+        const uint32_t ot = owner_host(h, target);
         HIPCHK(h, hipMemsetAsync(h->d.dense_cur, 0, 4, h->s));
-        hipLaunchKernelGGL(k_snapshot_row, dim3(1), dim3(64), 0, h->s, h->d, ol, h->hdesc + 0);      // MA
-        hipLaunchKernelGGL(k_snapshot_row, dim3(1), dim3(64), 0, h->s, h->d, tol, h->hdesc + 1);     // MB
-        hipLaunchKernelGGL(k_heal_diff, dim3(1), dim3(64), 0, h->s, h->d, h->hdesc + 0, h->hdesc + 1, h->hdesc + 2,
-                           h->hdesc + 3);
+        if (h->G == 1) {
+            hipLaunchKernelGGL(k_snapshot_row, dim3(1), dim3(64), 0, h->s, h->d, target - h->lo, h->hdesc + 1);   // MB
+        } else {
+            if (h->rank == ot) {
+                hipLaunchKernelGGL(k_snapshot_row, dim3(1), dim3(64), 0, h->s, h->d, target - h->lo, h->hdesc + 6);
+                push_item(h, make_uint4(root, P_HEALROW, target, 0));
+            }
+            if (int rc = xchg(h)) return rc;
+        }
+        uint32_t lens[2] = {0, 0};
         MsgDesc hd[4];
-        HIPCHK(h, hipMemcpyAsync(hd, h->hdesc, sizeof hd, hipMemcpyDeviceToHost, h->s));
-        HIPCHK(h, hipStreamSynchronize(h->s));
-        if (hd[0].kind != 1 || hd[1].kind != 1) return h->fail(SWIMSIM_ECAPACITY, "dense snapshot pool overflow in heal");
-        if (hd[2].len || hd[3].len) {                                        // reincarnateNodes (97-108)
-            if (hd[2].len) hipLaunchKernelGGL(k_apply_msg, dim3(1), dim3(64), 0, h->s, h->d, ol, h->hdesc + 2, h->round);
-            if (hd[3].len)
-                if (int rc = ping_with(h, o, (uint32_t)target, h->hdesc + 3)) return rc;
+        if (me) {
+            hipLaunchKernelGGL(k_snapshot_row, dim3(1), dim3(64), 0, h->s, h->d, ol, h->hdesc + 0);          // MA
+            hipLaunchKernelGGL(k_heal_diff, dim3(1), dim3(64), 0, h->s, h->d, h->hdesc + 0, h->hdesc + 1, h->hdesc + 2,
+                               h->hdesc + 3);
+            HIPCHK(h, hipMemcpyAsync(hd, h->hdesc, sizeof hd, hipMemcpyDeviceToHost, h->s));
+            HIPCHK(h, hipStreamSynchronize(h->s));
+            if (hd[0].kind != 1 || hd[1].kind != 1) return h->fail(SWIMSIM_ECAPACITY, "dense snapshot pool overflow in heal");
+            lens[0] = hd[2].len;
+            lens[1] = hd[3].len;
+        }
+        if (h->G > 1)
+            if (int rc = h->xp->bcast(lens, sizeof lens, root)) return h->fail(rc, "heal broadcast failed");
+        if (lens[0] || lens[1]) {                                            // reincarnateNodes (97-108)
+            if (me && lens[0]) hipLaunchKernelGGL(k_apply_msg, dim3(1), dim3(64), 0, h->s, h->d, ol, h->hdesc + 2, h->round);
+            if (lens[1])
+                if (int rc = ping_with(h, o, target, 3)) return rc;
         } else {                                                             // mergePartitions (112-124)
-            hipLaunchKernelGGL(k_apply_msg, dim3(1), dim3(64), 0, h->s, h->d, ol, h->hdesc + 1, h->round);
-            hipLaunchKernelGGL(k_snapshot_row, dim3(1), dim3(64), 0, h->s, h->d, ol, h->hdesc + 4);
-            if (int rc = ping_with(h, o, (uint32_t)target, h->hdesc + 4)) return rc;
+            if (me) {
+                hipLaunchKernelGGL(k_apply_msg, dim3(1), dim3(64), 0, h->s, h->d, ol, h->hdesc + 1, h->round);
+                hipLaunchKernelGGL(k_snapshot_row, dim3(1), dim3(64), 0, h->s, h->d, ol, h->hdesc + 4);
+            }
+            if (int rc = ping_with(h, o, target, 4)) return rc;
         }
-        std::vector<uint32_t> mb(h->NP);                                     // pingableHosts(MB)
-        HIPCHK(h, hipMemcpyAsync(mb.data(), h->d.dense + (size_t)hd[1].off_lo * h->NP, h->NP * 4, hipMemcpyDeviceToHost,
-                                 h->s));
-        HIPCHK(h, hipStreamSynchronize(h->s));
-        for (uint32_t m = 0; m < h->N; m++) {
-            const uint32_t st = mb[m] & 7u;
-            if (st != ST_UNKNOWN && is_pingable(st == ST_TOMB ? ST_FAULTY : st)) del(targets, (int32_t)m);
+        if (me) {
+            std::vector<uint32_t> mb(h->NP);                                 // pingableHosts(MB)
+            HIPCHK(h, hipMemcpyAsync(mb.data(), h->d.dense + (size_t)hd[1].off_lo * h->NP, h->NP * 4,
+                                     hipMemcpyDeviceToHost, h->s));
+            HIPCHK(h, hipStreamSynchronize(h->s));
+            for (uint32_t m = 0; m < h->N; m++) {
+                const uint32_t st = mb[m] & 7u;
+                if (st != ST_UNKNOWN && is_pingable(st == ST_TOMB ? ST_FAULTY : st)) del(targets, (int32_t)m);
+            }
+            if (ret) ret->push_back(cmd);
         }
-        if (ret) ret->push_back(target);
     }
     return 0;
 }
 
-// one protocol round (docs/ROUND_SEMANTICS.md §4)
+// one protocol round (docs/ROUND_SEMANTICS.md §4). With G > 1 shards every call is collective: the
+// exchanges sit at the same points on every shard.
 int step_one(swimsim *h, const swimsim_event *ev, size_t nev) {
     const uint32_t r = h->round;
+    const bool sharded = h->G > 1;
     HIPCHK(h, hipMemsetAsync(h->d.pool_cur, 0, 8, h->s));
-    // ---- E: events ----
+    // ---- E: events (the event list is the same on every shard; row events act on owned rows) ----
     std::vector<uint4> batch;
     bool topo_dirty = false;
     for (size_t i = 0; i < nev; i++) {
@@ -432,12 +740,12 @@ int step_one(swimsim *h, const swimsim_event *ev, size_t nev) {
         case SWIMSIM_EV_KILL: h->live[a] = 0; topo_dirty = true; break;
         case SWIMSIM_EV_REVIVE:
             h->live[a] = 1; topo_dirty = true;
-            batch.push_back(make_uint4(2, a, a, 0));
+            if (own(h, a)) batch.push_back(make_uint4(2, a, a, 0));
             break;
-        case SWIMSIM_EV_REINCARNATE: if (h->live[a]) batch.push_back(make_uint4(2, a, a, 0)); break;
-        case SWIMSIM_EV_LEAVE: if (h->live[a]) batch.push_back(make_uint4(3, a, a, 0)); break;
+        case SWIMSIM_EV_REINCARNATE: if (h->live[a] && own(h, a)) batch.push_back(make_uint4(2, a, a, 0)); break;
+        case SWIMSIM_EV_LEAVE: if (h->live[a] && own(h, a)) batch.push_back(make_uint4(3, a, a, 0)); break;
         case SWIMSIM_EV_PARTITION: h->part[a] = e.b; topo_dirty = true; break;
-        case SWIMSIM_EV_REAP: if (h->live[a]) batch.push_back(make_uint4(4, a, a, 0)); break;
+        case SWIMSIM_EV_REAP: if (h->live[a] && own(h, a)) batch.push_back(make_uint4(4, a, a, 0)); break;
         case SWIMSIM_EV_HEAL:
             if (!h->live[a]) break;
             if (int rc = flush_events(h, batch)) return rc;
@@ -466,29 +774,44 @@ int step_one(swimsim *h, const swimsim_event *ev, size_t nev) {
     }
     // ---- I: issue (ping requests) ----
     checksum_dirty(h, 1);
+    uint32_t *hi = h->hinfo;
+    uint32_t ninbox = h->NL;
     {
         Scope sc(h, F_ISSUE);
         hipLaunchKernelGGL(k_issue, dim3(blocks_for_waves(h->NL)), dim3(256), 0, h->s, h->d, 0, h->tgt, h->failed,
                            h->sdesc, h->sI, h->sC);
         HIPCHK(h, hipMemsetAsync(h->info + 2, 0, 4, h->s));
-        hipLaunchKernelGGL(k_pairs_direct, dim3(blocks_for_threads(h->NL)), dim3(256), 0, h->s, h->d, h->tgt, h->keys_in,
-                           h->vals_in, h->failed, h->info);
+        hipLaunchKernelGGL(k_pairs_direct, dim3(blocks_for_threads(h->NL)), dim3(256), 0, h->s, h->d, h->tgt, h->keys,
+                           h->failed, h->info, h->xitems, h->xcnt, h->xcap);
+    }
+    if (sharded) {                                                   // requests to targets on other shards
+        HIPCHK(h, hipMemcpyAsync(h->npairs, &h->NL, 4, hipMemcpyHostToDevice, h->s));
+        if (int rc = xchg(h)) return rc;
+        HIPCHK(h, hipMemcpyAsync(&hi[5], h->npairs, 4, hipMemcpyDeviceToHost, h->s));
     }
     // ---- D: deliver in waves ----
-    uint32_t *hi = h->hinfo;
     HIPCHK(h, hipMemcpyAsync(hi + 4, h->info + 2, 4, hipMemcpyDeviceToHost, h->s));
-    if (int rc = sort_inbox(h, h->NL, hi)) return rc;
+    HIPCHK(h, hipStreamSynchronize(h->s));
+    if (sharded) ninbox = std::min(hi[5], h->keycap);
     const uint32_t nfailed = hi[4];
+    if (int rc = sort_inbox(h, ninbox, hi)) return rc;
     HIPCHK(h, hipMemsetAsync(h->d.dense_cur, 0, 4, h->s));
     run_waves(h, 0, hi[0], hi[1]);
+    if (sharded) {                                                   // responses to senders on other shards
+        hipLaunchKernelGGL(k_x_resp, dim3(blocks_for_threads(ninbox)), dim3(256), 0, h->s, h->d, h->keys, ninbox, 0,
+                           h->xitems, h->xcnt, h->xcap);
+        if (int rc = xchg(h)) return rc;
+    }
     // ---- R: responses ----
     {
         Scope sc(h, F_RESP);
         hipLaunchKernelGGL(k_resp, dim3(blocks_for_waves(h->NL)), dim3(256), 0, h->s, h->d, h->tgt, h->failed, h->sdesc,
                            h->rdesc, r);
     }
-    // ---- Q: indirect pings ----
-    if (nfailed) {
+    // ---- Q: indirect pings (collective if any shard has a failed ping) ----
+    uint64_t anyfailed = nfailed;
+    if (int rc = shard_sum(h, nfailed, &anyfailed)) return rc;
+    if (anyfailed) {
         {
             Scope sc(h, F_PINGREQ);
             hipLaunchKernelGGL(k_helpers, dim3(blocks_for_threads(h->NL)), dim3(256), 0, h->s, h->d, h->tgt, h->failed,
@@ -500,26 +823,57 @@ int step_one(swimsim *h, const swimsim_event *ev, size_t nev) {
             hipLaunchKernelGGL(k_issue, dim3(blocks_for_waves(h->NL)), dim3(256), 0, h->s, h->d, 1, h->tgt, h->failed,
                                h->sdesc2, h->sI2, h->sC2);
             hipLaunchKernelGGL(k_pairs_helpers, dim3(blocks_for_threads(h->NL * h->K)), dim3(256), 0, h->s, h->d,
-                               h->failed, h->H, h->nh, h->keys_in, h->vals_in);
+                               h->failed, h->H, h->nh, h->keys, h->xitems, h->xcnt, h->xcap);
         }
-        if (int rc = sort_inbox(h, h->NL * h->K, hi)) return rc;
+        uint32_t ninbox2 = h->NL * h->K;
+        if (sharded) {
+            HIPCHK(h, hipMemcpyAsync(h->npairs, &ninbox2, 4, hipMemcpyHostToDevice, h->s));
+            if (int rc = xchg(h)) return rc;
+            HIPCHK(h, hipMemcpyAsync(&hi[5], h->npairs, 4, hipMemcpyDeviceToHost, h->s));
+            HIPCHK(h, hipStreamSynchronize(h->s));
+            ninbox2 = std::min(hi[5], h->keycap);
+        }
+        if (int rc = sort_inbox(h, ninbox2, hi)) return rc;
         HIPCHK(h, hipMemsetAsync(h->d.dense_cur, 0, 4, h->s));
         run_waves(h, 1, hi[0], hi[1]);
+        if (sharded) {
+            hipLaunchKernelGGL(k_x_resp, dim3(blocks_for_threads(ninbox2)), dim3(256), 0, h->s, h->d, h->keys, ninbox2, 1,
+                               h->xitems, h->xcnt, h->xcap);
+            if (int rc = xchg(h)) return rc;
+        }
         {
             Scope sc(h, F_PINGREQ);
             hipLaunchKernelGGL(k_resolve, dim3(blocks_for_waves(h->NL)), dim3(256), 0, h->s, h->d, h->tgt, h->failed,
                                h->H, h->nh, h->sdesc2, h->rdesc2, r);
         }
     }
-    // ---- F: reverse full syncs ----
+    // ---- F: reverse full syncs (sources on other shards are requested, snapshotted there, shipped) ----
     {
         Scope sc(h, F_JOBS);
         HIPCHK(h, hipMemsetAsync(h->d.dense_cur, 0, 4, h->s));
         hipLaunchKernelGGL(k_jobs_mark, dim3(blocks_for_threads(h->NL)), dim3(256), 0, h->s, h->d, h->need);
+    }
+    if (sharded) {
+        HIPCHK(h, hipMemsetAsync(h->needcnt, 0, 4, h->s));
+        hipLaunchKernelGGL(k_x_need, dim3(blocks_for_threads(h->N)), dim3(256), 0, h->s, h->d, h->need, h->xitems,
+                           h->xcnt, h->xcap);
+        if (int rc = xchg(h)) return rc;
+    }
+    {
+        Scope sc(h, F_JOBS);
         hipLaunchKernelGGL(k_jobs_snap, dim3(blocks_for_waves(h->NL)), dim3(256), 0, h->s, h->d, h->need, h->snapdesc);
+    }
+    if (sharded) {
+        hipLaunchKernelGGL(k_x_snap, dim3(blocks_for_threads(h->needcap)), dim3(256), 0, h->s, h->d, h->needlist,
+                           h->needcnt, h->xitems, h->xcnt, h->xcap);
+        if (int rc = xchg(h)) return rc;
+    }
+    {
+        Scope sc(h, F_JOBS);
         for (uint32_t q = 0; q < h->maxjobs; q++)
             hipLaunchKernelGGL(k_jobs_merge, dim3(blocks_for_waves(h->NL)), dim3(256), 0, h->s, h->d, q, h->snapdesc, r);
-        hipLaunchKernelGGL(k_jobs_reset, dim3(blocks_for_threads(h->NL)), dim3(256), 0, h->s, h->d, h->need);
+        hipLaunchKernelGGL(k_jobs_reset, dim3(blocks_for_threads(std::max(h->NL, h->N))), dim3(256), 0, h->s, h->d,
+                           h->need);
     }
     // ---- C: checksums of dirty rows ----
     checksum_dirty(h, 0);
@@ -547,6 +901,40 @@ int to_e(swimsim *h, int64_t inc_ms, uint32_t *e) {
 }
 
 inline int64_t from_e(const swimsim *h, uint32_t e) { return h->t0 + (int64_t)e * h->period; }
+
+// canonical split of N observer rows over G shards: shard r holds [N*r/G, N*(r+1)/G)
+std::vector<uint32_t> canonical_split(uint32_t N, uint32_t G) {
+    std::vector<uint32_t> lo(G + 1);
+    for (uint32_t r = 0; r <= G; r++) lo[r] = (uint32_t)((uint64_t)N * r / G);
+    return lo;
+}
+
+int set_shards(swimsim *h, uint32_t G, uint32_t rank, const std::vector<uint32_t> &lo) {
+    if (lo[rank] != h->lo || lo[rank + 1] != h->lo + h->NL)
+        return h->fail(SWIMSIM_EINVAL, "observer range [%u, %u) is not shard %u of %u ([%u, %u))", h->lo, h->lo + h->NL,
+                       rank, G, lo[rank], lo[rank + 1]);
+    int rc = 0;
+    uint32_t *sl = nullptr;
+    h->xcap = (uint32_t)((size_t)h->N * h->K + h->N + 64);
+    h->needcap = h->NL * (G - 1) + 64;
+    if ((rc = dalloc(h, &sl, G + 1, "shard table")) || (rc = dalloc(h, &h->xitems, h->xcap, "exchange items")) ||
+        (rc = dalloc(h, &h->xcnt, 1, "exchange count")) || (rc = dalloc(h, &h->xsz, 2 * G, "exchange sizes")) ||
+        (rc = dalloc(h, &h->xseg, 3 * G, "exchange cursors")) || (rc = dalloc(h, &h->xsrcs, G, "exchange sources")) ||
+        (rc = dalloc(h, &h->needlist, h->needcap, "need list")) || (rc = dalloc(h, &h->needcnt, 1, "need count")))
+        return rc;
+    h->xtcur = h->xseg + G;
+    h->xdcur = h->xseg + 2 * G;
+    HIPCHK(h, hipMemcpy(sl, lo.data(), (G + 1) * 4, hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemset(h->xcnt, 0, 4));
+    HIPCHK(h, hipMemset(h->needcnt, 0, 4));
+    h->G = G;
+    h->rank = rank;
+    h->shard_lo = lo;
+    h->d.G = G;
+    h->d.rank = rank;
+    h->d.shard_lo = sl;
+    return 0;
+}
 
 }  // namespace
 
@@ -684,42 +1072,55 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
         (rc = dalloc(h, &d.dense_len, d.dense_cap, "dense len")) || (rc = dalloc(h, &d.dense_last, d.dense_cap, "dense last")) ||
         (rc = dalloc(h, &d.dense_cs, d.dense_cap, "dense cs")))
         return bail(rc);
-    // work buffers
-    const size_t NLK = (size_t)h->NL * h->K;
+    // work buffers. Message descriptors are indexed by global observer id (a shard imports the
+    // messages of remote senders there); inbox arrays hold local pairs plus imported ones.
+    const size_t NLK = (size_t)h->NL * h->K, NK = (size_t)h->N * h->K;
+    h->keycap = (uint32_t)(NK + 64);
+    const size_t KC = h->keycap;
     if ((rc = dalloc(h, &h->tgt, h->NL, "tgt")) || (rc = dalloc(h, &h->failed, h->NL, "failed")) ||
-        (rc = dalloc(h, &h->sdesc, h->NL, "sdesc")) || (rc = dalloc(h, &h->rdesc, h->NL, "rdesc")) ||
-        (rc = dalloc(h, &h->sdesc2, h->NL, "sdesc2")) || (rc = dalloc(h, &h->rdesc2, NLK, "rdesc2")) ||
-        (rc = dalloc(h, &h->snapdesc, h->NL, "snapdesc")) || (rc = dalloc(h, &h->hdesc, 8, "hdesc")) ||
-        (rc = dalloc(h, &h->sI, h->NL, "sI")) || (rc = dalloc(h, &h->sC, h->NL, "sC")) ||
-        (rc = dalloc(h, &h->sI2, h->NL, "sI2")) || (rc = dalloc(h, &h->sC2, h->NL, "sC2")) ||
+        (rc = dalloc(h, &h->sdesc, h->N, "sdesc")) || (rc = dalloc(h, &h->rdesc, h->N, "rdesc")) ||
+        (rc = dalloc(h, &h->sdesc2, h->N, "sdesc2")) || (rc = dalloc(h, &h->rdesc2, NK, "rdesc2")) ||
+        (rc = dalloc(h, &h->snapdesc, h->N, "snapdesc")) || (rc = dalloc(h, &h->hdesc, 10, "hdesc")) ||
+        (rc = dalloc(h, &h->sI, h->N, "sI")) || (rc = dalloc(h, &h->sC, h->N, "sC")) ||
+        (rc = dalloc(h, &h->sI2, h->N, "sI2")) || (rc = dalloc(h, &h->sC2, h->N, "sC2")) ||
         (rc = dalloc(h, &h->H, NLK, "H")) || (rc = dalloc(h, &h->nh, h->NL, "nh")) ||
-        (rc = dalloc(h, &h->keys_in, NLK, "keys_in")) || (rc = dalloc(h, &h->vals_in, NLK, "vals_in")) ||
-        (rc = dalloc(h, &h->keys_out, NLK, "keys_out")) || (rc = dalloc(h, &h->vals_out, NLK, "vals_out")) ||
-        (rc = dalloc(h, &h->ukeys, NLK, "ukeys")) || (rc = dalloc(h, &h->counts, NLK, "counts")) ||
-        (rc = dalloc(h, &h->offs, NLK, "offs")) || (rc = dalloc(h, &h->nruns, 1, "nruns")) ||
-        (rc = dalloc(h, &h->info, 8, "info")) || (rc = dalloc(h, &h->list, NLK + 2 * (size_t)h->NL + 64, "list")) ||
-        (rc = dalloc(h, &h->cnt, 1, "cnt")) || (rc = dalloc(h, &h->defer, NLK + 2 * (size_t)h->NL + 64, "defer")) ||
+        (rc = dalloc(h, &h->keys, KC, "keys")) || (rc = dalloc(h, &h->keys_sorted, KC, "keys_sorted")) ||
+        (rc = dalloc(h, &h->keys_in, KC, "receivers")) || (rc = dalloc(h, &h->vals_out, KC, "vals_out")) ||
+        (rc = dalloc(h, &h->ukeys, KC, "ukeys")) || (rc = dalloc(h, &h->counts, KC, "counts")) ||
+        (rc = dalloc(h, &h->offs, KC, "offs")) || (rc = dalloc(h, &h->nruns, 1, "nruns")) ||
+        (rc = dalloc(h, &h->info, 8, "info")) || (rc = dalloc(h, &h->list, KC + 2 * (size_t)h->NL + 64, "list")) ||
+        (rc = dalloc(h, &h->cnt, 1, "cnt")) || (rc = dalloc(h, &h->defer, KC + 2 * (size_t)h->NL + 64, "defer")) ||
         (rc = dalloc(h, &h->defer_cnt, 1, "defer_cnt")) || (rc = dalloc(h, &h->exh_list, h->NL, "exh_list")) ||
         (rc = dalloc(h, &h->exh_cnt, 1, "exh_cnt")) || (rc = dalloc(h, &h->scratch, (size_t)64 * (h->NP / 32), "scratch")) ||
-        (rc = dalloc(h, &h->need, h->NL, "need")) || (rc = dalloc(h, &h->digest_buf, 4, "digest")) ||
-        (rc = dalloc(h, &h->fsflag, NLK, "fsflag")))
+        (rc = dalloc(h, &h->need, h->N, "need")) || (rc = dalloc(h, &h->digest_buf, 4, "digest")) ||
+        (rc = dalloc(h, &h->fsflag, KC, "fsflag")) || (rc = dalloc(h, &h->hsics, 4, "hsics")) ||
+        (rc = dalloc(h, &h->npairs, 1, "npairs")))
         return bail(rc);
     h->evcap = 4 * h->N + 64;
     if ((rc = dalloc(h, &h->evbuf, h->evcap, "events")) || (rc = dalloc(h, &h->ev_applied, h->evcap, "ev_applied")))
         return bail(rc);
     {
         size_t b1 = 0, b2 = 0, b3 = 0;
-        hipcub::DeviceRadixSort::SortPairs(nullptr, b1, h->keys_in, h->keys_out, h->vals_in, h->vals_out, (int)NLK, 0, 32);
-        hipcub::DeviceRunLengthEncode::Encode(nullptr, b2, h->keys_out, h->ukeys, h->counts, h->nruns, (int)NLK);
-        hipcub::DeviceScan::ExclusiveSum(nullptr, b3, h->counts, h->offs, (int)NLK);
+        hipcub::DeviceRadixSort::SortKeys(nullptr, b1, h->keys, h->keys_sorted, (int)KC, 0, 64);
+        hipcub::DeviceRunLengthEncode::Encode(nullptr, b2, h->keys_in, h->ukeys, h->counts, h->nruns, (int)KC);
+        hipcub::DeviceScan::ExclusiveSum(nullptr, b3, h->counts, h->offs, (int)KC);
         h->cub_bytes = std::max(b1, std::max(b2, b3));
         if ((rc = dalloc(h, (uint8_t **)&h->cub_tmp, h->cub_bytes, "cub temp"))) return bail(rc);
+    }
+    // single shard until swimsim_comm_attach / swimsim_group_create says otherwise
+    {
+        uint32_t *sl = nullptr;
+        if ((rc = dalloc(h, &sl, 2, "shard table"))) return bail(rc);
+        const uint32_t t2[2] = {0, h->N};
+        if (hipMemcpy(sl, t2, 8, hipMemcpyHostToDevice) != hipSuccess) return bail(SWIMSIM_EHIP);
+        h->shard_lo = {0, h->N};
+        d.G = 1; d.rank = 0; d.shard_lo = sl;
     }
     if (hipHostMalloc((void **)&h->hinfo, 64, 0) != hipSuccess) return bail(SWIMSIM_ENOMEM);
     hipMemset(d.ctr, 0, 32 * 8);
     hipMemset(d.err, 0, 4);
-    hipMemset(h->need, 0, h->NL);
-    hipMemset(h->fsflag, 0, NLK);
+    hipMemset(h->need, 0, h->N);
+    hipMemset(h->fsflag, 0, KC);
     hipMemset(d.njobs, 0, h->NL * 4);
     h->live.assign(h->N, 1);
     h->part.assign(h->N, 0);
@@ -735,6 +1136,9 @@ int swimsim_destroy(swimsim_t *h) {
     for (auto &t : h->pending) { hipEventDestroy(t.a); hipEventDestroy(t.b); }
     for (auto e : h->evpool) hipEventDestroy(e);
     for (void *p : h->allocs) hipFree(p);
+    if (h->sbuf) hipFree(h->sbuf);
+    if (h->rbuf) hipFree(h->rbuf);
+    h->xp.reset();
     if (h->hinfo) hipHostFree(h->hinfo);
     if (h->s) hipStreamDestroy(h->s);
     delete h;
@@ -750,7 +1154,6 @@ static int init_rows(swimsim_t *h, int mode) {
 int swimsim_init_converged(swimsim_t *h) { return h ? init_rows(h, 0) : SWIMSIM_EINVAL; }
 int swimsim_init_self_only(swimsim_t *h) { return h ? init_rows(h, 1) : SWIMSIM_EINVAL; }
 
-static bool own(const swimsim *h, uint32_t o) { return o >= h->lo && o < h->lo + h->NL; }
 
 int swimsim_set_member(swimsim_t *h, uint32_t o, uint32_t m, int32_t status, int64_t inc_ms) {
     if (!h || !own(h, o) || m >= h->N) return SWIMSIM_EINVAL;
@@ -804,6 +1207,7 @@ int swimsim_set_round(swimsim_t *h, uint32_t r) {
 
 int swimsim_step(swimsim_t *h, uint32_t nrounds, const swimsim_event *events, size_t nevents) {
     if (!h) return SWIMSIM_EINVAL;
+    if (h->G == 1 && h->NL != h->N) return h->fail(SWIMSIM_EINVAL, "a partial observer range needs a shard transport");
     for (uint32_t i = 0; i < nrounds; i++) {
         if (int rc = ensure_ecap(h, h->round + 1)) return rc;
         if (int rc = step_one(h, events, nevents)) return rc;
@@ -815,6 +1219,7 @@ int swimsim_step(swimsim_t *h, uint32_t nrounds, const swimsim_event *events, si
 
 int swimsim_heal(swimsim_t *h, uint32_t o, int32_t *targets, size_t cap, size_t *ntargets) {
     if (!h || !own(h, o)) return SWIMSIM_EINVAL;
+    if (h->G > 1) return h->fail(SWIMSIM_EINVAL, "sharded clusters heal through SWIMSIM_EV_HEAL events (collective)");
     std::vector<int32_t> ret;
     HIPCHK(h, hipMemsetAsync(h->d.pool_cur, 0, 8, h->s));
     if (int rc = do_heal(h, o, &ret)) return rc;
@@ -1063,6 +1468,98 @@ int swimsim_kernel_times(swimsim_t *h, const char **names, double *avg_ms, uint6
         }
     }
     if (n) *n = F_NFAM;
+    return SWIMSIM_OK;
+}
+
+// ---- shards ----
+int swimsim_group_create(const swimsim_config *cfg, uint32_t nshards, const int32_t *devices, swimsim_t **out) {
+    if (!cfg || !out || nshards < 1 || nshards > 64 || cfg->num_members < nshards) return SWIMSIM_EINVAL;
+    const std::vector<uint32_t> lo = canonical_split(cfg->num_members, nshards);
+    auto hub = std::make_shared<LocalHub>(nshards);
+    for (uint32_t i = 0; i < nshards; i++) out[i] = nullptr;
+    for (uint32_t i = 0; i < nshards; i++) {
+        swimsim_config c = *cfg;
+        c.observer_begin = lo[i];
+        c.observer_end = lo[i + 1];
+        if (devices) c.device = (uint32_t)devices[i];
+        int rc = swimsim_create(&c, &out[i]);
+        if (rc == 0 && nshards > 1) {
+            rc = set_shards(out[i], nshards, i, lo);
+            if (rc == 0) {
+                auto port = std::make_unique<LocalPort>();
+                port->G = nshards;
+                port->rank = i;
+                port->hub = hub;
+                port->device = out[i]->device;
+                out[i]->xp = std::move(port);
+            }
+        }
+        if (rc) {
+            for (uint32_t j = 0; j <= i; j++) {
+                swimsim_destroy(out[j]);
+                out[j] = nullptr;
+            }
+            return rc;
+        }
+    }
+    return SWIMSIM_OK;
+}
+
+int swimsim_group_step(swimsim_t *const *hs, uint32_t n, uint32_t nrounds, const swimsim_event *events, size_t nevents) {
+    if (!hs || n < 1) return SWIMSIM_EINVAL;
+    if (n == 1) return swimsim_step(hs[0], nrounds, events, nevents);
+    std::vector<int> rcs(n, 0);
+    std::vector<std::thread> th;
+    for (uint32_t i = 0; i < n; i++) {
+        th.emplace_back([&, i] {
+            hipSetDevice(hs[i]->device);
+            rcs[i] = swimsim_step(hs[i], nrounds, events, nevents);
+            if (rcs[i]) {
+                LocalPort *lp = dynamic_cast<LocalPort *>(hs[i]->xp.get());
+                if (lp) lp->hub->abort();                        // release the other shards' barriers
+            }
+        });
+    }
+    for (auto &t : th) t.join();
+    for (uint32_t i = 0; i < n; i++)
+        if (rcs[i]) return rcs[i];
+    return SWIMSIM_OK;
+}
+
+int swimsim_comm_unique_id(uint8_t *out, size_t cap) {
+    if (!out || cap < NCCL_UNIQUE_ID_BYTES) return SWIMSIM_EINVAL;
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return SWIMSIM_EHIP;
+    memcpy(out, id.internal, NCCL_UNIQUE_ID_BYTES);
+    return NCCL_UNIQUE_ID_BYTES;
+}
+
+int swimsim_comm_attach(swimsim_t *h, uint32_t nranks, uint32_t rank, const uint8_t *id, size_t len) {
+    if (!h || !id || len < NCCL_UNIQUE_ID_BYTES || rank >= nranks || h->G != 1) return SWIMSIM_EINVAL;
+    const std::vector<uint32_t> lo = canonical_split(h->N, nranks);
+    if (int rc = set_shards(h, nranks, rank, lo)) return rc;
+    ncclUniqueId uid;
+    memcpy(uid.internal, id, NCCL_UNIQUE_ID_BYTES);
+    auto port = std::make_unique<RcclPort>();
+    port->G = nranks;
+    port->rank = rank;
+    port->st = h->s;
+    HIPCHK(h, hipSetDevice(h->device));
+    const ncclResult_t nr = ncclCommInitRank(&port->comm, (int)nranks, uid, (int)rank);
+    if (nr != ncclSuccess) return h->fail(SWIMSIM_EHIP, "ncclCommInitRank: %s", ncclGetErrorString(nr));
+    h->xp = std::move(port);
+    return SWIMSIM_OK;
+}
+
+int swimsim_shard_info(swimsim_t *h, uint32_t *nshards, uint32_t *rank, uint32_t *lo, uint32_t *hi,
+                       uint64_t *xbytes, uint64_t *xcalls) {
+    if (!h) return SWIMSIM_EINVAL;
+    if (nshards) *nshards = h->G;
+    if (rank) *rank = h->rank;
+    if (lo) *lo = h->lo;
+    if (hi) *hi = h->lo + h->NL;
+    if (xbytes) *xbytes = h->x_bytes;
+    if (xcalls) *xcalls = h->x_calls;
     return SWIMSIM_OK;
 }
 

@@ -559,9 +559,9 @@ __global__ void k_issue(DS d, int mode, const int32_t *tgt, const uint8_t *faile
     MsgDesc md;
     wave_issue(d, ol, md);
     if (lane_id() == 0) {
-        sdesc[ol] = md;
-        sI[ol] = d.mw[(size_t)ol * d.NP + o] >> 3;
-        sC[ol] = d.cs[ol];
+        sdesc[o] = md;                                               // message descriptors are indexed by
+        sI[o] = d.mw[(size_t)ol * d.NP + o] >> 3;                    // global sender id (remote senders'
+        sC[o] = d.cs[ol];                                            // messages are imported there)
         if (mode == 0) {
             atomicAdd(&d.ctr[C_PINGS], 1ull);
             atomicAdd(&d.ctr[C_MSG_CHANGES], (unsigned long long)md.len);   // counted per helper call in Q2
@@ -573,20 +573,33 @@ __global__ void k_issue(DS d, int mode, const int32_t *tgt, const uint8_t *faile
 // ---------------------------------------------------------------------------------------------
 // phase D / Q2 inbox construction (sorted by receiver; ascending sender inside a receiver)
 // ---------------------------------------------------------------------------------------------
-__global__ void k_pairs_direct(DS d, const int32_t *tgt, uint32_t *keys, uint32_t *vals, uint8_t *failed,
-                               uint32_t *info) {
+// inbox keys are (receiver << 32 | sender value): sorting them orders every receiver's inbox by sender,
+// wherever the pair came from (local or imported from another shard)
+__device__ __forceinline__ void x_push(uint4 *items, uint32_t *cnt, uint32_t cap, uint32_t *err, uint4 it) {
+    const uint32_t i = atomicAdd(cnt, 1u);
+    if (i < cap) items[i] = it;
+    else atomicOr(err, E_XCAP);
+}
+
+__global__ void k_pairs_direct(DS d, const int32_t *tgt, unsigned long long *keys, uint8_t *failed, uint32_t *info,
+                               uint4 *xitems, uint32_t *xcnt, uint32_t xcap) {
     const uint32_t ol = blockIdx.x * blockDim.x + threadIdx.x;
     if (ol >= d.NL) return;
     const uint32_t o = d.lo + ol;
     const int32_t t = tgt[ol];
-    uint32_t key = d.N;
+    unsigned long long key = (unsigned long long)d.N << 32;
     uint8_t f = 0;
     if (t >= 0) {
-        if (reach(d, o, (uint32_t)t)) key = (uint32_t)t;
-        else { f = 1; atomicAdd(&info[2], 1u); }
+        if (!reach(d, o, (uint32_t)t)) {
+            f = 1;
+            atomicAdd(&info[2], 1u);
+        } else if (d.G > 1 && owner_of(d, (uint32_t)t) != d.rank) {
+            x_push(xitems, xcnt, xcap, d.err, make_uint4(owner_of(d, (uint32_t)t), 1u /*P_REQ*/, o, (uint32_t)t));
+        } else {
+            key = ((unsigned long long)(uint32_t)t << 32) | o;
+        }
     }
     keys[ol] = key;
-    vals[ol] = o;
     failed[ol] = f;
 }
 
@@ -626,19 +639,32 @@ __global__ void k_helpers(DS d, const int32_t *tgt, const uint8_t *failed, uint3
     nh[ol] = got;
 }
 
-__global__ void k_pairs_helpers(DS d, const uint8_t *failed, const uint32_t *H, const uint32_t *nh, uint32_t *keys,
-                                uint32_t *vals) {
+__global__ void k_pairs_helpers(DS d, const uint8_t *failed, const uint32_t *H, const uint32_t *nh,
+                                unsigned long long *keys, uint4 *xitems, uint32_t *xcnt, uint32_t xcap) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t K = d.K;
     if (i >= d.NL * K) return;
     const uint32_t ol = i / K, q = i % K, o = d.lo + ol;
-    uint32_t key = d.N;
+    unsigned long long key = (unsigned long long)d.N << 32;
     if (failed[ol] && q < nh[ol]) {
         const uint32_t h = H[i];
-        if (reach(d, o, h)) key = h;
+        if (reach(d, o, h)) {
+            if (d.G > 1 && owner_of(d, h) != d.rank)
+                x_push(xitems, xcnt, xcap, d.err, make_uint4(owner_of(d, h), 2u /*P_REQ2*/, o * K + q, h));
+            else
+                key = ((unsigned long long)h << 32) | (o * K + q);
+        }
     }
     keys[i] = key;
-    vals[i] = o * K + q;
+}
+
+// sorted 64-bit inbox keys → receiver column (run-length encoded next) and sender-value column
+__global__ void k_split_keys(const unsigned long long *keys, uint32_t n, uint32_t *recv, uint32_t *vals) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const unsigned long long k = keys[i];
+    recv[i] = (uint32_t)(k >> 32);
+    vals[i] = (uint32_t)k;
 }
 
 // runs: number of receivers (excluding the sentinel) and the longest inbox
@@ -660,9 +686,9 @@ struct RecvArgs {
     uint32_t nruns_max;
     uint32_t w;                                     // wave index
     int phase;                                      // 0: direct ping (phase D), 1: ping-req (Q2)
-    const MsgDesc *sdesc;                           // sender snapshots (by sender row)
+    const MsgDesc *sdesc;                           // sender snapshots (by global sender id)
     const uint32_t *sI, *sC;
-    MsgDesc *rdesc;                                 // responses (by sender row / (row, slot))
+    MsgDesc *rdesc;                                 // responses (by sender id / sender id * K + slot)
     uint4 *defer;                                   // {resp index, dense slot, sender checksum, pair index}
     uint32_t *defer_cnt;
     uint8_t *fsflag;                                // per inbox pair: the receiver answered with a full sync
@@ -673,10 +699,10 @@ struct RecvArgs {
 // empty and checksums differ. A dirty receiver snapshots its row (the full-sync payload) and the
 // decision waits for one batched checksum of all snapshots after the last wave. Reverse full syncs
 // are queued afterwards in inbox order (k_build_jobs).
-__device__ void recv_one(const DS &d, const RecvArgs &a, uint32_t j, uint32_t sender_row, uint32_t resp_idx,
+__device__ void recv_one(const DS &d, const RecvArgs &a, uint32_t j, uint32_t sender, uint32_t resp_idx,
                          uint32_t pair) {
     const uint32_t ol = j - d.lo;
-    const uint32_t sender = d.lo + sender_row;
+    const uint32_t sender_row = sender;                             // descriptor index = global sender id
     wave_merge_msg(d, ol, j, a.sdesc[sender_row], a.r, a.r);
     MsgDesc resp;
     const uint32_t kept = wave_issue_recv(d, ol, sender, a.sI[sender_row], resp);
@@ -711,11 +737,8 @@ __global__ void k_recv(DS d, RecvArgs a) {
     if (key >= d.N || a.counts[u] <= a.w) return;
     const uint32_t pair = a.offs[u] + a.w;
     const uint32_t v = a.vals[pair];
-    if (a.phase == 0) recv_one(d, a, key, v - d.lo, v - d.lo, pair);
-    else {
-        const uint32_t o = v / d.K, q = v % d.K;
-        recv_one(d, a, key, o - d.lo, (o - d.lo) * d.K + q, pair);
-    }
+    if (a.phase == 0) recv_one(d, a, key, v, v, pair);
+    else recv_one(d, a, key, v / d.K, v, pair);
 }
 
 // resolve deferred full-sync decisions once the snapshot checksums exist (phase 2 = heal ping:
@@ -773,8 +796,8 @@ __global__ void k_resp(DS d, const int32_t *tgt, const uint8_t *failed, const Ms
     if (ol >= d.NL) return;
     if (tgt[ol] < 0 || failed[ol]) return;
     const uint32_t o = d.lo + ol;
-    wave_bump(d, ol, sdesc[ol]);
-    wave_merge_msg(d, ol, o, rdesc[ol], r, r);
+    wave_bump(d, ol, sdesc[o]);
+    wave_merge_msg(d, ol, o, rdesc[o], r, r);
     if (lane_id() == 0) atomicAdd(&d.ctr[C_PINGS_OK], 1ull);
 }
 
@@ -789,9 +812,9 @@ __global__ void k_resolve(DS d, const int32_t *tgt, const uint8_t *failed, const
         const uint32_t h = H[(size_t)ol * K + q];
         if (!reach(d, o, h)) {
             errs++;
-            wave_bump(d, ol, sdesc2[ol]);                           // bump only on error (105-106)
+            wave_bump(d, ol, sdesc2[o]);                            // bump only on error (105-106)
         } else {
-            wave_merge_msg(d, ol, o, rdesc2[(size_t)ol * K + q], r, r);
+            wave_merge_msg(d, ol, o, rdesc2[(size_t)o * K + q], r, r);
         }
     }
     if (lane_id() == 0) {
@@ -813,30 +836,29 @@ __global__ void k_resolve(DS d, const int32_t *tgt, const uint8_t *failed, const
 __global__ void k_jobs_mark(DS d, uint8_t *need) {
     const uint32_t ol = blockIdx.x * blockDim.x + threadIdx.x;
     if (ol >= d.NL) return;
-    for (uint32_t q = 0; q < d.njobs[ol]; q++) need[d.jobs[(size_t)ol * d.maxjobs + q] - d.lo] = 1;
+    for (uint32_t q = 0; q < d.njobs[ol]; q++) need[d.jobs[(size_t)ol * d.maxjobs + q]] = 1;   // [N], global
 }
 
 __global__ void k_jobs_snap(DS d, const uint8_t *need, MsgDesc *snapdesc) {
     const uint32_t ol = wave_gid();
-    if (ol >= d.NL || !need[ol]) return;
+    if (ol >= d.NL || !need[d.lo + ol]) return;
     MsgDesc md;
     wave_snapshot(d, ol, d.lo + ol, md);
-    if (lane_id() == 0) snapdesc[ol] = md;
+    if (lane_id() == 0) snapdesc[d.lo + ol] = md;
 }
 
 __global__ void k_jobs_merge(DS d, uint32_t q, const MsgDesc *snapdesc, uint32_t r) {
     const uint32_t ol = wave_gid();
     if (ol >= d.NL || d.njobs[ol] <= q) return;
     const uint32_t src = d.jobs[(size_t)ol * d.maxjobs + q];
-    wave_merge_msg(d, ol, d.lo + ol, snapdesc[src - d.lo], r, r);
+    wave_merge_msg(d, ol, d.lo + ol, snapdesc[src], r, r);
     if (lane_id() == 0) atomicAdd(&d.ctr[C_RFS_DONE], 1ull);
 }
 
 __global__ void k_jobs_reset(DS d, uint8_t *need) {
-    const uint32_t ol = blockIdx.x * blockDim.x + threadIdx.x;
-    if (ol >= d.NL) return;
-    d.njobs[ol] = 0;
-    need[ol] = 0;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < d.NL) d.njobs[i] = 0;
+    if (i < d.N) need[i] = 0;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1232,14 +1254,22 @@ __global__ void k_heal_diff(DS d, const MsgDesc *ma, const MsgDesc *mb, MsgDesc 
     }
 }
 
+// I_o and C_o of observer row ol (the heal ping's sender fields)
+__global__ void k_sender_info(DS d, uint32_t ol, uint32_t *out) {
+    if (threadIdx.x) return;
+    out[0] = d.mw[(size_t)ol * d.NP + d.lo + ol] >> 3;
+    out[1] = d.cs[ol];
+}
+
 __global__ void k_apply_msg(DS d, uint32_t ol, const MsgDesc *md, uint32_t r) {
     wave_merge_msg(d, ol, d.lo + ol, *md, r, r);
 }
 
 // sendPingWithChanges o → t whose response is discarded (heal_partition.go:97-124): target runs
 // handlePing: Update, IssueAsReceiver(o, I_o, C_o); a full sync queues a reverse full sync
-__global__ void k_ping_with(DS d, uint32_t tol, uint32_t sender, const MsgDesc *md, uint32_t sinc, uint32_t scs,
+__global__ void k_ping_with(DS d, uint32_t tol, uint32_t sender, const MsgDesc *md, const uint32_t *sics,
                             MsgDesc *resp_out, uint4 *defer, uint32_t *defer_cnt, uint32_t r) {
+    const uint32_t sinc = sics[0], scs = sics[1];
     wave_merge_msg(d, tol, d.lo + tol, *md, r, r);
     MsgDesc resp;
     const uint32_t kept = wave_issue_recv(d, tol, sender, sinc, resp);

@@ -1,0 +1,224 @@
+// swimsim_xchg.hip — device side of the observer-row shard exchange.
+//
+// A cluster's observer rows may be split over G shards (one per GPU, or several in one process for
+// testing). Every message whose two ends live on different shards becomes a parcel: a 64-byte
+// header plus its payload (16-byte change records, or a dense NP-word row snapshot). Parcels are
+// produced from an item list {dest shard, type, index, key}, packed into one contiguous segment per
+// destination, moved by the transport (RCCL send/recv over xGMI, or peer copies inside one process)
+// and unpacked into the receiving shard's own message pool, dense pool and descriptor arrays, which
+// are indexed by global observer id. After an exchange the round's kernels run unchanged.
+//
+// Segment layout: [u32 parcel offsets, padded to 16 B][parcels]; each parcel 16-byte aligned.
+#pragma once
+
+namespace swimdev {
+
+enum ParcelType : uint32_t {
+    P_REQ = 1,      // direct ping request: sender o → target t (idx o, key t)
+    P_REQ2 = 2,     // ping-req: sender o → helper h (idx o*K+q, key h)
+    P_RESP = 3,     // response of a remote receiver to sender o (idx o)
+    P_RESP2 = 4,    // helper response (idx o*K+q)
+    P_NEED = 5,     // reverse-full-sync source request (idx = source row, key = requesting shard)
+    P_SNAP = 6,     // reverse-full-sync source snapshot (idx = source row)
+    P_HEALROW = 7,  // heal: target's membership for the healing observer
+    P_PING = 8      // heal: ping-with-changes to a remote target (idx target, key sender)
+};
+
+struct Parcel {                 // 64 bytes
+    uint32_t type, idx, key, kind;
+    uint32_t len, sI, sC, pbytes;
+    uint4 meta;
+    uint32_t dlen;
+    int32_t dlast;
+    uint32_t dcs, pad;
+};
+
+// descriptor arrays and scratch the exchange reads and fills
+struct XArgs {
+    MsgDesc *sdesc, *sdesc2, *rdesc, *rdesc2, *snapdesc, *hdesc;
+    uint32_t *sI, *sC, *sI2, *sC2;
+    uint32_t *hsics;              // [4]: heal ping sender fields (out: 0-1, in: 2-3)
+    uint8_t *need;                // [N]
+    unsigned long long *keys;     // inbox keys (imported pairs are appended)
+    uint32_t *npairs;             // append cursor of keys
+    uint32_t keycap;
+    uint2 *needlist;              // (source row, requesting shard) of imported P_NEED
+    uint32_t *needcnt;
+    uint32_t needcap;
+};
+
+__device__ __forceinline__ const MsgDesc *item_desc(const DS &d, const XArgs &x, uint4 it) {
+    switch (it.y) {
+    case P_REQ: return &x.sdesc[it.z];
+    case P_REQ2: return &x.sdesc2[it.z / d.K];
+    case P_RESP: return &x.rdesc[it.z];
+    case P_RESP2: return &x.rdesc2[it.z];
+    case P_SNAP: return &x.snapdesc[it.z];
+    case P_HEALROW: return &x.hdesc[6];
+    case P_PING: return &x.hdesc[7];
+    default: return nullptr;
+    }
+}
+
+__device__ __forceinline__ uint32_t payload_bytes(const DS &d, const MsgDesc *md) {
+    if (!md) return 0;
+    if (md->kind == 0) return md->len * 16u;
+    if (md->kind == 1) return d.NP * 4u;
+    return 0;
+}
+
+// per-destination parcel count and byte total
+__global__ void k_x_size(DS d, XArgs x, const uint4 *items, const uint32_t *cnt, uint32_t cap, unsigned long long *sz) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= min(*cnt, cap)) return;
+    const uint4 it = items[i];
+    const uint32_t b = (uint32_t)sizeof(Parcel) + payload_bytes(d, item_desc(d, x, it));
+    atomicAdd(&sz[2 * it.x], (unsigned long long)b);
+    atomicAdd(&sz[2 * it.x + 1], 1ull);
+}
+
+// one wave per item: claim a table slot and a parcel offset in the destination's segment, write both
+__global__ void k_x_pack(DS d, XArgs x, const uint4 *items, const uint32_t *cnt, uint32_t cap, uint8_t *buf,
+                         const unsigned long long *segoff, unsigned long long *tcur, unsigned long long *dcur) {
+    const uint32_t i = wave_gid();
+    if (i >= min(*cnt, cap)) return;
+    const uint4 it = items[i];
+    const MsgDesc *md = item_desc(d, x, it);
+    const uint32_t pb = payload_bytes(d, md);
+    unsigned long long off = 0, ti = 0;
+    if (lane_id() == 0) {
+        off = atomicAdd(&dcur[it.x], (unsigned long long)(sizeof(Parcel) + pb));
+        ti = atomicAdd(&tcur[it.x], 1ull);
+    }
+    off = bcast64(off);
+    ti = bcast64(ti);
+    uint8_t *seg = buf + segoff[it.x];
+    Parcel *pc = (Parcel *)(seg + off);
+    if (lane_id() == 0) {
+        ((uint32_t *)seg)[ti] = (uint32_t)off;
+        Parcel h{};
+        h.type = it.y; h.idx = it.z; h.key = it.w;
+        h.kind = md ? md->kind : 2u;
+        h.len = md ? md->len : 0u;
+        h.pbytes = pb;
+        if (it.y == P_REQ) { h.sI = x.sI[it.z]; h.sC = x.sC[it.z]; }
+        if (it.y == P_REQ2) { h.sI = x.sI2[it.z / d.K]; h.sC = x.sC2[it.z / d.K]; }
+        if (it.y == P_PING) { h.sI = x.hsics[0]; h.sC = x.hsics[1]; }
+        if (md && md->kind == 1) {
+            const uint32_t slot = md->off_lo;
+            h.meta = d.dense_meta[slot];
+            h.dlen = d.dense_len[slot];
+            h.dlast = d.dense_last[slot];
+            h.dcs = d.dense_cs[slot];
+        }
+        *pc = h;
+    }
+    if (!md || pb == 0) return;
+    uint4 *dst = (uint4 *)(pc + 1);
+    const uint4 *src = md->kind == 0
+                           ? d.pool + (((unsigned long long)md->off_hi << 32) | md->off_lo)
+                           : (const uint4 *)(d.dense + (size_t)md->off_lo * d.NP);
+    for (uint32_t k = lane_id(); k < pb / 16u; k += 64) dst[k] = src[k];
+}
+
+// one wave per received parcel; srcs[s] = {segment offset, parcel count, first global parcel index}
+__global__ void k_x_unpack(DS d, XArgs x, const uint8_t *buf, const ulonglong2 *srcs, uint32_t nsrc,
+                           uint32_t total) {
+    const uint32_t i = wave_gid();
+    if (i >= total) return;
+    uint32_t s = 0;
+    while (s + 1 < nsrc && i >= (uint32_t)srcs[s + 1].y) s++;
+    const uint8_t *seg = buf + srcs[s].x;
+    const uint32_t k = i - (uint32_t)srcs[s].y;
+    const Parcel *pc = (const Parcel *)(seg + ((const uint32_t *)seg)[k]);
+    const Parcel h = *pc;
+    const uint4 *payload = (const uint4 *)(pc + 1);
+    MsgDesc md;
+    md.kind = h.kind; md.len = h.len; md.off_lo = md.off_hi = 0;
+    if (h.kind == 0 && h.len) {                                    // change records → local pool
+        const unsigned long long off = pool_alloc(d, h.len);
+        if (off == ~0ull) return;
+        for (uint32_t q = lane_id(); q < h.len; q += 64) d.pool[off + q] = payload[q];
+        md.off_lo = (uint32_t)off;
+        md.off_hi = (uint32_t)(off >> 32);
+    } else if (h.kind == 1) {                                      // dense snapshot → local dense pool
+        uint32_t slot = 0;
+        if (lane_id() == 0) slot = atomicAdd(d.dense_cur, 1u);
+        slot = (uint32_t)__shfl((int)slot, 0, 64);
+        if (slot >= d.dense_cap) {
+            if (lane_id() == 0) atomicOr(d.err, E_DENSE);
+            return;
+        }
+        uint4 *dst = (uint4 *)(d.dense + (size_t)slot * d.NP);
+        for (uint32_t q = lane_id(); q < d.NP / 4; q += 64) dst[q] = payload[q];
+        if (lane_id() == 0) {
+            d.dense_meta[slot] = h.meta;
+            d.dense_len[slot] = h.dlen;
+            d.dense_last[slot] = h.dlast;
+            d.dense_cs[slot] = h.dcs;
+        }
+        md.off_lo = slot;
+    }
+    __threadfence_block();
+    if (lane_id() != 0) return;
+    switch (h.type) {
+    case P_REQ:
+    case P_REQ2: {
+        if (h.type == P_REQ) { x.sdesc[h.idx] = md; x.sI[h.idx] = h.sI; x.sC[h.idx] = h.sC; }
+        else { const uint32_t o = h.idx / d.K; x.sdesc2[o] = md; x.sI2[o] = h.sI; x.sC2[o] = h.sC; }
+        const uint32_t p = atomicAdd(x.npairs, 1u);
+        if (p < x.keycap) x.keys[p] = ((unsigned long long)h.key << 32) | h.idx;
+        else atomicOr(d.err, E_XCAP);
+        break;
+    }
+    case P_RESP: x.rdesc[h.idx] = md; break;
+    case P_RESP2: x.rdesc2[h.idx] = md; break;
+    case P_NEED: {
+        x.need[h.idx] = 1;
+        const uint32_t p = atomicAdd(x.needcnt, 1u);
+        if (p < x.needcap) x.needlist[p] = make_uint2(h.idx, h.key);
+        else atomicOr(d.err, E_XCAP);
+        break;
+    }
+    case P_SNAP: x.snapdesc[h.idx] = md; break;
+    case P_HEALROW: x.hdesc[1] = md; break;
+    case P_PING: x.hdesc[5] = md; x.hsics[2] = h.sI; x.hsics[3] = h.sC; break;
+    default: break;
+    }
+}
+
+// responses of local receivers to remote senders (after the receive waves resolved them)
+__global__ void k_x_resp(DS d, const unsigned long long *keys, uint32_t n, int phase, uint4 *items, uint32_t *cnt,
+                         uint32_t cap) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const unsigned long long k = keys[i];
+    if ((uint32_t)(k >> 32) >= d.N) return;
+    const uint32_t v = (uint32_t)k;
+    const uint32_t o = phase == 0 ? v : v / d.K;
+    const uint32_t r = owner_of(d, o);
+    if (r != d.rank) x_push(items, cnt, cap, d.err, make_uint4(r, phase == 0 ? P_RESP : P_RESP2, v, 0));
+}
+
+// reverse-full-sync sources held by other shards: one request per distinct source
+__global__ void k_x_need(DS d, const uint8_t *need, uint4 *items, uint32_t *cnt, uint32_t cap) {
+    const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
+    if (o >= d.N || !need[o]) return;
+    const uint32_t r = owner_of(d, o);
+    if (r != d.rank) x_push(items, cnt, cap, d.err, make_uint4(r, P_NEED, o, d.rank));
+}
+
+// snapshots for the shards that requested them (sources are local rows, snapshotted by k_jobs_snap)
+__global__ void k_x_snap(DS d, const uint2 *needlist, const uint32_t *needcnt, uint4 *items, uint32_t *cnt,
+                         uint32_t cap) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= *needcnt) return;
+    const uint2 e = needlist[i];
+    x_push(items, cnt, cap, d.err, make_uint4(e.y, P_SNAP, e.x, 0));
+}
+
+__global__ void k_x_item(DS d, uint4 it, uint4 *items, uint32_t *cnt, uint32_t cap) {
+    if (threadIdx.x == 0) x_push(items, cnt, cap, d.err, it);
+}
+
+}  // namespace swimdev

@@ -98,6 +98,12 @@ def load_library(path: str = LIB_PATH):
         "swimsim_kernel_times": (C.c_int, [P, P, P, P, P, sz, C.POINTER(sz)]),
         "swimsim_enable_timing": (C.c_int, [P, i32]),
         "swimsim_bench_checksum": (C.c_int, [P, u32, i32, i32, C.POINTER(C.c_double)]),
+        "swimsim_group_create": (C.c_int, [C.POINTER(Config), u32, P, P]),
+        "swimsim_group_step": (C.c_int, [P, u32, u32, C.POINTER(Event), sz]),
+        "swimsim_comm_unique_id": (C.c_int, [P, sz]),
+        "swimsim_comm_attach": (C.c_int, [P, u32, u32, P, sz]),
+        "swimsim_shard_info": (C.c_int, [P, C.POINTER(u32), C.POINTER(u32), C.POINTER(u32), C.POINTER(u32),
+                                         C.POINTER(u64), C.POINTER(u64)]),
     }
     for name, (res, args) in sigs.items():
         f = getattr(L, name)
@@ -114,15 +120,54 @@ def _events(events):
     return arr
 
 
+def make_config(n, *, t0_ms=T0_MS, period_ms=200, suspect_ms=5000, faulty_ms=24 * 3600 * 1000, tombstone_ms=60_000,
+                ping_request_size=3, max_rfs_jobs=5, p_factor=15, seed=1, device=0, max_rounds=0,
+                message_pool_bytes=0, observer_range=None):
+    cfg = Config()
+    cfg.num_members, cfg.device, cfg.t0_ms, cfg.protocol_period_ms = n, device, t0_ms, period_ms
+    cfg.suspect_timeout_ms, cfg.faulty_timeout_ms, cfg.tombstone_timeout_ms = suspect_ms, faulty_ms, tombstone_ms
+    cfg.ping_request_size, cfg.max_reverse_full_sync_jobs, cfg.p_factor = ping_request_size, max_rfs_jobs, p_factor
+    cfg.seed, cfg.max_rounds, cfg.message_pool_bytes = seed, max_rounds, message_pool_bytes
+    if observer_range:
+        cfg.observer_begin, cfg.observer_end = observer_range
+    return cfg
+
+
+def shard_range(n, nshards, rank):
+    """Observer rows of shard `rank` of `nshards` (the canonical split of include/swimsim.h)."""
+    return n * rank // nshards, n * (rank + 1) // nshards
+
+
+def unique_id() -> bytes:
+    """A fresh RCCL communicator id (rank 0 makes it; the launcher broadcasts it to the other ranks)."""
+    buf = (C.c_uint8 * 128)()
+    rc = load_library().swimsim_comm_unique_id(C.cast(buf, C.c_void_p), 128)
+    if rc < 0:
+        raise SwimsimError(f"swimsim_comm_unique_id failed: {ERRORS.get(rc, rc)}")
+    return bytes(buf)
+
+
 class Cluster:
-    """N swim nodes simulated on one MI355X (or one shard of observer rows)."""
+    """N swim nodes simulated on one MI355X, or one shard of a sharded cluster's observer rows."""
+
+    @classmethod
+    def _adopt(cls, h, n, lo, nl, t0_ms=T0_MS, period_ms=200):
+        self = cls.__new__(cls)
+        self.h, self.n, self.lo, self.nl = h, n, lo, nl
+        self.t0_ms, self.period_ms = t0_ms, period_ms
+        self._addr_buf = None
+        return self
 
     def __init__(self, n, *, t0_ms=T0_MS, period_ms=200, suspect_ms=5000, faulty_ms=24 * 3600 * 1000,
                  tombstone_ms=60_000, ping_request_size=3, max_rfs_jobs=5, p_factor=15, seed=1, addresses=None,
-                 device=0, init="converged", max_rounds=0, message_pool_bytes=0, observer_range=None):
+                 device=0, init="converged", max_rounds=0, message_pool_bytes=0, observer_range=None, comm=None):
+        """comm = (nranks, rank, unique_id): attach this handle as shard `rank` of a cluster spread over
+        nranks processes (RCCL); observer_range then defaults to the canonical shard."""
         L = load_library()
         self.n = n
         self.t0_ms, self.period_ms = t0_ms, period_ms
+        if comm is not None and observer_range is None:
+            observer_range = shard_range(n, comm[0], comm[1])
         cfg = Config()
         cfg.num_members, cfg.device, cfg.t0_ms, cfg.protocol_period_ms = n, device, t0_ms, period_ms
         cfg.suspect_timeout_ms, cfg.faulty_timeout_ms, cfg.tombstone_timeout_ms = suspect_ms, faulty_ms, tombstone_ms
@@ -144,6 +189,10 @@ class Cluster:
         self.h = h
         self.lo = observer_range[0] if observer_range else 0
         self.nl = (observer_range[1] - observer_range[0]) if observer_range else n
+        if comm is not None:
+            nranks, rank, uid = comm
+            idb = (C.c_uint8 * len(uid)).from_buffer_copy(uid)
+            self._chk(L.swimsim_comm_attach(self.h, nranks, rank, C.cast(idb, C.c_void_p), len(uid)))
         if init == "converged":
             self._chk(L.swimsim_init_converged(self.h))
         elif init == "self":
@@ -294,6 +343,14 @@ class Cluster:
         return {names[i].decode(): {"avg_ms": float(avg[i]), "launches": int(n_l[i]), "alg_bytes": float(byt[i])}
                 for i in range(n.value)}
 
+    def shard_info(self):
+        g, r, lo, hi = C.c_uint32(), C.c_uint32(), C.c_uint32(), C.c_uint32()
+        xb, xc = C.c_uint64(), C.c_uint64()
+        self._chk(load_library().swimsim_shard_info(self.h, C.byref(g), C.byref(r), C.byref(lo), C.byref(hi),
+                                                    C.byref(xb), C.byref(xc)))
+        return {"shards": g.value, "rank": r.value, "lo": lo.value, "hi": hi.value, "exchanged_bytes": xb.value,
+                "exchanges": xc.value}
+
     def bench_checksum(self, nrows, mode=0, reps=3):
         ms = C.c_double()
         self._chk(load_library().swimsim_bench_checksum(self.h, nrows, mode, reps, C.byref(ms)))
@@ -304,6 +361,119 @@ class Cluster:
 
 
 @dataclass
+class ShardedCluster:
+    """One cluster whose observer rows are split over `nshards` shards of this process (threads, one
+    per shard, exchanging cross-shard messages by device copies; devices[i] places shard i on another
+    GPU). Results are bit-identical to an unsharded Cluster; read-back merges the shards."""
+
+    def __init__(self, n, nshards, *, devices=None, init="converged", **kw):
+        L = load_library()
+        self.n, self.nshards = n, nshards
+        cfg = make_config(n, **{k: v for k, v in kw.items() if k != "addresses"})
+        arr = (C.c_void_p * nshards)()
+        devs = (C.c_int32 * nshards)(*devices) if devices else None
+        rc = L.swimsim_group_create(C.byref(cfg), nshards, C.cast(devs, C.c_void_p) if devs else None, arr)
+        if rc != 0:
+            raise SwimsimError(f"swimsim_group_create failed: {ERRORS.get(rc, rc)}")
+        self._arr = arr
+        self.live = np.ones(n, bool)
+        self.shards = []
+        for i in range(nshards):
+            lo, hi = shard_range(n, nshards, i)
+            self.shards.append(Cluster._adopt(C.c_void_p(arr[i]), n, lo, hi - lo, kw.get("t0_ms", T0_MS),
+                                              kw.get("period_ms", 200)))
+        for c in self.shards:
+            if init == "converged":
+                c._chk(L.swimsim_init_converged(c.h))
+            elif init == "self":
+                c._chk(L.swimsim_init_self_only(c.h))
+
+    def owner(self, o):
+        return next(c for c in self.shards if c.lo <= o < c.lo + c.nl)
+
+    def close(self):
+        for c in self.shards:
+            c.close()
+
+    def step(self, rounds=1, events=()):
+        r0 = self.round
+        for (r, k, a, b) in events:                      # liveness mirror for converged()
+            if r0 <= r < r0 + rounds and k in (EV_KILL, EV_REVIVE):
+                self.live[a] = k == EV_REVIVE
+        ev = _events(events)
+        rc = load_library().swimsim_group_step(self._arr, self.nshards, rounds, ev, len(events))
+        if rc < 0:
+            msgs = "; ".join(load_library().swimsim_last_error(c.h).decode() for c in self.shards)
+            raise SwimsimError(f"{ERRORS.get(rc, rc)}: {msgs}")
+
+    @property
+    def round(self):
+        return self.shards[0].round
+
+    def checksums(self):
+        return np.concatenate([c.checksums() for c in self.shards])
+
+    def last_targets(self):
+        return np.concatenate([c.last_targets() for c in self.shards])
+
+    def digest(self):
+        ds = [c.digest() for c in self.shards]
+        return tuple(sum(d[i] for d in ds) % (1 << 64) for i in range(3))
+
+    def counters(self):
+        cs = [c.counters() for c in self.shards]
+        out = {k: sum(c[k] for c in cs) for k in COUNTER_NAMES}
+        out["rounds"] = cs[0]["rounds"]
+        return out
+
+    def rows(self):
+        parts = [c.rows() for c in self.shards]
+        return np.concatenate([p[0] for p in parts]), np.concatenate([p[1] for p in parts])
+
+    def row(self, o):
+        return self.owner(o).row(o)
+
+    def changes(self, o):
+        return self.owner(o).changes(o)
+
+    def timers(self, o):
+        return self.owner(o).timers(o)
+
+    def node_stats(self, o):
+        return self.owner(o).node_stats(o)
+
+    def iter_state(self, o):
+        return self.owner(o).iter_state(o)
+
+    def converged(self):
+        """test_utils.go:188-198 over all shards: no live node has changes, all live checksums equal"""
+        cs = self.checksums()
+        live = [o for o in range(self.n) if self.live[o]]
+        return all(c.converged() for c in self.shards) and len(set(int(cs[o]) for o in live)) <= 1
+
+    def shard_info(self):
+        return [c.shard_info() for c in self.shards]
+
+    # setup calls act on the owning shard (row writes) or on every shard (topology)
+    def set_member(self, o, m, status, inc):
+        self.owner(o).set_member(o, m, status, inc)
+
+    def make_change(self, o, m, inc, status):
+        return self.owner(o).make_change(o, m, inc, status)
+
+    def clear_changes(self, o):
+        self.owner(o).clear_changes(o)
+
+    def set_live(self, m, live):
+        self.live[m] = bool(live)
+        for c in self.shards:
+            c.set_live(m, live)
+
+    def set_partition(self, m, label):
+        for c in self.shards:
+            c.set_partition(m, label)
+
+
 class MemberView:
     address: str
     status: str

@@ -40,7 +40,29 @@ def test_python_binding_covers_header(lib):
 
 def test_abi_version(lib):
     lib.swimsim_abi_version.restype = ctypes.c_int
-    assert lib.swimsim_abi_version() == 1
+    want = int(re.search(r"#define SWIMSIM_ABI_VERSION (\d+)", open(HEADER).read()).group(1))
+    assert lib.swimsim_abi_version() == want
+
+
+def test_shard_entry_points_reject_bad_arguments_without_touching_device(lib):
+    import swimsim
+    L = swimsim.load_library(LIB)
+    cfg = swimsim.make_config(8)
+    out = (ctypes.c_void_p * 4)()
+    assert L.swimsim_group_create(ctypes.byref(cfg), 0, None, out) == -1        # no shards
+    assert L.swimsim_group_create(ctypes.byref(cfg), 9, None, out) == -1        # more shards than rows
+    assert L.swimsim_group_step(None, 2, 1, None, 0) == -1
+    assert L.swimsim_comm_attach(None, 2, 0, None, 0) == -1
+    assert L.swimsim_shard_info(None, None, None, None, None, None, None) == -1
+
+
+@pytest.mark.parametrize("n,g", [(1, 1), (5, 4), (16, 3), (65536, 8), (65537, 7)])
+def test_canonical_shard_split_covers_all_rows(n, g):
+    import swimsim
+    ranges = [swimsim.shard_range(n, g, r) for r in range(g)]
+    assert ranges[0][0] == 0 and ranges[-1][1] == n
+    assert all(a[1] == b[0] for a, b in zip(ranges, ranges[1:]))
+    assert all(hi > lo for lo, hi in ranges)
 
 
 def test_create_rejects_bad_config_without_touching_device(lib):
