@@ -152,6 +152,8 @@ int swimsim_enable_timing(swimsim_t *h, int32_t enable);
 /* time the checksum kernel alone on the first nrows rows (mode 0 full, 1 hasher only, 2 formatting
  * only; the last two are diagnostics and leave garbage checksums) — average ms per launch */
 int swimsim_bench_checksum(swimsim_t *h, uint32_t nrows, int32_t mode, int32_t reps, double *ms);
+/* diagnostics: the 32-bit words of every 20-byte block the checksum kernel hashes for row o (W = 19) */
+int swimsim_debug_cs_stream(swimsim_t *h, uint32_t o, uint32_t *out, size_t cap_words);
 
 /* ---- shards: one cluster's observer rows split over G shards ----
  * The reference runs one swim.Node per process; here a shard owns observer rows

@@ -31,6 +31,8 @@ enum Counter {
     C_X_MERGED = C_NCOUNTERS, C_X_APPLIED, C_X_ISSUED, C_X_CS_ROWS, C_NALL
 };
 
+constexpr int CTR_SHARDS = 64, CTR_STRIDE = 32;   // d.ctr is [CTR_SHARDS][CTR_STRIDE] u64
+
 enum ErrBits : uint32_t {
     E_POOL = 1, E_DENSE = 2, E_ECAP = 4, E_SHORT = 8, E_ITER = 16, E_COUNT = 32, E_XCAP = 64
 };
@@ -62,9 +64,10 @@ struct DS {
     int32_t *part;
     const uint32_t *addrw;  // [N][6]
     const uint32_t *tailw;  // [ecap*4][8]: tail bytes status‖digits‖';' as words, word 6 = tail length
-    const uint32_t *rtail;  // [ecap*4][8]: record words W/4.. of addr‖tail with the address bytes zeroed
-                            // (tail pre-shifted by W%4 bytes); word 0's low byte = record length when
-                            // W%4 != 0; word 7 = the record's last 4 bytes
+    const uint32_t *rtail;  // [ecap*4][8]: record bytes [4*(W/4), 4*(W/4) + 28) of addr‖tail with the
+                            // address bytes zeroed (tail pre-shifted by W%4 bytes); byte 27 (word 6's
+                            // high byte, never a record byte) = record length; word 7 = the record's
+                            // last 4 bytes
     unsigned long long *ctr;
     uint32_t *err;
     uint4 *pool;
@@ -80,6 +83,8 @@ struct DS {
     uint32_t *clen;         // [NL] checksum-string length of each row
     int32_t *clast;         // [NL] last included member (-2: rescan)
     uint32_t dig_d0;          // decimal digits of t0
+    uint32_t max_tail;        // longest record tail (status ‖ digits ‖ ';') in the incarnation table
+    uint32_t min_tail;        // shortest one
     uint32_t G, rank;         // observer-row shards of the cluster and this handle's shard
     const uint32_t *shard_lo; // [G+1] first observer of each shard (ascending, shard_lo[G] = N)
     uint32_t dig_thr[8];      // e at which t0 + e*period gains a digit (0xFFFFFFFF = never)

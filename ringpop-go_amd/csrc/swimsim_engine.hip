@@ -318,7 +318,7 @@ inline uint32_t blocks_for_threads(uint32_t n) { return n ? (n + 255) / 256 : 1;
 
 int build_tail_table(swimsim *h, uint32_t ecap) {
     std::vector<uint32_t> t((size_t)ecap * 4 * 8, 0u);
-    uint32_t max_tl = 0;
+    uint32_t max_tl = 0, min_tl = 0xFFFFFFFFu;
     for (uint32_t e = 0; e < ecap; e++) {
         char digits[32];
         snprintf(digits, sizeof digits, "%lld", (long long)(h->t0 + (int64_t)e * h->period));
@@ -334,6 +334,7 @@ int build_tail_table(swimsim *h, uint32_t ecap) {
                          ((uint32_t)bytes[4 * w + 3] << 24);
             dst[6] = (uint32_t)n;
             max_tl = std::max(max_tl, (uint32_t)n);
+            min_tl = std::min(min_tl, (uint32_t)n);
         }
     }
     // record-tail table of the checksum formatter: record bytes [4*(W/4), 4*(W/4) + 28) with the
@@ -352,8 +353,9 @@ int build_tail_table(swimsim *h, uint32_t ecap) {
         const uint8_t *tb = (const uint8_t *)&t[i * 8];       // tails are >= 7 bytes: the last 4 are tail bytes
         rt[i * 8 + 7] = (uint32_t)tb[n - 4] | ((uint32_t)tb[n - 3] << 8) | ((uint32_t)tb[n - 2] << 16) |
                         ((uint32_t)tb[n - 1] << 24);
-        // record length in the low byte of word 0 (the address bytes' slot; masked off by the kernel)
-        if (r) rt[i * 8] |= L;
+        // record length in byte 27 (word 6's high byte): r + tail <= 27 keeps it out of the record
+        if (r + n > 27) return h->fail(SWIMSIM_EINVAL, "record tail too long for the checksum tail table");
+        rt[i * 8 + 6] |= L << 24;
     }
     (void)q;
     uint32_t *dev = nullptr, *rdev = nullptr;
@@ -381,6 +383,8 @@ int build_tail_table(swimsim *h, uint32_t ecap) {
     h->ecap = ecap;
     h->d.ecap = ecap;
     h->max_tl = max_tl;
+    h->d.max_tail = max_tl;
+    h->d.min_tail = min_tl;
     h->fast_cs = (h->W == 19 && h->W + max_tl <= 40);
     return 0;
 }
@@ -397,6 +401,19 @@ int check_err(swimsim *h) {
     if (e & E_SHORT) return h->fail(SWIMSIM_EINVAL, "checksum string of <= 24 bytes is not supported");
     if (e & E_ITER) return h->fail(SWIMSIM_EINVAL, "iterator found no pingable member despite a positive count");
     return h->fail(SWIMSIM_EINVAL, "dissemination count mismatch (internal error %u)", e);
+}
+
+// device counters summed over their shards (k ctr_add)
+int read_counters(swimsim *h, uint64_t *out /* [CTR_STRIDE] */) {
+    std::vector<uint64_t> c((size_t)CTR_SHARDS * CTR_STRIDE);
+    HIPCHK(h, hipMemcpyAsync(c.data(), h->d.ctr, c.size() * 8, hipMemcpyDeviceToHost, h->s));
+    HIPCHK(h, hipStreamSynchronize(h->s));
+    for (int i = 0; i < CTR_STRIDE; i++) {
+        uint64_t t = 0;
+        for (int k = 0; k < CTR_SHARDS; k++) t += c[(size_t)k * CTR_STRIDE + i];
+        out[i] = t;
+    }
+    return 0;
 }
 
 // --- sorting the (receiver << 32 | sender value) inbox keys and run-length encoding by receiver ---
@@ -1033,7 +1050,7 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
         (rc = dalloc(h, &d.njobs, h->NL, "njobs")) || (rc = dalloc(h, &d.jobs, (size_t)h->NL * h->maxjobs, "jobs")) ||
         (rc = dalloc(h, &d.dblk, (size_t)h->NL * d.NBW, "dblk")) || (rc = dalloc(h, &d.tblk, (size_t)h->NL * d.NB, "tblk")) ||
         (rc = dalloc(h, &d.live, h->N, "live")) || (rc = dalloc(h, &d.part, h->N, "part")) ||
-        (rc = dalloc(h, &d.ctr, 32, "counters")) || (rc = dalloc(h, &d.err, 4, "err")) ||
+        (rc = dalloc(h, &d.ctr, (size_t)CTR_SHARDS * CTR_STRIDE, "counters")) || (rc = dalloc(h, &d.err, 4, "err")) ||
         (rc = dalloc(h, &d.clen, h->NL, "clen")) || (rc = dalloc(h, &d.clast, h->NL, "clast")))
         return bail(rc);
     // address words
@@ -1117,7 +1134,7 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
         d.G = 1; d.rank = 0; d.shard_lo = sl;
     }
     if (hipHostMalloc((void **)&h->hinfo, 64, 0) != hipSuccess) return bail(SWIMSIM_ENOMEM);
-    hipMemset(d.ctr, 0, 32 * 8);
+    hipMemset(d.ctr, 0, (size_t)CTR_SHARDS * CTR_STRIDE * 8);
     hipMemset(d.err, 0, 4);
     hipMemset(h->need, 0, h->N);
     hipMemset(h->fsflag, 0, KC);
@@ -1366,9 +1383,8 @@ int swimsim_last_targets(swimsim_t *h, int32_t *out) {
 
 int swimsim_counters(swimsim_t *h, uint64_t *out) {
     if (!h || !out) return SWIMSIM_EINVAL;
-    uint64_t c[32];
-    HIPCHK(h, hipMemcpyAsync(c, h->d.ctr, sizeof c, hipMemcpyDeviceToHost, h->s));
-    HIPCHK(h, hipStreamSynchronize(h->s));
+    uint64_t c[CTR_STRIDE];
+    if (int rc = read_counters(h, c)) return rc;
     for (int i = 0; i < SWIMSIM_NCOUNTERS; i++) out[i] = c[i] + h->host_ctr[i];
     return SWIMSIM_OK;
 }
@@ -1430,13 +1446,30 @@ int swimsim_bench_checksum(swimsim_t *h, uint32_t nrows, int32_t mode, int32_t r
     return check_err(h);
 }
 
+int swimsim_debug_cs_stream(swimsim_t *h, uint32_t ol, uint32_t *out, size_t cap_words) {
+    if (!h || !out || ol >= h->NL || cap_words == 0) return SWIMSIM_EINVAL;
+    uint32_t *dev = nullptr;
+    HIPCHK(h, hipMalloc(&dev, cap_words * 4));
+    HIPCHK(h, hipMemsetAsync(dev, 0xEE, cap_words * 4, h->s));
+    hipLaunchKernelGGL(k_list_one, dim3(1), dim3(64), 0, h->s, h->list, h->cnt, ol, h->d);
+    HIPCHK(h, hipMemsetAsync(h->cnt, 0, 4, h->s));
+    const uint32_t one = 1;
+    HIPCHK(h, hipMemcpyAsync(h->cnt, &one, 4, hipMemcpyHostToDevice, h->s));
+    launch_checksum_dump(h->d, h->list, h->cnt, dev, (uint32_t)cap_words, h->s);
+    HIPCHK(h, hipMemcpyAsync(out, dev, cap_words * 4, hipMemcpyDeviceToHost, h->s));
+    HIPCHK(h, hipStreamSynchronize(h->s));
+    hipFree(dev);
+    return check_err(h);
+}
+
 int swimsim_enable_timing(swimsim_t *h, int32_t enable) {
     if (!h) return SWIMSIM_EINVAL;
     drain_timing(h);
     h->timing = enable != 0;
     for (int f = 0; f < F_NFAM; f++) { h->fam_ms[f] = 0; h->fam_n[f] = 0; }
-    HIPCHK(h, hipMemcpyAsync(h->fam_bytes_base, h->d.ctr, sizeof(h->fam_bytes_base), hipMemcpyDeviceToHost, h->s));
-    HIPCHK(h, hipStreamSynchronize(h->s));
+    uint64_t c[CTR_STRIDE];
+    if (int rc = read_counters(h, c)) return rc;
+    for (int i = 0; i < C_NALL; i++) h->fam_bytes_base[i] = c[i];
     return SWIMSIM_OK;
 }
 
@@ -1444,9 +1477,8 @@ int swimsim_kernel_times(swimsim_t *h, const char **names, double *avg_ms, uint6
                          size_t cap, size_t *n) {
     if (!h) return SWIMSIM_EINVAL;
     drain_timing(h);
-    uint64_t c[32];
-    HIPCHK(h, hipMemcpyAsync(c, h->d.ctr, sizeof c, hipMemcpyDeviceToHost, h->s));
-    HIPCHK(h, hipStreamSynchronize(h->s));
+    uint64_t c[CTR_STRIDE];
+    if (int rc = read_counters(h, c)) return rc;
     const double merged = (double)(c[C_X_MERGED] - h->fam_bytes_base[C_X_MERGED]);
     const double applied = (double)(c[C_X_APPLIED] - h->fam_bytes_base[C_X_APPLIED]);
     const double issued = (double)(c[C_X_ISSUED] - h->fam_bytes_base[C_X_ISSUED]);

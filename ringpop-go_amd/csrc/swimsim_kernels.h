@@ -5,6 +5,8 @@
 namespace swimdev {
 void launch_checksum(const DS &d, const uint32_t *list, const uint32_t *count, uint32_t maxn, bool fast,
                      hipStream_t s);
+void launch_checksum_dump(const DS &d, const uint32_t *list, const uint32_t *count, uint32_t *dbg, uint32_t cap,
+                          hipStream_t s);
 void launch_checksum_mode(const DS &d, const uint32_t *list, const uint32_t *count, uint32_t maxn, int mode,
                           hipStream_t s);
 }

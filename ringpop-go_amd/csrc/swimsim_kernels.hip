@@ -28,6 +28,12 @@ __device__ __forceinline__ unsigned long long bcast64(unsigned long long v) {
     return ((unsigned long long)hi << 32) | lo;
 }
 
+// protocol counters: CTR_SHARDS copies on separate lines, picked by workgroup, summed at read-back
+// (one shared word saturates at ~88 atomics/us, MI355X_MICROARCH.md row "dequeue")
+__device__ __forceinline__ void ctr_add(const DS &d, int c, unsigned long long v) {
+    atomicAdd(&d.ctr[(size_t)(blockIdx.x & (CTR_SHARDS - 1)) * CTR_STRIDE + c], v);
+}
+
 __device__ __forceinline__ uint32_t timeout_rounds(const DS &d, uint32_t st) {
     return st == ST_SUSPECT ? d.to_susp : st == ST_FAULTY ? d.to_faulty : d.to_tomb;
 }
@@ -117,13 +123,13 @@ __device__ __forceinline__ void fold_row(const DS &d, uint32_t ol, int dping, in
     if (ddc) d.dcnt[ol] += ddc;
     if (napp) {
         d.maxp[ol] = (int32_t)d.pfactor * digits10(d.ping[ol]);    // AdjustMaxPropagations
-        atomicAdd(&d.ctr[C_APPLIED], (unsigned long long)napp);
+        ctr_add(d, C_APPLIED, (unsigned long long)napp);
     }
     if (napp || evict) d.dirty[ol] = 1;                            // ComputeChecksum pending
     if (dlen) d.clen[ol] += dlen;
     if (maxlast > d.clast[ol]) d.clast[ol] = maxlast;
     else if (inval) d.clast[ol] = -2;                              // rescanned by the checksum kernel
-    if (nref) atomicAdd(&d.ctr[C_REFUTES], (unsigned long long)nref);
+    if (nref) ctr_add(d, C_REFUTES, (unsigned long long)nref);
 }
 
 __device__ __forceinline__ int wmax(int v) {
@@ -138,8 +144,8 @@ __device__ __forceinline__ void wave_finalize(const DS &d, uint32_t ol, const MA
     const int inv = wmax(acc.inval);
     if (lane_id() == 0) {
         fold_row(d, ol, dping, ddc, napp, nref, ev, dl, ml, inv);
-        if (np) atomicAdd(&d.ctr[C_X_MERGED], (unsigned long long)np);
-        if (napp) atomicAdd(&d.ctr[C_X_APPLIED], (unsigned long long)napp);
+        if (np) ctr_add(d, C_X_MERGED, (unsigned long long)np);
+        if (napp) ctr_add(d, C_X_APPLIED, (unsigned long long)napp);
     }
     __threadfence_block();
 }
@@ -371,11 +377,13 @@ __global__ void k_clear_changes(DS d, uint32_t ol) {
 // ---------------------------------------------------------------------------------------------
 // phase E: host events, applied in order by one thread (few per round)
 // ---------------------------------------------------------------------------------------------
-__device__ void thread_make_change(const DS &d, uint32_t ol, uint32_t o, uint32_t m, uint32_t e, uint32_t st, uint32_t r) {
+// returns the number of applied changes (0/1)
+__device__ int thread_make_change(const DS &d, uint32_t ol, uint32_t o, uint32_t m, uint32_t e, uint32_t st, uint32_t r) {
     MAcc acc;
     const uint32_t self_e = d.mw[(size_t)ol * d.NP + o] >> 3;   // MakeChange: SourceIncarnation = local inc
     merge_change(d, ol, o, m, st, e, o, self_e, r, r, acc);
     fold_row(d, ol, acc.dping, acc.ddc, acc.napp, acc.nref, 0, acc.dlen, acc.maxlast, acc.inval);
+    return acc.napp;
 }
 
 __global__ void k_events(DS d, const uint4 *ev, uint32_t nev, uint32_t r, uint32_t *applied_out) {
@@ -385,25 +393,25 @@ __global__ void k_events(DS d, const uint4 *ev, uint32_t nev, uint32_t r, uint32
         const uint32_t kind = e.x, o = e.y;
         if (o < d.lo || o >= d.lo + d.NL) continue;
         const uint32_t ol = o - d.lo;
-        const unsigned long long before = d.ctr[C_APPLIED];
+        int applied = 0;
         switch (kind) {
         case 1:  // MakeChange(o, member, e, status)
-            thread_make_change(d, ol, o, e.z, e.w & 0x1FFFFFFFu, e.w >> 29, r);
+            applied = thread_make_change(d, ol, o, e.z, e.w & 0x1FFFFFFFu, e.w >> 29, r);
             break;
         case 2:  // Reincarnate: MakeAlive(self, now) (memberlist.go:234-236)
-            thread_make_change(d, ol, o, o, r, ST_ALIVE, r);
+            applied = thread_make_change(d, ol, o, o, r, ST_ALIVE, r);
             break;
         case 3:  // admin leave: MakeLeave(self, local inc) (handlers.go:145-148)
-            thread_make_change(d, ol, o, o, d.mw[(size_t)ol * d.NP + o] >> 3, ST_LEAVE, r);
+            applied = thread_make_change(d, ol, o, o, d.mw[(size_t)ol * d.NP + o] >> 3, ST_LEAVE, r);
             break;
         case 4:  // reap: faulty → tombstone (handlers.go:154-163)
             for (uint32_t m = 0; m < d.N; m++) {
                 const uint32_t w = d.mw[(size_t)ol * d.NP + m];
-                if ((w & 7u) == ST_FAULTY) thread_make_change(d, ol, o, m, w >> 3, ST_TOMB, r);
+                if ((w & 7u) == ST_FAULTY) applied += thread_make_change(d, ol, o, m, w >> 3, ST_TOMB, r);
             }
             break;
         }
-        if (applied_out) applied_out[i] = (uint32_t)(d.ctr[C_APPLIED] - before);
+        if (applied_out) applied_out[i] = (uint32_t)applied;
     }
 }
 
@@ -461,7 +469,7 @@ __global__ void k_timers(DS d, uint32_t r) {
     newmin = wmin(newmin);
     if (lane_id() == 0) d.tmin[ol] = newmin;
     fired = wsum(fired);
-    if (lane_id() == 0 && fired) atomicAdd(&d.ctr[C_TIMERS_FIRED], (unsigned long long)fired);
+    if (lane_id() == 0 && fired) ctr_add(d, C_TIMERS_FIRED, (unsigned long long)fired);
     __threadfence_block();
     wave_finalize(d, ol, acc);
 }
@@ -563,10 +571,10 @@ __global__ void k_issue(DS d, int mode, const int32_t *tgt, const uint8_t *faile
         sI[o] = d.mw[(size_t)ol * d.NP + o] >> 3;                    // global sender id (remote senders'
         sC[o] = d.cs[ol];                                            // messages are imported there)
         if (mode == 0) {
-            atomicAdd(&d.ctr[C_PINGS], 1ull);
-            atomicAdd(&d.ctr[C_MSG_CHANGES], (unsigned long long)md.len);   // counted per helper call in Q2
+            ctr_add(d, C_PINGS, 1ull);
+            ctr_add(d, C_MSG_CHANGES, (unsigned long long)md.len);   // counted per helper call in Q2
         }
-        atomicAdd(&d.ctr[C_X_ISSUED], (unsigned long long)md.len);
+        ctr_add(d, C_X_ISSUED, (unsigned long long)md.len);
     }
 }
 
@@ -611,7 +619,7 @@ __global__ void k_helpers(DS d, const int32_t *tgt, const uint8_t *failed, uint3
     if (!failed[ol]) return;
     const uint32_t o = d.lo + ol, t = (uint32_t)tgt[ol], K = d.K;
     const uint32_t *row = d.mw + (size_t)ol * d.NP;
-    atomicAdd(&d.ctr[C_PINGREQS], 1ull);
+    ctr_add(d, C_PINGREQS, 1ull);
     const int32_t eligible = d.ping[ol] - (is_pingable(row[t] & 7u) ? 1 : 0);
     const uint32_t need = (uint32_t)max(0, min((int32_t)K, eligible));
     uint32_t got = 0, h[8];
@@ -716,16 +724,16 @@ __device__ void recv_one(const DS &d, const RecvArgs &a, uint32_t j, uint32_t se
             wave_snapshot(d, ol, j, resp);
             if (lane_id() == 0) {
                 if (a.phase == 0) a.fsflag[pair] = 1;
-                atomicAdd(&d.ctr[a.phase == 0 ? C_FULL_SYNCS : C_FULL_SYNCS_PINGREQ], 1ull);
+                ctr_add(d, a.phase == 0 ? C_FULL_SYNCS : C_FULL_SYNCS_PINGREQ, 1ull);
             }
         }
     }
     if (lane_id() == 0) {
         a.rdesc[resp_idx] = resp;
-        if (resp.kind != 2) atomicAdd(&d.ctr[C_MSG_CHANGES], (unsigned long long)resp.len);
+        if (resp.kind != 2) ctr_add(d, C_MSG_CHANGES, (unsigned long long)resp.len);
         if (a.phase == 1) {
-            atomicAdd(&d.ctr[C_HELPER_CALLS], 1ull);
-            atomicAdd(&d.ctr[C_MSG_CHANGES], (unsigned long long)a.sdesc[sender_row].len);
+            ctr_add(d, C_HELPER_CALLS, 1ull);
+            ctr_add(d, C_MSG_CHANGES, (unsigned long long)a.sdesc[sender_row].len);
         }
     }
 }
@@ -753,17 +761,17 @@ __global__ void k_recv_finish(DS d, const uint4 *defer, const uint32_t *defer_cn
     resp.kind = 0; resp.len = 0; resp.off_lo = resp.off_hi = 0;
     if (d.dense_cs[slot] != e.z) {
         resp.kind = 1; resp.off_lo = slot; resp.len = d.dense_meta[slot].z;
-        atomicAdd(&d.ctr[phase == 1 ? C_FULL_SYNCS_PINGREQ : C_FULL_SYNCS], 1ull);
+        ctr_add(d, phase == 1 ? C_FULL_SYNCS_PINGREQ : C_FULL_SYNCS, 1ull);
         if (phase == 2) {
             const uint32_t ol = d.dense_meta[slot].x - d.lo;
             if (d.njobs[ol] < d.maxjobs) d.jobs[(size_t)ol * d.maxjobs + d.njobs[ol]++] = e.w;
-            else atomicAdd(&d.ctr[C_RFS_OMITTED], 1ull);
+            else ctr_add(d, C_RFS_OMITTED, 1ull);
         } else if (phase == 0) {
             fsflag[e.w] = 1;
         }
     }
     rdesc[e.x] = resp;
-    if (phase != 2) atomicAdd(&d.ctr[C_MSG_CHANGES], (unsigned long long)resp.len);
+    if (phase != 2) ctr_add(d, C_MSG_CHANGES, (unsigned long long)resp.len);
 }
 
 // defer list → checksum list of dense-snapshot ids (NL + slot)
@@ -785,7 +793,7 @@ __global__ void k_build_jobs(DS d, const uint32_t *ukeys, const uint32_t *counts
         if (!fsflag[p]) continue;
         fsflag[p] = 0;
         if (d.njobs[ol] < d.maxjobs) d.jobs[(size_t)ol * d.maxjobs + d.njobs[ol]++] = vals[p];
-        else atomicAdd(&d.ctr[C_RFS_OMITTED], 1ull);
+        else ctr_add(d, C_RFS_OMITTED, 1ull);
     }
 }
 
@@ -798,7 +806,7 @@ __global__ void k_resp(DS d, const int32_t *tgt, const uint8_t *failed, const Ms
     const uint32_t o = d.lo + ol;
     wave_bump(d, ol, sdesc[o]);
     wave_merge_msg(d, ol, o, rdesc[o], r, r);
-    if (lane_id() == 0) atomicAdd(&d.ctr[C_PINGS_OK], 1ull);
+    if (lane_id() == 0) ctr_add(d, C_PINGS_OK, 1ull);
 }
 
 // Q3: resolve indirect pings (ping_request_sender.go:65-138, node.go:494-509)
@@ -818,11 +826,11 @@ __global__ void k_resolve(DS d, const int32_t *tgt, const uint8_t *failed, const
         }
     }
     if (lane_id() == 0) {
-        if (errs) atomicAdd(&d.ctr[C_HELPER_ERRORS], (unsigned long long)errs);
+        if (errs) ctr_add(d, C_HELPER_ERRORS, (unsigned long long)errs);
         if (errs == K) {
-            atomicAdd(&d.ctr[C_INCONCLUSIVE], 1ull);
+            ctr_add(d, C_INCONCLUSIVE, 1ull);
         } else {
-            atomicAdd(&d.ctr[C_SUSPECT_DECL], 1ull);
+            ctr_add(d, C_SUSPECT_DECL, 1ull);
             const uint32_t t = (uint32_t)tgt[ol];
             const uint32_t te = d.mw[(size_t)ol * d.NP + t] >> 3;      // member.Incarnation read now (node.go:508)
             thread_make_change(d, ol, o, t, te, ST_SUSPECT, r);
@@ -852,7 +860,7 @@ __global__ void k_jobs_merge(DS d, uint32_t q, const MsgDesc *snapdesc, uint32_t
     if (ol >= d.NL || d.njobs[ol] <= q) return;
     const uint32_t src = d.jobs[(size_t)ol * d.maxjobs + q];
     wave_merge_msg(d, ol, d.lo + ol, snapdesc[src], r, r);
-    if (lane_id() == 0) atomicAdd(&d.ctr[C_RFS_DONE], 1ull);
+    if (lane_id() == 0) ctr_add(d, C_RFS_DONE, 1ull);
 }
 
 __global__ void k_jobs_reset(DS d, uint8_t *need) {
@@ -861,343 +869,7 @@ __global__ void k_jobs_reset(DS d, uint8_t *need) {
     if (i < d.N) need[i] = 0;
 }
 
-// ---------------------------------------------------------------------------------------------
-// phase C: checksum (memberlist.go:83-128): FarmHash-32 mk (go-farm Fingerprint32) over the byte
-// stream addr ‖ status ‖ decimal(inc) ‖ ';' of every non-tombstone member in index order (fixed-width
-// ascending addresses make the sorted order the index order).
-//
-// The chain is sequential within a row, so its latency sets the time of a launch. One
-// workgroup takes 64 rows. Wave 0 is the hasher: one lane per row, and it does only the FarmHash
-// block function on 20-byte blocks read from LDS. Waves 1-4 are formatters: they build the byte
-// stream of the same 64 rows into a per-row LDS ring, CS_CHUNK members ahead of the hasher, with one
-// workgroup barrier per chunk. The string length and the last record (the hash prologue) come
-// from per-row values maintained by the merges.
-// ---------------------------------------------------------------------------------------------
-constexpr int CS_ROWS = 64;                     // rows per workgroup: one lane per row in each of the 3 waves
-constexpr int CS_IT = 4;                        // members formatted per pipeline step
-constexpr int CS_SUP = 16;                      // members per register prefetch (4 steps)
-constexpr int CS_RING = 110;                    // ring words per row (22 blocks); holds 2 steps + a block + slack
-constexpr int CS_PRE = 13, CS_POST = 13;        // write spill areas in front of / behind the ring
-constexpr int CS_PHYS = CS_PRE + CS_RING + CS_POST;
-constexpr int CS_RW = 11;                       // record words of the prologue record (<= 44 bytes)
-
-template <int W, int RW>
-__device__ __forceinline__ void build_rec(uint32_t (&R)[RW], const uint32_t *A, const uint32_t (&T)[6]) {
-    constexpr int wW = W / 4, bW = W % 4;
-#pragma unroll
-    for (int i = 0; i < RW; i++) {
-        uint32_t v;
-        if (i < wW) {
-            v = A[i];
-        } else if (bW == 0) {
-            const int k = i - wW;
-            v = k < 6 ? T[k] : 0u;
-        } else if (i == wW) {
-            v = (A[wW] & ((1u << (8 * bW)) - 1u)) | (T[0] << (8 * bW));
-        } else {
-            const int k = i - wW - 1;
-            const uint32_t lo = k < 6 ? (T[k] >> (32 - 8 * bW)) : 0u;
-            const uint32_t hi = (k + 1) < 6 ? (T[k + 1] << (8 * bW)) : 0u;
-            v = lo | hi;
-        }
-        R[i] = v;
-    }
-}
-
-__device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t sh_bits) {
-    return (uint32_t)((((uint64_t)hi << 32) | lo) >> sh_bits);
-}
-
-// record words of member m (member word w); returns the record length (0 = not in the string)
-template <int W>
-__device__ __forceinline__ uint32_t record(const DS &d, uint32_t m, uint32_t w, uint32_t (&R)[CS_RW]) {
-    const uint32_t st = w & 7u, e = min(w >> 3, d.ecap - 1);
-    const uint32_t *tp = d.tailw + ((size_t)e * 4 + (st & 3u)) * 8;
-    const uint4 ta = *(const uint4 *)tp;
-    const uint4 tb = *(const uint4 *)(tp + 4);
-    const uint32_t T[6] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y};
-    build_rec<W, CS_RW>(R, d.addrw + (size_t)m * 6, T);
-    return (st < 4u && m < d.N) ? W + tb.z : 0u;
-}
-
-// M(x) = mur's data-only half: ror(x * c1, 17) * c2. mur(x, h) = ror(h ^ M(x), 19) * 5 + 0xe6546b64.
-__device__ __forceinline__ uint32_t fh_m(uint32_t x) { return ror32(x * FH_C1, 17) * FH_C2; }
-__device__ __forceinline__ uint32_t x5(uint32_t h) {          // h * 5 as one full-rate v_lshl_add_u32
-    uint32_t r;                                              // (LLVM would re-fold a C shift-add into a
-    asm("v_lshl_add_u32 %0, %1, 2, %1" : "=v"(r) : "v"(h)); //  quarter-rate multiply)
-    return r;
-}
-// mur(x, h) + add with M(x) precomputed: ror(h ^ M(x), 19) * 5 + 0xe6546b64 + add
-__device__ __forceinline__ uint32_t fh_fold(uint32_t h, uint32_t mx, uint32_t add) {
-    return x5(ror32(h ^ mx, 19)) + 0xe6546b64u + add;
-}
-
-// The byte stream addr(m) ‖ status ‖ decimal(inc) ‖ ';' of one row goes through a per-row ring in LDS
-// (word-major: word q of row l at ring[q*64 + l], so every per-lane access is bank-conflict free):
-//   wave 2 (formatter): CS_IT members per step; each record is assembled from the row's member word
-//                       (register-prefetched), the member's address words (uniform loads one step
-//                       ahead) and a pre-shifted record tail (per-lane LDS cache keyed by incarnation,
-//                       read for the next step before the step barrier), and written as whole words
-//                       with v_perm byte alignment against the carried partial word;
-//   wave 0 (h chain)  : FarmHash-mk h-lane of each 20-byte block of the previous steps;
-//   wave 1 (g/f chain): the coupled g and f lanes of the same blocks.
-// One barrier per step; the hashers trail the formatter by one step.
-// MODE 0: normal; 1: hashers only (formatter skips its stores); 2: formatter only.
-template <int W, int MODE>
-__global__ void __launch_bounds__(192) k_checksum(DS d, const uint32_t *list, const uint32_t *count) {
-    __shared__ uint32_t ring[CS_PHYS * CS_ROWS];
-    __shared__ uint4 tcache[4 * 2 * CS_ROWS];     // [status][half][row]: record-tail words for the cached e
-    __shared__ uint32_t wp[2][CS_ROWS];
-    __shared__ uint32_t xgf[2][CS_ROWS];
-    constexpr int Q = W / 4;                      // record words that are pure address words
-    constexpr int NR = Q + 7;                     // record words
-    constexpr int NO = NR + 1;                    // ring words one record can touch
-    static_assert(NO <= CS_PRE && NO <= CS_POST, "spill areas too small");
-    const uint32_t cnt = *count;
-    if (blockIdx.x * CS_ROWS >= cnt) return;                       // uniform per workgroup
-    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-    const uint32_t gi = blockIdx.x * CS_ROWS + lane;
-    const bool valid = gi < cnt;
-    const uint32_t id = list[valid ? gi : blockIdx.x * CS_ROWS];
-    const bool is_row = id < d.NL;
-    const uint32_t *row = is_row ? d.mw + (size_t)id * d.NP : d.dense + (size_t)(id - d.NL) * d.NP;
-    const uint32_t nsup = (d.N + CS_SUP - 1) / CS_SUP;
-    const uint32_t nit = nsup * (CS_SUP / CS_IT);
-
-    if (wave == 2) {
-        // ------------------------------- formatter -------------------------------
-        // The carried partial word after a record is its last 4 bytes (tail table word 7).
-        uint4 *tc = tcache;
-        uint32_t pos = 0, phys = 0, hc = 0, ce = 0xFFFFFFFFu;
-        uint4 pre[4], cur[4];
-        uint4 c0[CS_IT], c1[CS_IT];
-        uint32_t Lk[CS_IT];                                        // record lengths (0 = not in the string)
-        uint32_t An[CS_IT][Q + 1];
-        auto load_addr = [&](uint32_t m0) {                        // uniform addresses: one line per load
-#pragma unroll
-            for (int k = 0; k < CS_IT; k++) {
-                const uint32_t *ap = d.addrw + (size_t)min(m0 + k, d.N - 1) * 6;
-#pragma unroll
-                for (int i = 0; i <= Q; i++) An[k][i] = ap[i];
-            }
-        };
-        // tails of the members of one step (cache refills are rare: mostly one incarnation per row)
-        auto prep = [&](const uint4 &q4, uint32_t mb) {
-            const uint32_t ws[4] = {q4.x, q4.y, q4.z, q4.w};
-#pragma unroll
-            for (int k = 0; k < CS_IT; k++) {
-                const uint32_t st = ws[k] & 7u, e = min(ws[k] >> 3, d.ecap - 1);
-                const bool ok = st < 4u && mb + k < d.N;
-                if (ok && e != ce) {
-                    const uint4 *tp = (const uint4 *)(d.rtail + (size_t)e * 32);
-#pragma unroll
-                    for (int q = 0; q < 8; q++) tc[q * CS_ROWS + lane] = tp[q];
-                    ce = e;
-                }
-                c0[k] = tc[((st & 3u) * 2) * CS_ROWS + lane];
-                c1[k] = tc[((st & 3u) * 2 + 1) * CS_ROWS + lane];
-                // W % 4 != 0: the length rides in the low byte of word 0 (an address byte slot)
-                Lk[k] = ok ? (W % 4 ? (c0[k].x & 0xFFu) : (uint32_t)reclen(d, st, e)) : 0u;
-            }
-        };
-#pragma unroll
-        for (int k = 0; k < 4; k++) pre[k] = *(const uint4 *)(row + 4 * k);
-        load_addr(0);
-        prep(pre[0], 0);
-        for (uint32_t sc = 0; sc < nsup; sc++) {
-#pragma unroll
-            for (int k = 0; k < 4; k++) cur[k] = pre[k];
-            if (sc + 1 < nsup) {
-#pragma unroll
-                for (int k = 0; k < 4; k++) pre[k] = *(const uint4 *)(row + (sc + 1) * CS_SUP + 4 * k);
-            }
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const uint32_t mb = sc * CS_SUP + u * CS_IT;
-                uint32_t A[CS_IT][Q + 1];
-#pragma unroll
-                for (int k = 0; k < CS_IT; k++)
-#pragma unroll
-                    for (int i = 0; i <= Q; i++) A[k][i] = An[k][i];
-                load_addr(mb + CS_IT);                             // one step ahead
-#pragma unroll
-                for (int k = 0; k < CS_IT; k++) {
-                    const uint32_t C[8] = {c0[k].x, c0[k].y, c0[k].z, c0[k].w, c1[k].x, c1[k].y, c1[k].z, c1[k].w};
-                    const uint32_t L = Lk[k];
-                    const uint32_t c0w = W % 4 ? (C[0] & 0xFFFFFF00u) : C[0];
-                    uint32_t R[NR + 1];
-#pragma unroll
-                    for (int i = 0; i < NR; i++) R[i] = i < Q ? A[k][i] : (i == Q ? (A[k][Q] | c0w) : C[i - Q]);
-                    R[NR] = 0u;
-                    const uint32_t s = pos & 3u;
-                    const uint32_t s2b = s | (s << 8);
-                    const uint32_t sel = 0x07060504u - (s2b | (s2b << 16));
-                    if (L) {
-                        if (MODE != 1) {
-                            // words past the record end are garbage that the next record overwrites (program order)
-                            const uint32_t i0 = (CS_PRE + phys) * CS_ROWS + lane;
-#pragma unroll
-                            for (int j = 0; j < NO; j++) ring[i0 + j * CS_ROWS] = __builtin_amdgcn_perm(R[j], j ? R[j - 1] : hc, sel);
-                            if (phys + NO > CS_RING) {                 // words past the ring end: also at the front
-                                const uint32_t i1 = (CS_PRE + phys - CS_RING) * CS_ROWS + lane;
-#pragma unroll
-                                for (int j = 0; j < NO; j++)
-                                    ring[i1 + j * CS_ROWS] = __builtin_amdgcn_perm(R[j], j ? R[j - 1] : hc, sel);
-                            }
-                        }
-                        hc = C[7];
-                        phys += (s + L) >> 2;
-                        phys = phys >= CS_RING ? phys - CS_RING : phys;
-                        pos += L;
-                    }
-                }
-                wp[(sc * 4 + u) & 1][lane] = pos;
-                prep(u < 3 ? cur[u + 1] : pre[0], mb + CS_IT);     // next step's tails, before the barrier
-                __syncthreads();
-            }
-        }
-        __syncthreads();
-        return;
-    }
-
-    // ------------------------------- hashers -------------------------------
-    const uint32_t len = is_row ? d.clen[id] : d.dense_len[id - d.NL];
-    int32_t last = is_row ? d.clast[id] : d.dense_last[id - d.NL];
-    if (last < 0) {                                                // invalidated: rescan from the end
-        last = -1;
-        for (int32_t m = (int32_t)d.N - 1; m >= 0; m--)
-            if ((row[m] & 7u) < 4u) { last = m; break; }
-    }
-    const bool ok = len > 24 && last >= 0;
-    if (!ok && valid && wave == 0) atomicOr(d.err, E_SHORT);
-    FH fh{0, 0, 0};
-    {
-        uint32_t R[CS_RW];
-        const uint32_t L = record<W>(d, (uint32_t)max(last, 0), row[max(last, 0)], R);
-        const uint32_t q = L >= 20 ? L - 20 : 0, qw = q >> 2, qb = (q & 3u) * 8u;
-        uint32_t t[5];
-#pragma unroll
-        for (int k = 0; k < 5; k++) {
-            uint32_t lo = 0, hi = 0;
-#pragma unroll
-            for (int s = 0; s < CS_RW; s++) {
-                lo = ((uint32_t)s == qw + k) ? R[s] : lo;
-                hi = ((uint32_t)s == qw + k + 1) ? R[s] : hi;
-            }
-            t[k] = funnel(hi, lo, qb);
-        }
-        fh.init(len, t[0], t[1], t[2], t[3], t[4]);
-    }
-    uint32_t h = fh.h, g = fh.g, f = fh.f;
-    const uint32_t iters = ok ? (len - 1) / 20 : 0;
-    const uint32_t *rb = ring + CS_PRE * CS_ROWS + lane;
-    uint32_t done = 0, rq = 0;
-    // hash blocks [done, lim) in groups of 4: all loads of a group first, then the arithmetic with
-    // branch-free predication (lanes have different limits); the role test is wave-uniform
-    const uint32_t role = __builtin_amdgcn_readfirstlane(wave);
-    auto advance = [&](uint32_t lim) {
-        const uint32_t n = done < lim ? min(lim - done, 4u) : 0u;
-        done += n;
-        rq += 5u * n;
-        rq = rq >= CS_RING ? rq - CS_RING : rq;
-    };
-    auto run_h = [&](uint32_t lim) {
-        while (__any(done < lim)) {
-            uint32_t a[4], dd[4], e[4];
-            uint32_t q = rq;
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const uint32_t *p = rb + q * CS_ROWS;
-                a[k] = p[0]; dd[k] = p[3 * CS_ROWS]; e[k] = p[4 * CS_ROWS];
-                q += 5;
-                q = q >= CS_RING ? q - CS_RING : q;
-            }
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const uint32_t hn = fh_fold(h + a[k], fh_m(dd[k]), e[k]);
-                h = done + k < lim ? hn : h;
-            }
-            advance(lim);
-        }
-    };
-    auto run_gf = [&](uint32_t lim) {
-        while (__any(done < lim)) {
-            uint32_t v[4][5];
-            uint32_t q = rq;
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const uint32_t *p = rb + q * CS_ROWS;
-#pragma unroll
-                for (int i = 0; i < 5; i++) v[k][i] = p[i * CS_ROWS];
-                q += 5;
-                q = q >= CS_RING ? q - CS_RING : q;
-            }
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const uint32_t a = v[k][0], b = v[k][1], c = v[k][2], dd = v[k][3], e = v[k][4];
-                uint32_t gn = fh_fold(g + b, fh_m(c), a);
-                uint32_t fn = fh_fold(f + c, fh_m(b + e * FH_C1), dd);
-                fn += gn; gn += fn;
-                const bool act = done + k < lim;
-                g = act ? gn : g;
-                f = act ? fn : f;
-            }
-            advance(lim);
-        }
-    };
-    uint32_t avail = 0;
-    if (role == 0) {
-        for (uint32_t t = 0; t < nit; t++) {
-            if (MODE != 2) run_h(MODE == 1 ? min(iters, t * 8u) : min(iters, avail));
-            __syncthreads();
-            avail = wp[t & 1][lane] / 20;
-        }
-        if (MODE != 2) run_h(iters);
-    } else {
-        for (uint32_t t = 0; t < nit; t++) {
-            if (MODE != 2) run_gf(MODE == 1 ? min(iters, t * 8u) : min(iters, avail));
-            __syncthreads();
-            avail = wp[t & 1][lane] / 20;
-        }
-        if (MODE != 2) run_gf(iters);
-    }
-    if (wave == 1) { xgf[0][lane] = g; xgf[1][lane] = f; }
-    __syncthreads();
-    if (wave == 0 && valid) {
-        fh.h = h; fh.g = xgf[0][lane]; fh.f = xgf[1][lane];
-        const uint32_t hv = ok ? fh.fin() : 0u;
-        if (is_row) {
-            d.cs[id] = hv;
-            d.dirty[id] = 0;
-            atomicAdd(&d.ctr[C_X_CS_ROWS], 1ull);
-        } else {
-            d.dense_cs[id - d.NL] = hv;
-        }
-    }
-}
-
-#define CS_INST(Wv) template __global__ void k_checksum<Wv, 0>(DS, const uint32_t *, const uint32_t *);
-CS_INST(13) CS_INST(14) CS_INST(15) CS_INST(16) CS_INST(17) CS_INST(18) CS_INST(19) CS_INST(20)
-
-void launch_checksum(const DS &d, const uint32_t *list, const uint32_t *count, uint32_t maxn, bool fast, hipStream_t s) {
-    (void)fast;
-    const uint32_t grid = (maxn + CS_ROWS - 1) / CS_ROWS;
-    if (grid == 0) return;
-    switch (d.W) {
-#define CS_CASE(Wv) case Wv: hipLaunchKernelGGL((k_checksum<Wv, 0>), dim3(grid), dim3(192), 0, s, d, list, count); break;
-        CS_CASE(13) CS_CASE(14) CS_CASE(15) CS_CASE(16) CS_CASE(17) CS_CASE(18) CS_CASE(19) CS_CASE(20)
-    default: break;
-    }
-}
-
-// measurement variants (swimsim_bench_checksum): W = 19 only
-void launch_checksum_mode(const DS &d, const uint32_t *list, const uint32_t *count, uint32_t maxn, int mode, hipStream_t s) {
-    const uint32_t grid = (maxn + CS_ROWS - 1) / CS_ROWS;
-    if (grid == 0 || d.W != 19) return;
-    if (mode == 1) hipLaunchKernelGGL((k_checksum<19, 1>), dim3(grid), dim3(192), 0, s, d, list, count);
-    else if (mode == 2) hipLaunchKernelGGL((k_checksum<19, 2>), dim3(grid), dim3(192), 0, s, d, list, count);
-    else hipLaunchKernelGGL((k_checksum<19, 0>), dim3(grid), dim3(192), 0, s, d, list, count);
-}
+#include "swimsim_checksum.hip"
 
 // ---------------------------------------------------------------------------------------------
 // heal helpers (heal_partition.go:33-145)
@@ -1281,9 +953,9 @@ __global__ void k_ping_with(DS d, uint32_t tol, uint32_t sender, const MsgDesc *
         } else if (d.cs[tol] != scs) {
             wave_snapshot(d, tol, d.lo + tol, resp);
             if (lane_id() == 0) {
-                atomicAdd(&d.ctr[C_FULL_SYNCS], 1ull);
+                ctr_add(d, C_FULL_SYNCS, 1ull);
                 if (d.njobs[tol] < d.maxjobs) d.jobs[(size_t)tol * d.maxjobs + d.njobs[tol]++] = sender;
-                else atomicAdd(&d.ctr[C_RFS_OMITTED], 1ull);
+                else ctr_add(d, C_RFS_OMITTED, 1ull);
             }
         }
     }

@@ -98,6 +98,7 @@ def load_library(path: str = LIB_PATH):
         "swimsim_kernel_times": (C.c_int, [P, P, P, P, P, sz, C.POINTER(sz)]),
         "swimsim_enable_timing": (C.c_int, [P, i32]),
         "swimsim_bench_checksum": (C.c_int, [P, u32, i32, i32, C.POINTER(C.c_double)]),
+        "swimsim_debug_cs_stream": (C.c_int, [P, u32, P, sz]),
         "swimsim_group_create": (C.c_int, [C.POINTER(Config), u32, P, P]),
         "swimsim_group_step": (C.c_int, [P, u32, u32, C.POINTER(Event), sz]),
         "swimsim_comm_unique_id": (C.c_int, [P, sz]),
@@ -350,6 +351,12 @@ class Cluster:
                                                     C.byref(xb), C.byref(xc)))
         return {"shards": g.value, "rank": r.value, "lo": lo.value, "hi": hi.value, "exchanged_bytes": xb.value,
                 "exchanges": xc.value}
+
+    def debug_cs_stream(self, o, nwords):
+        """the words of every 20-byte block the checksum kernel hashes for observer o (diagnostics)"""
+        out = np.zeros(nwords, dtype=np.uint32)
+        self._chk(load_library().swimsim_debug_cs_stream(self.h, o - self.lo, out.ctypes.data, nwords))
+        return out
 
     def bench_checksum(self, nrows, mode=0, reps=3):
         ms = C.c_double()

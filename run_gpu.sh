@@ -25,6 +25,10 @@ for mode in "$@"; do
       -- python3 bench.py --no-cpu-baseline > gpurun_out/prof.log 2>&1
     rc=$?; echo "rocprof rc=$rc" >> gpurun_out/prof.log; [ $rc -eq 0 ] || exit $rc
     ;;
+  csbench)
+    timeout -k 10 300 python -u tools_cs_bench.py 65536 64,1024,16384,65536 2 > gpurun_out/csbench.json 2> gpurun_out/csbench.err
+    rc=$?; echo "csbench rc=$rc" >> gpurun_out/csbench.err; [ $rc -eq 0 ] || exit $rc
+    ;;
   pmc)
     timeout -k 10 -s KILL 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run \
       --output-format csv -- python3 bench.py --no-cpu-baseline > gpurun_out/pmc_fetch.log 2>&1
