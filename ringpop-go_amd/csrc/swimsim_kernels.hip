@@ -71,10 +71,11 @@ __device__ __forceinline__ void track_len(const DS &d, uint32_t ol, uint32_t m, 
     else if (os < 4u && (int)m == d.clast[ol]) acc.inval = 1;
 }
 
-__device__ __forceinline__ void merge_change(const DS &d, uint32_t ol, uint32_t o, uint32_t m, uint32_t cst, uint32_t ce,
-                                             uint32_t csrc, uint32_t csinc, uint32_t now_e, uint32_t sched_r, MAcc &acc) {
+// cur = the row word d.mw[ol][m] (callers batch these loads)
+__device__ __forceinline__ void merge_change_w(const DS &d, uint32_t ol, uint32_t o, uint32_t m, uint32_t cur, uint32_t cst,
+                                               uint32_t ce, uint32_t csrc, uint32_t csinc, uint32_t now_e, uint32_t sched_r,
+                                               MAcc &acc) {
     const size_t idx = (size_t)ol * d.NP + m;
-    const uint32_t cur = d.mw[idx];
     const uint32_t cur_st = cur & 7u;
     uint32_t nst, ne, nsrc, nsinc;
     acc.nproc++;
@@ -117,6 +118,11 @@ __device__ __forceinline__ void merge_change(const DS &d, uint32_t ol, uint32_t 
     acc.napp++;
 }
 
+__device__ __forceinline__ void merge_change(const DS &d, uint32_t ol, uint32_t o, uint32_t m, uint32_t cst, uint32_t ce,
+                                             uint32_t csrc, uint32_t csinc, uint32_t now_e, uint32_t sched_r, MAcc &acc) {
+    merge_change_w(d, ol, o, m, d.mw[(size_t)ol * d.NP + m], cst, ce, csrc, csinc, now_e, sched_r, acc);
+}
+
 __device__ __forceinline__ void fold_row(const DS &d, uint32_t ol, int dping, int ddc, int napp, int nref, int evict,
                                          int dlen, int maxlast, int inval) {
     if (dping) d.ping[ol] += dping;
@@ -150,24 +156,50 @@ __device__ __forceinline__ void wave_finalize(const DS &d, uint32_t ol, const MA
     __threadfence_block();
 }
 
+// Batched gathers: the loops below issue MB independent loads per lane before using any of them (a
+// message's changes are distinct members, so no load of a batch depends on a store of the same batch).
+constexpr int MB = 4;
+
 // merge a whole message into row ol (wave-wide; the changes of one message are distinct members)
 __device__ void wave_merge_msg(const DS &d, uint32_t ol, uint32_t o, const MsgDesc &md, uint32_t now_e, uint32_t sched_r) {
     MAcc acc;
+    const uint32_t *rowp = d.mw + (size_t)ol * d.NP;
     if (md.kind == 0) {
         const unsigned long long off = ((unsigned long long)md.off_hi << 32) | md.off_lo;
-        for (uint32_t i = lane_id(); i < md.len; i += 64) {
-            const uint4 r = d.pool[off + i];
-            merge_change(d, ol, o, r.x & 0xFFFFFFu, r.x >> 24, r.y, r.z, r.w, now_e, sched_r, acc);
+        for (uint32_t base = 0; base < md.len; base += 64 * MB) {
+            uint4 rec[MB];
+            uint32_t cur[MB];
+#pragma unroll
+            for (int u = 0; u < MB; u++) {
+                const uint32_t i = base + u * 64 + lane_id();
+                rec[u] = i < md.len ? d.pool[off + i] : make_uint4(0xFFFFFFFFu, 0, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < MB; u++) cur[u] = rec[u].x != 0xFFFFFFFFu ? rowp[rec[u].x & 0xFFFFFFu] : 0u;
+#pragma unroll
+            for (int u = 0; u < MB; u++)
+                if (rec[u].x != 0xFFFFFFFFu)
+                    merge_change_w(d, ol, o, rec[u].x & 0xFFFFFFu, cur[u], rec[u].x >> 24, rec[u].y, rec[u].z, rec[u].w, now_e,
+                                   sched_r, acc);
         }
     } else if (md.kind == 1) {
         const uint32_t slot = md.off_lo;
         const uint4 meta = d.dense_meta[slot];
         const uint32_t *snap = d.dense + (size_t)slot * d.NP;
-        for (uint32_t m = lane_id(); m < d.N; m += 64) {
-            const uint32_t w = snap[m];
-            const uint32_t st = w & 7u;
-            if (st == ST_UNKNOWN) continue;
-            merge_change(d, ol, o, m, st, w >> 3, meta.x, meta.y, now_e, sched_r, acc);
+        for (uint32_t base = 0; base < d.N; base += 64 * MB) {
+            uint32_t w[MB], cur[MB];
+#pragma unroll
+            for (int u = 0; u < MB; u++) {
+                const uint32_t m = base + u * 64 + lane_id();
+                w[u] = m < d.N ? snap[m] : ST_UNKNOWN;
+                cur[u] = m < d.N ? rowp[m] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < MB; u++) {
+                const uint32_t m = base + u * 64 + lane_id();
+                if ((w[u] & 7u) != ST_UNKNOWN)
+                    merge_change_w(d, ol, o, m, cur[u], w[u] & 7u, w[u] >> 3, meta.x, meta.y, now_e, sched_r, acc);
+            }
         }
     }
     __threadfence_block();
@@ -179,14 +211,23 @@ __device__ void wave_bump(const DS &d, uint32_t ol, const MsgDesc &md) {
     if (md.kind != 0) return;
     const unsigned long long off = ((unsigned long long)md.off_hi << 32) | md.off_lo;
     const int maxp = d.maxp[ol];
+    uint8_t *dpr = d.dp + (size_t)ol * d.NP;
     int del = 0;
-    for (uint32_t i = lane_id(); i < md.len; i += 64) {
-        const uint32_t m = d.pool[off + i].x & 0xFFFFFFu;
-        const size_t idx = (size_t)ol * d.NP + m;
-        const uint32_t p = d.dp[idx];
-        if (p == DP_NONE) continue;
-        if ((int)(p + 1) >= maxp) { d.dp[idx] = DP_NONE; del++; }
-        else d.dp[idx] = (uint8_t)(p + 1);
+    for (uint32_t base = 0; base < md.len; base += 64 * MB) {
+        uint32_t m[MB], p[MB];
+#pragma unroll
+        for (int u = 0; u < MB; u++) {
+            const uint32_t i = base + u * 64 + lane_id();
+            m[u] = i < md.len ? (d.pool[off + i].x & 0xFFFFFFu) : 0xFFFFFFFFu;
+        }
+#pragma unroll
+        for (int u = 0; u < MB; u++) p[u] = m[u] != 0xFFFFFFFFu ? dpr[m[u]] : DP_NONE;
+#pragma unroll
+        for (int u = 0; u < MB; u++) {
+            if (p[u] == DP_NONE) continue;
+            if ((int)(p[u] + 1) >= maxp) { dpr[m[u]] = DP_NONE; del++; }
+            else dpr[m[u]] = (uint8_t)(p[u] + 1);
+        }
     }
     del = wsum(del);
     if (lane_id() == 0 && del) d.dcnt[ol] -= del;
@@ -204,86 +245,82 @@ __device__ __forceinline__ unsigned long long pool_alloc(const DS &d, uint32_t n
     return off;
 }
 
-// issueChanges / IssueAsSender (disseminator.go:128-133,201-215): snapshot of every entry
-__device__ void wave_issue(const DS &d, uint32_t ol, MsgDesc &out) {
-    const uint32_t cnt = (uint32_t)d.dcnt[ol];
-    out.kind = 0; out.len = 0; out.off_lo = out.off_hi = 0;
-    if (cnt == 0) return;
-    const unsigned long long off = pool_alloc(d, cnt);
-    if (off == ~0ull) return;
-    uint32_t pos = 0;
-    for (uint32_t w = 0; w < d.NBW; w++) {
-        unsigned long long bits = d.dblk[(size_t)ol * d.NBW + w];
-        while (bits) {
-            const uint32_t b = __ffsll((long long)bits) - 1;
-            bits &= bits - 1;
-            const uint32_t m = ((w * 64 + b) << 6) + lane_id();
-            const size_t idx = (size_t)ol * d.NP + m;
-            const bool present = d.dp[idx] != DP_NONE;
-            const unsigned long long mask = __ballot(present);
-            if (!mask) {
-                if (lane_id() == 0) d.dblk[(size_t)ol * d.NBW + w] &= ~(1ull << b);
-                continue;
-            }
-            if (present) {
-                const uint32_t rank = __popcll(mask & lanemask_lt());
-                const uint32_t wv = d.mw[idx];
-                const uint32_t st = (wv & 7u) == ST_UNKNOWN ? ST_TOMB : (wv & 7u);   // evicted: (tombstone, inc)
-                const uint4 a = d.aux[idx];
-                if (pos + rank < cnt) d.pool[off + pos + rank] = make_uint4(m | (st << 24), wv >> 3, a.x, a.y);
-            }
-            pos += __popcll(mask);
-        }
-    }
-    if (pos != cnt && lane_id() == 0) atomicOr(d.err, E_COUNT);
-    out.off_lo = (uint32_t)off;
-    out.off_hi = (uint32_t)(off >> 32);
-    out.len = min(pos, cnt);
-}
-
-// IssueAsReceiver up to the full-sync decision (disseminator.go:156-199). Returns kept count.
-__device__ uint32_t wave_issue_recv(const DS &d, uint32_t ol, uint32_t sender, uint32_t sinc, MsgDesc &out) {
+// The dissemination buffer of row ol in member order, MB non-empty 64-member blocks (dblk bits) at a
+// time: dp loads of the group first, then the entries' row words and aux, then the records.
+// RECV = IssueAsReceiver (disseminator.go:156-199): drop entries from (sender, sinc), bump the rest
+// (p++, delete at maxP). Otherwise IssueAsSender (disseminator.go:128-133,201-215).
+template <bool RECV>
+__device__ uint32_t wave_issue_t(const DS &d, uint32_t ol, uint32_t sender, uint32_t sinc, MsgDesc &out) {
     const uint32_t cnt = (uint32_t)d.dcnt[ol];
     out.kind = 0; out.len = 0; out.off_lo = out.off_hi = 0;
     if (cnt == 0) return 0;
     const unsigned long long off = pool_alloc(d, cnt);
     if (off == ~0ull) return 0;
-    const int maxp = d.maxp[ol];
+    const int maxp = RECV ? d.maxp[ol] : 0;
+    const size_t rb = (size_t)ol * d.NP;
+    unsigned long long *bw = d.dblk + (size_t)ol * d.NBW;
     uint32_t pos = 0;
     int del = 0;
     for (uint32_t w = 0; w < d.NBW; w++) {
-        unsigned long long bits = d.dblk[(size_t)ol * d.NBW + w];
+        unsigned long long bits = bw[w];
         while (bits) {
-            const uint32_t b = __ffsll((long long)bits) - 1;
-            bits &= bits - 1;
-            const uint32_t m = ((w * 64 + b) << 6) + lane_id();
-            const size_t idx = (size_t)ol * d.NP + m;
-            const uint32_t p = d.dp[idx];
-            const bool present = p != DP_NONE;
-            uint4 a = make_uint4(0, 0, 0, 0);
-            if (present) a = d.aux[idx];
-            const bool keep = present && !(a.x == sender && a.y == sinc);   // filterChangesFromSender
-            const unsigned long long kmask = __ballot(keep);
-            bool remain = present;
-            if (keep) {
-                const uint32_t rank = __popcll(kmask & lanemask_lt());
-                const uint32_t wv = d.mw[idx];
-                const uint32_t st = (wv & 7u) == ST_UNKNOWN ? ST_TOMB : (wv & 7u);
-                d.pool[off + pos + rank] = make_uint4(m | (st << 24), wv >> 3, a.x, a.y);
-                if ((int)(p + 1) >= maxp) { d.dp[idx] = DP_NONE; del++; remain = false; }   // bump
-                else d.dp[idx] = (uint8_t)(p + 1);
+            uint32_t blk[MB], p[MB];
+#pragma unroll
+            for (int k = 0; k < MB; k++) {
+                blk[k] = bits ? (uint32_t)(__ffsll((long long)bits) - 1) : 64u;
+                bits &= bits ? bits - 1 : 0ull;
             }
-            pos += __popcll(kmask);
-            if (!__ballot(remain) && lane_id() == 0) d.dblk[(size_t)ol * d.NBW + w] &= ~(1ull << b);
+#pragma unroll
+            for (int k = 0; k < MB; k++) p[k] = blk[k] < 64u ? d.dp[rb + ((w * 64 + blk[k]) << 6) + lane_id()] : DP_NONE;
+            uint4 a[MB];
+            uint32_t wv[MB];
+#pragma unroll
+            for (int k = 0; k < MB; k++) {
+                const uint32_t m = ((w * 64 + blk[k]) << 6) + lane_id();
+                a[k] = p[k] != DP_NONE ? d.aux[rb + m] : make_uint4(0, 0, 0, 0);
+                wv[k] = p[k] != DP_NONE ? d.mw[rb + m] : 0u;
+            }
+#pragma unroll
+            for (int k = 0; k < MB; k++) {
+                if (blk[k] == 64u) continue;
+                const uint32_t m = ((w * 64 + blk[k]) << 6) + lane_id();
+                const bool present = p[k] != DP_NONE;
+                const bool keep = present && !(RECV && a[k].x == sender && a[k].y == sinc);   // filterChangesFromSender
+                const unsigned long long kmask = __ballot(keep);
+                bool remain = present;
+                if (keep) {
+                    const uint32_t rank = __popcll(kmask & lanemask_lt());
+                    const uint32_t st = (wv[k] & 7u) == ST_UNKNOWN ? ST_TOMB : (wv[k] & 7u);   // evicted: (tombstone, inc)
+                    if (pos + rank < cnt) d.pool[off + pos + rank] = make_uint4(m | (st << 24), wv[k] >> 3, a[k].x, a[k].y);
+                    if (RECV) {                                                   // bump
+                        if ((int)(p[k] + 1) >= maxp) { d.dp[rb + m] = DP_NONE; del++; remain = false; }
+                        else d.dp[rb + m] = (uint8_t)(p[k] + 1);
+                    }
+                }
+                pos += __popcll(kmask);
+                if (!__ballot(remain) && lane_id() == 0) bw[w] &= ~(1ull << blk[k]);
+            }
         }
     }
-    del = wsum(del);
-    if (lane_id() == 0 && del) d.dcnt[ol] -= del;
+    if (RECV) {
+        del = wsum(del);
+        if (lane_id() == 0 && del) d.dcnt[ol] -= del;
+    } else if (pos != cnt && lane_id() == 0) {
+        atomicOr(d.err, E_COUNT);
+    }
     __threadfence_block();
     out.off_lo = (uint32_t)off;
     out.off_hi = (uint32_t)(off >> 32);
-    out.len = pos;
-    return pos;
+    out.len = min(pos, cnt);
+    return out.len;
+}
+
+// issueChanges / IssueAsSender (disseminator.go:128-133,201-215): snapshot of every entry
+__device__ void wave_issue(const DS &d, uint32_t ol, MsgDesc &out) { wave_issue_t<false>(d, ol, 0, 0, out); }
+
+// IssueAsReceiver up to the full-sync decision (disseminator.go:156-199). Returns kept count.
+__device__ uint32_t wave_issue_recv(const DS &d, uint32_t ol, uint32_t sender, uint32_t sinc, MsgDesc &out) {
+    return wave_issue_t<true>(d, ol, sender, sinc, out);
 }
 
 // MembershipAsChanges (disseminator.go:107-123) as a dense snapshot of row ol
