@@ -214,6 +214,7 @@ struct swimsim {
     uint8_t *failed = nullptr;
     MsgDesc *sdesc = nullptr, *rdesc = nullptr, *sdesc2 = nullptr, *rdesc2 = nullptr, *snapdesc = nullptr, *hdesc = nullptr;
     uint32_t *sI = nullptr, *sC = nullptr, *sI2 = nullptr, *sC2 = nullptr;
+    uint32_t *sS = nullptr, *sS2 = nullptr;       // lazy sender checksums: dense slot of the sender's row or none
     uint32_t *H = nullptr, *nh = nullptr;
     uint32_t *keys_in = nullptr, *vals_out = nullptr;    // sorted inbox: receiver column, sender-value column
     uint32_t *ukeys = nullptr, *counts = nullptr, *offs = nullptr, *nruns = nullptr, *info = nullptr;
@@ -547,9 +548,10 @@ void checksum_dirty(swimsim *h, int mode) {
 void resolve_deferred(swimsim *h, int phase, MsgDesc *rdesc, uint32_t maxn) {
     {
         Scope sc(h, F_CHECKSUM);
+        hipMemsetAsync(h->cnt, 0, 4, h->s);
         hipLaunchKernelGGL(k_defer_ids, dim3(blocks_for_threads(maxn)), dim3(256), 0, h->s, h->d, h->defer,
                            h->defer_cnt, h->list, h->cnt);
-        launch_checksum(h->d, h->list, h->cnt, maxn, h->fast_cs, h->s);
+        launch_checksum(h->d, h->list, h->cnt, 2 * maxn, h->fast_cs, h->s);
     }
     Scope sc(h, phase == 1 ? F_PINGREQ : F_RECV);
     hipLaunchKernelGGL(k_recv_finish, dim3(blocks_for_threads(maxn)), dim3(256), 0, h->s, h->d, h->defer,
@@ -564,6 +566,7 @@ void run_waves(swimsim *h, int phase, uint32_t nruns_valid, uint32_t maxcount) {
     a.sdesc = phase == 0 ? h->sdesc : h->sdesc2;
     a.sI = phase == 0 ? h->sI : h->sI2;
     a.sC = phase == 0 ? h->sC : h->sC2;
+    a.sS = h->G == 1 ? (phase == 0 ? h->sS : h->sS2) : nullptr;
     a.rdesc = phase == 0 ? h->rdesc : h->rdesc2;
     a.defer = h->defer;
     a.defer_cnt = h->defer_cnt;
@@ -789,14 +792,17 @@ int step_one(swimsim *h, const swimsim_event *ev, size_t nev) {
                            h->exh_cnt);
         hipLaunchKernelGGL(k_select_exhaust, dim3(64), dim3(64), 0, h->s, h->d, h->exh_list, h->exh_cnt, h->scratch);
     }
-    // ---- I: issue (ping requests) ----
-    checksum_dirty(h, 1);
+    // ---- I: issue (ping requests). One shard: C_o of dirty senders is lazy (k_issue). Shards: computed
+    //      here, since the value travels with the request to another shard. ----
+    const bool lazy = !sharded;
+    if (!lazy) checksum_dirty(h, 1);
     uint32_t *hi = h->hinfo;
     uint32_t ninbox = h->NL;
+    HIPCHK(h, hipMemsetAsync(h->d.dense_cur, 0, 4, h->s));         // dense snapshots live from here through R
     {
         Scope sc(h, F_ISSUE);
         hipLaunchKernelGGL(k_issue, dim3(blocks_for_waves(h->NL)), dim3(256), 0, h->s, h->d, 0, h->tgt, h->failed,
-                           h->sdesc, h->sI, h->sC);
+                           h->sdesc, h->sI, h->sC, lazy ? h->sS : nullptr);
         HIPCHK(h, hipMemsetAsync(h->info + 2, 0, 4, h->s));
         hipLaunchKernelGGL(k_pairs_direct, dim3(blocks_for_threads(h->NL)), dim3(256), 0, h->s, h->d, h->tgt, h->keys,
                            h->failed, h->info, h->xitems, h->xcnt, h->xcap);
@@ -812,7 +818,6 @@ int step_one(swimsim *h, const swimsim_event *ev, size_t nev) {
     if (sharded) ninbox = std::min(hi[5], h->keycap);
     const uint32_t nfailed = hi[4];
     if (int rc = sort_inbox(h, ninbox, hi)) return rc;
-    HIPCHK(h, hipMemsetAsync(h->d.dense_cur, 0, 4, h->s));
     run_waves(h, 0, hi[0], hi[1]);
     if (sharded) {                                                   // responses to senders on other shards
         hipLaunchKernelGGL(k_x_resp, dim3(blocks_for_threads(ninbox)), dim3(256), 0, h->s, h->d, h->keys, ninbox, 0,
@@ -834,11 +839,12 @@ int step_one(swimsim *h, const swimsim_event *ev, size_t nev) {
             hipLaunchKernelGGL(k_helpers, dim3(blocks_for_threads(h->NL)), dim3(256), 0, h->s, h->d, h->tgt, h->failed,
                                h->H, h->nh, r);
         }
-        checksum_dirty(h, 2);
+        if (!lazy) checksum_dirty(h, 2);
+        HIPCHK(h, hipMemsetAsync(h->d.dense_cur, 0, 4, h->s));     // dense snapshots live from here through Q3
         {
             Scope sc(h, F_PINGREQ);
             hipLaunchKernelGGL(k_issue, dim3(blocks_for_waves(h->NL)), dim3(256), 0, h->s, h->d, 1, h->tgt, h->failed,
-                               h->sdesc2, h->sI2, h->sC2);
+                               h->sdesc2, h->sI2, h->sC2, lazy ? h->sS2 : nullptr);
             hipLaunchKernelGGL(k_pairs_helpers, dim3(blocks_for_threads(h->NL * h->K)), dim3(256), 0, h->s, h->d,
                                h->failed, h->H, h->nh, h->keys, h->xitems, h->xcnt, h->xcap);
         }
@@ -851,7 +857,6 @@ int step_one(swimsim *h, const swimsim_event *ev, size_t nev) {
             ninbox2 = std::min(hi[5], h->keycap);
         }
         if (int rc = sort_inbox(h, ninbox2, hi)) return rc;
-        HIPCHK(h, hipMemsetAsync(h->d.dense_cur, 0, 4, h->s));
         run_waves(h, 1, hi[0], hi[1]);
         if (sharded) {
             hipLaunchKernelGGL(k_x_resp, dim3(blocks_for_threads(ninbox2)), dim3(256), 0, h->s, h->d, h->keys, ninbox2, 1,
@@ -1100,12 +1105,13 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
         (rc = dalloc(h, &h->snapdesc, h->N, "snapdesc")) || (rc = dalloc(h, &h->hdesc, 10, "hdesc")) ||
         (rc = dalloc(h, &h->sI, h->N, "sI")) || (rc = dalloc(h, &h->sC, h->N, "sC")) ||
         (rc = dalloc(h, &h->sI2, h->N, "sI2")) || (rc = dalloc(h, &h->sC2, h->N, "sC2")) ||
+        (rc = dalloc(h, &h->sS, h->N, "sS")) || (rc = dalloc(h, &h->sS2, h->N, "sS2")) ||
         (rc = dalloc(h, &h->H, NLK, "H")) || (rc = dalloc(h, &h->nh, h->NL, "nh")) ||
         (rc = dalloc(h, &h->keys, KC, "keys")) || (rc = dalloc(h, &h->keys_sorted, KC, "keys_sorted")) ||
         (rc = dalloc(h, &h->keys_in, KC, "receivers")) || (rc = dalloc(h, &h->vals_out, KC, "vals_out")) ||
         (rc = dalloc(h, &h->ukeys, KC, "ukeys")) || (rc = dalloc(h, &h->counts, KC, "counts")) ||
         (rc = dalloc(h, &h->offs, KC, "offs")) || (rc = dalloc(h, &h->nruns, 1, "nruns")) ||
-        (rc = dalloc(h, &h->info, 8, "info")) || (rc = dalloc(h, &h->list, KC + 2 * (size_t)h->NL + 64, "list")) ||
+        (rc = dalloc(h, &h->info, 8, "info")) || (rc = dalloc(h, &h->list, 2 * KC + 2 * (size_t)h->NL + 64, "list")) ||
         (rc = dalloc(h, &h->cnt, 1, "cnt")) || (rc = dalloc(h, &h->defer, KC + 2 * (size_t)h->NL + 64, "defer")) ||
         (rc = dalloc(h, &h->defer_cnt, 1, "defer_cnt")) || (rc = dalloc(h, &h->exh_list, h->NL, "exh_list")) ||
         (rc = dalloc(h, &h->exh_cnt, 1, "exh_cnt")) || (rc = dalloc(h, &h->scratch, (size_t)64 * (h->NP / 32), "scratch")) ||
@@ -1138,6 +1144,8 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
     hipMemset(d.err, 0, 4);
     hipMemset(h->need, 0, h->N);
     hipMemset(h->fsflag, 0, KC);
+    hipMemset(h->sS, 0xFF, h->N * 4);
+    hipMemset(h->sS2, 0xFF, h->N * 4);
     hipMemset(d.njobs, 0, h->NL * 4);
     h->live.assign(h->N, 1);
     h->part.assign(h->N, 0);

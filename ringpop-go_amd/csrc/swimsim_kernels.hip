@@ -594,8 +594,11 @@ __global__ void k_list_one(uint32_t *list, uint32_t *cnt, uint32_t ol, const DS 
 }
 
 // phase I (ping_sender.go:43-66) / Q1: snapshot S_o, C_o, I_o for the senders of this phase
+// Lazy C_o (sS != nullptr): a dirty sender's checksum is not computed here. Its row is snapshotted
+// (sS[o] = dense slot) and hashed only if a receiver compares it (IssueAsReceiver with nothing left to
+// send, disseminator.go:170-180), in the batched deferred resolution after the receive waves.
 __global__ void k_issue(DS d, int mode, const int32_t *tgt, const uint8_t *failed, MsgDesc *sdesc, uint32_t *sI,
-                        uint32_t *sC) {
+                        uint32_t *sC, uint32_t *sS) {
     const uint32_t ol = wave_gid();
     if (ol >= d.NL) return;
     if (mode == 0 && tgt[ol] < 0) return;
@@ -603,10 +606,16 @@ __global__ void k_issue(DS d, int mode, const int32_t *tgt, const uint8_t *faile
     const uint32_t o = d.lo + ol;
     MsgDesc md;
     wave_issue(d, ol, md);
+    uint32_t slot = SRC_NONE;
+    if (sS && d.dirty[ol]) {
+        MsgDesc sn;
+        if (wave_snapshot(d, ol, o, sn)) slot = sn.off_lo;
+    }
     if (lane_id() == 0) {
         sdesc[o] = md;                                               // message descriptors are indexed by
         sI[o] = d.mw[(size_t)ol * d.NP + o] >> 3;                    // global sender id (remote senders'
         sC[o] = d.cs[ol];                                            // messages are imported there)
+        if (sS) sS[o] = slot;
         if (mode == 0) {
             ctr_add(d, C_PINGS, 1ull);
             ctr_add(d, C_MSG_CHANGES, (unsigned long long)md.len);   // counted per helper call in Q2
@@ -733,8 +742,10 @@ struct RecvArgs {
     int phase;                                      // 0: direct ping (phase D), 1: ping-req (Q2)
     const MsgDesc *sdesc;                           // sender snapshots (by global sender id)
     const uint32_t *sI, *sC;
+    const uint32_t *sS;                             // lazy sender checksum: dense slot of the sender's row, or none
     MsgDesc *rdesc;                                 // responses (by sender id / sender id * K + slot)
-    uint4 *defer;                                   // {resp index, dense slot, sender checksum, pair index}
+    uint4 *defer;                                   // {resp index | rdirty<<31, receiver slot, sender checksum or
+                                                    //  slot, pair index | spending<<31}
     uint32_t *defer_cnt;
     uint8_t *fsflag;                                // per inbox pair: the receiver answered with a full sync
     uint32_t r;
@@ -753,9 +764,17 @@ __device__ void recv_one(const DS &d, const RecvArgs &a, uint32_t j, uint32_t se
     const uint32_t kept = wave_issue_recv(d, ol, sender, a.sI[sender_row], resp);
     if (kept == 0) {
         const uint32_t scs = a.sC[sender_row];
-        if (d.dirty[ol]) {
-            if (wave_snapshot(d, ol, j, resp) && lane_id() == 0)
-                a.defer[atomicAdd(a.defer_cnt, 1u)] = make_uint4(resp_idx, resp.off_lo, scs, pair);
+        const uint32_t sslot = a.sS ? a.sS[sender_row] : SRC_NONE;
+        const bool rdirty = d.dirty[ol] != 0;
+        if (rdirty || sslot != SRC_NONE) {
+            // a checksum is not known yet: snapshot the receiver (the full-sync payload if the decision goes that
+            // way) and decide after the batched checksum of every deferred snapshot
+            if (wave_snapshot(d, ol, j, resp) && lane_id() == 0) {
+                if (!rdirty) d.dense_cs[resp.off_lo] = d.cs[ol];
+                a.defer[atomicAdd(a.defer_cnt, 1u)] =
+                    make_uint4(resp_idx | (rdirty ? 0x80000000u : 0u), resp.off_lo, sslot != SRC_NONE ? sslot : scs,
+                               pair | (sslot != SRC_NONE ? 0x80000000u : 0u));
+            }
             resp.kind = 2;
         } else if (d.cs[ol] != scs) {
             wave_snapshot(d, ol, j, resp);
@@ -793,30 +812,33 @@ __global__ void k_recv_finish(DS d, const uint4 *defer, const uint32_t *defer_cn
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= *defer_cnt) return;
     const uint4 e = defer[i];
-    const uint32_t slot = e.y;
+    const uint32_t slot = e.y, pair = e.w & 0x7FFFFFFFu;
+    const uint32_t scs = (e.w & 0x80000000u) ? d.dense_cs[e.z] : e.z;
     MsgDesc resp;
     resp.kind = 0; resp.len = 0; resp.off_lo = resp.off_hi = 0;
-    if (d.dense_cs[slot] != e.z) {
+    if (d.dense_cs[slot] != scs) {
         resp.kind = 1; resp.off_lo = slot; resp.len = d.dense_meta[slot].z;
         ctr_add(d, phase == 1 ? C_FULL_SYNCS_PINGREQ : C_FULL_SYNCS, 1ull);
         if (phase == 2) {
             const uint32_t ol = d.dense_meta[slot].x - d.lo;
-            if (d.njobs[ol] < d.maxjobs) d.jobs[(size_t)ol * d.maxjobs + d.njobs[ol]++] = e.w;
+            if (d.njobs[ol] < d.maxjobs) d.jobs[(size_t)ol * d.maxjobs + d.njobs[ol]++] = pair;
             else ctr_add(d, C_RFS_OMITTED, 1ull);
         } else if (phase == 0) {
-            fsflag[e.w] = 1;
+            fsflag[pair] = 1;
         }
     }
-    rdesc[e.x] = resp;
+    rdesc[e.x & 0x7FFFFFFFu] = resp;
     if (phase != 2) ctr_add(d, C_MSG_CHANGES, (unsigned long long)resp.len);
 }
 
-// defer list → checksum list of dense-snapshot ids (NL + slot)
+// defer list → checksum list of the dense snapshots that need a hash (NL + slot): dirty receivers and
+// pending senders (a sender referenced by several deferred decisions is hashed once per reference)
 __global__ void k_defer_ids(DS d, const uint4 *defer, const uint32_t *defer_cnt, uint32_t *list, uint32_t *cnt) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t n = *defer_cnt;
-    if (i == 0) *cnt = n;
-    if (i < n) list[i] = d.NL + defer[i].y;
+    if (i >= *defer_cnt) return;
+    const uint4 e = defer[i];
+    if (e.x & 0x80000000u) list[atomicAdd(cnt, 1u)] = d.NL + e.y;
+    if (e.w & 0x80000000u) list[atomicAdd(cnt, 1u)] = d.NL + e.z;
 }
 
 // tryStartReverseFullSync (disseminator.go:257-278) in inbox order: at most maxjobs per receiver
@@ -985,7 +1007,7 @@ __global__ void k_ping_with(DS d, uint32_t tol, uint32_t sender, const MsgDesc *
     if (kept == 0) {
         if (d.dirty[tol]) {
             if (wave_snapshot(d, tol, d.lo + tol, resp) && lane_id() == 0)
-                defer[atomicAdd(defer_cnt, 1u)] = make_uint4(0, resp.off_lo, scs, sender);
+                defer[atomicAdd(defer_cnt, 1u)] = make_uint4(0x80000000u, resp.off_lo, scs, sender);
             resp.kind = 2;
         } else if (d.cs[tol] != scs) {
             wave_snapshot(d, tol, d.lo + tol, resp);
