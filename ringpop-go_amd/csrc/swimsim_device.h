@@ -28,7 +28,7 @@ enum Counter {
     C_SUSPECT_DECL, C_APPLIED, C_REFUTES, C_FULL_SYNCS, C_FULL_SYNCS_PINGREQ, C_RFS_DONE, C_RFS_OMITTED,
     C_TIMERS_FIRED, C_MSG_CHANGES, C_HEAL_ATTEMPTS, C_HEAL_FAILURES, C_NCOUNTERS,
     // measurement-only counters (not part of the parity record)
-    C_X_MERGED = C_NCOUNTERS, C_X_APPLIED, C_X_ISSUED, C_X_CS_ROWS, C_NALL
+    C_X_MERGED = C_NCOUNTERS, C_X_APPLIED, C_X_ISSUED, C_X_CS_ROWS, C_X_CS_DUP, C_NALL
 };
 
 constexpr int CTR_SHARDS = 64, CTR_STRIDE = 32;   // d.ctr is [CTR_SHARDS][CTR_STRIDE] u64
@@ -82,6 +82,7 @@ struct DS {
     uint32_t *dense_cs;     // checksum of each snapshot (deferred full-sync decisions)
     uint32_t *clen;         // [NL] checksum-string length of each row
     int32_t *clast;         // [NL] last included member (-2: rescan)
+    unsigned long long *fp; // [NL] row fingerprint: sum over members of fpmix(m, member word), kept by the merges
     uint32_t dig_d0;          // decimal digits of t0
     uint32_t max_tail;        // longest record tail (status ‖ digits ‖ ';') in the incarnation table
     uint32_t min_tail;        // shortest one
@@ -219,6 +220,14 @@ struct FH {
         return h;
     }
 };
+
+// per-member term of the row fingerprint (order-free sum; equal rows have equal sums, so the
+// checksum kernel hashes one row per distinct content after an exact comparison)
+__host__ __device__ inline uint64_t fpmix(uint32_t m, uint32_t w) {
+    uint64_t k = ((uint64_t)m << 32) | w;
+    k ^= k >> 33; k *= 0xff51afd7ed558ccdULL; k ^= k >> 33; k *= 0xc4ceb9fe1a85ec53ULL; k ^= k >> 33;
+    return k;
+}
 
 // canonical state digest mix (identical definition in oracle/swim_oracle.c or_digest)
 __host__ __device__ inline uint64_t fmix64(uint64_t k) {

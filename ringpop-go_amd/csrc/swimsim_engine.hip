@@ -215,6 +215,9 @@ struct swimsim {
     MsgDesc *sdesc = nullptr, *rdesc = nullptr, *sdesc2 = nullptr, *rdesc2 = nullptr, *snapdesc = nullptr, *hdesc = nullptr;
     uint32_t *sI = nullptr, *sC = nullptr, *sI2 = nullptr, *sC2 = nullptr;
     uint32_t *sS = nullptr, *sS2 = nullptr;       // lazy sender checksums: dense slot of the sender's row or none
+    uint32_t *fpv = nullptr, *fpv_s = nullptr, *fph = nullptr, *fph_s = nullptr, *fplist = nullptr, *fpcnt = nullptr,
+             *dup_of = nullptr;                   // checksum dedup (rows by fingerprint)
+    uint8_t *hflag = nullptr;
     uint32_t *H = nullptr, *nh = nullptr;
     uint32_t *keys_in = nullptr, *vals_out = nullptr;    // sorted inbox: receiver column, sender-value column
     uint32_t *ukeys = nullptr, *counts = nullptr, *offs = nullptr, *nruns = nullptr, *info = nullptr;
@@ -535,12 +538,41 @@ int shard_sum(swimsim *h, uint64_t v, uint64_t *out) {
     return 0;
 }
 
-void checksum_dirty(swimsim *h, int mode) {
+// checksums of the dirty rows selected by mode (k_list). Mode 0 (all dirty rows) hashes one row per
+// distinct content: rows are grouped by fingerprint, compared word for word with their group's first
+// row, and equal rows copy its checksum (k_fp_*).
+int checksum_dirty(swimsim *h, int mode) {
     Scope sc(h, F_CHECKSUM);
-    hipMemsetAsync(h->cnt, 0, 4, h->s);
+    HIPCHK(h, hipMemsetAsync(h->cnt, 0, 4, h->s));
     hipLaunchKernelGGL(k_list, dim3(blocks_for_threads(h->NL)), dim3(256), 0, h->s, h->d, mode, h->tgt, h->failed,
                        h->list, h->cnt);
-    launch_checksum(h->d, h->list, h->cnt, h->NL, h->fast_cs, h->s);
+    if (mode != 0) {
+        launch_checksum(h->d, h->list, h->cnt, h->NL, h->fast_cs, h->s);
+        return 0;
+    }
+    uint32_t *hn = h->hinfo + 8;
+    HIPCHK(h, hipMemcpyAsync(hn, h->cnt, 4, hipMemcpyDeviceToHost, h->s));
+    HIPCHK(h, hipStreamSynchronize(h->s));
+    const uint32_t n = *hn;
+    if (n < 2) {
+        launch_checksum(h->d, h->list, h->cnt, n, h->fast_cs, h->s);
+        return 0;
+    }
+    hipLaunchKernelGGL(k_fp_keys, dim3(blocks_for_threads(n)), dim3(256), 0, h->s, h->d, h->list, n, h->keys, h->fpv);
+    size_t bytes = h->cub_bytes;
+    HIPCHK(h, hipcub::DeviceRadixSort::SortPairs(h->cub_tmp, bytes, h->keys, h->keys_sorted, h->fpv, h->fpv_s, (int)n, 0,
+                                                 64, h->s));
+    hipLaunchKernelGGL(k_fp_heads, dim3(blocks_for_threads(n)), dim3(256), 0, h->s, h->keys_sorted, n, h->fph);
+    bytes = h->cub_bytes;
+    HIPCHK(h, hipcub::DeviceScan::InclusiveScan(h->cub_tmp, bytes, h->fph, h->fph_s, hipcub::Max(), (int)n, h->s));
+    HIPCHK(h, hipMemsetAsync(h->fpcnt, 0, 4, h->s));
+    hipLaunchKernelGGL(k_fp_verify, dim3(blocks_for_waves(n)), dim3(256), 0, h->s, h->d, h->fpv_s, h->fph_s, n, h->hflag,
+                       h->dup_of);
+    hipLaunchKernelGGL(k_list_flagged, dim3(blocks_for_threads(h->NL)), dim3(256), 0, h->s, h->NL, h->hflag, h->fplist,
+                       h->fpcnt);
+    launch_checksum(h->d, h->fplist, h->fpcnt, n, h->fast_cs, h->s);
+    hipLaunchKernelGGL(k_fp_copy, dim3(blocks_for_threads(n)), dim3(256), 0, h->s, h->d, h->fpv_s, n, h->dup_of);
+    return 0;
 }
 
 // run the receive waves over a sorted inbox (phase D when phase==0, phase Q2 when phase==1), then
@@ -573,8 +605,7 @@ void run_waves(swimsim *h, int phase, uint32_t nruns_valid, uint32_t maxcount) {
     a.fsflag = h->fsflag;
     a.r = h->round;
     hipMemsetAsync(h->defer_cnt, 0, 4, h->s);
-    for (uint32_t w = 0; w < maxcount; w++) {
-        a.w = w;
+    {
         Scope sc(h, phase == 0 ? F_RECV : F_PINGREQ);
         hipLaunchKernelGGL(k_recv, dim3(blocks_for_waves(nruns_valid)), dim3(256), 0, h->s, h->d, a);
     }
@@ -898,7 +929,7 @@ int step_one(swimsim *h, const swimsim_event *ev, size_t nev) {
                            h->need);
     }
     // ---- C: checksums of dirty rows ----
-    checksum_dirty(h, 0);
+    if (int rc = checksum_dirty(h, 0)) return rc;
     h->round++;
     h->host_ctr[SWIMSIM_C_ROUNDS]++;
     HIPCHK(h, hipGetLastError());
@@ -1106,6 +1137,10 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
         (rc = dalloc(h, &h->sI, h->N, "sI")) || (rc = dalloc(h, &h->sC, h->N, "sC")) ||
         (rc = dalloc(h, &h->sI2, h->N, "sI2")) || (rc = dalloc(h, &h->sC2, h->N, "sC2")) ||
         (rc = dalloc(h, &h->sS, h->N, "sS")) || (rc = dalloc(h, &h->sS2, h->N, "sS2")) ||
+        (rc = dalloc(h, &h->fpv, h->NL, "fpv")) || (rc = dalloc(h, &h->fpv_s, h->NL, "fpv_s")) ||
+        (rc = dalloc(h, &h->fph, h->NL, "fph")) || (rc = dalloc(h, &h->fph_s, h->NL, "fph_s")) ||
+        (rc = dalloc(h, &h->fplist, h->NL, "fplist")) || (rc = dalloc(h, &h->fpcnt, 1, "fpcnt")) ||
+        (rc = dalloc(h, &h->dup_of, h->NL, "dup_of")) || (rc = dalloc(h, &h->hflag, h->NL, "hflag")) || (rc = dalloc(h, &h->d.fp, h->NL, "fp")) ||
         (rc = dalloc(h, &h->H, NLK, "H")) || (rc = dalloc(h, &h->nh, h->NL, "nh")) ||
         (rc = dalloc(h, &h->keys, KC, "keys")) || (rc = dalloc(h, &h->keys_sorted, KC, "keys_sorted")) ||
         (rc = dalloc(h, &h->keys_in, KC, "receivers")) || (rc = dalloc(h, &h->vals_out, KC, "vals_out")) ||
@@ -1123,11 +1158,13 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
     if ((rc = dalloc(h, &h->evbuf, h->evcap, "events")) || (rc = dalloc(h, &h->ev_applied, h->evcap, "ev_applied")))
         return bail(rc);
     {
-        size_t b1 = 0, b2 = 0, b3 = 0;
+        size_t b1 = 0, b2 = 0, b3 = 0, b4 = 0, b5 = 0;
         hipcub::DeviceRadixSort::SortKeys(nullptr, b1, h->keys, h->keys_sorted, (int)KC, 0, 64);
         hipcub::DeviceRunLengthEncode::Encode(nullptr, b2, h->keys_in, h->ukeys, h->counts, h->nruns, (int)KC);
         hipcub::DeviceScan::ExclusiveSum(nullptr, b3, h->counts, h->offs, (int)KC);
-        h->cub_bytes = std::max(b1, std::max(b2, b3));
+        hipcub::DeviceRadixSort::SortPairs(nullptr, b4, h->keys, h->keys_sorted, h->fpv, h->fpv_s, (int)h->NL, 0, 64);
+        hipcub::DeviceScan::InclusiveScan(nullptr, b5, h->fph, h->fph_s, hipcub::Max(), (int)h->NL);
+        h->cub_bytes = std::max(std::max(b1, std::max(b2, b3)), std::max(b4, b5));
         if ((rc = dalloc(h, (uint8_t **)&h->cub_tmp, h->cub_bytes, "cub temp"))) return bail(rc);
     }
     // single shard until swimsim_comm_attach / swimsim_group_create says otherwise
@@ -1145,6 +1182,7 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
     hipMemset(h->need, 0, h->N);
     hipMemset(h->fsflag, 0, KC);
     hipMemset(h->sS, 0xFF, h->N * 4);
+    hipMemset(h->hflag, 0, h->NL);
     hipMemset(h->sS2, 0xFF, h->N * 4);
     hipMemset(d.njobs, 0, h->NL * 4);
     h->live.assign(h->N, 1);
@@ -1491,6 +1529,7 @@ int swimsim_kernel_times(swimsim_t *h, const char **names, double *avg_ms, uint6
     const double applied = (double)(c[C_X_APPLIED] - h->fam_bytes_base[C_X_APPLIED]);
     const double issued = (double)(c[C_X_ISSUED] - h->fam_bytes_base[C_X_ISSUED]);
     const double csrows = (double)(c[C_X_CS_ROWS] - h->fam_bytes_base[C_X_CS_ROWS]);
+    const double csdups = (double)(c[C_X_CS_DUP] - h->fam_bytes_base[C_X_CS_DUP]);
     // algorithmic bytes: merge = 16 B record + 4 B row word read per processed
     // change; + 4 B row word + 1 B counter + 16 B dissem/timer entry + 1 B timer state per applied change.
     // checksum = 4 B member word per member per dirty row. issue = 16 B per record written (+ 16 B read).
@@ -1501,7 +1540,7 @@ int swimsim_kernel_times(swimsim_t *h, const char **names, double *avg_ms, uint6
         if (launches) launches[f] = h->fam_n[f];
         if (alg_bytes) {
             double b = 0;
-            if (f == F_CHECKSUM) b = csrows * 4.0 * h->N;
+            if (f == F_CHECKSUM) b = csrows * 4.0 * h->N + csdups * 8.0 * h->N;   // hashed rows + verified duplicates
             if (f == F_ISSUE) b = issued * 32.0;
             if (f == F_RECV) b = merge_bytes;  // merge volume is attributed to the receive waves (the bulk)
             alg_bytes[f] = b;

@@ -49,7 +49,8 @@ __device__ __forceinline__ bool reach(const DS &d, uint32_t a, uint32_t b) {
 // ---------------------------------------------------------------------------------------------
 struct MAcc {
     int dping, ddc, napp, nref, nproc, evict, dlen, maxlast, inval;
-    __device__ MAcc() : dping(0), ddc(0), napp(0), nref(0), nproc(0), evict(0), dlen(0), maxlast(-1), inval(0) {}
+    unsigned long long dfp;   // row fingerprint delta
+    __device__ MAcc() : dping(0), ddc(0), napp(0), nref(0), nproc(0), evict(0), dlen(0), maxlast(-1), inval(0), dfp(0) {}
 };
 
 // bytes of one member's checksum record addr ‖ status ‖ decimal(inc) ‖ ';' (memberlist.go:115-121);
@@ -92,6 +93,7 @@ __device__ __forceinline__ void merge_change_w(const DS &d, uint32_t ol, uint32_
     }
     d.mw[idx] = (ne << 3) | nst;
     track_len(d, ol, m, cur, (ne << 3) | nst, acc);
+    acc.dfp += fpmix(m, (ne << 3) | nst) - fpmix(m, cur);
     if (m != o) acc.dping += (int)is_pingable(nst) - (int)is_pingable(cur_st);
     // RecordChange (disseminator.go:223-227): entry = {p 0, source, source incarnation}
     if (d.dp[idx] == DP_NONE) acc.ddc++;
@@ -124,7 +126,8 @@ __device__ __forceinline__ void merge_change(const DS &d, uint32_t ol, uint32_t 
 }
 
 __device__ __forceinline__ void fold_row(const DS &d, uint32_t ol, int dping, int ddc, int napp, int nref, int evict,
-                                         int dlen, int maxlast, int inval) {
+                                         int dlen, int maxlast, int inval, unsigned long long dfp) {
+    if (dfp) d.fp[ol] += dfp;
     if (dping) d.ping[ol] += dping;
     if (ddc) d.dcnt[ol] += ddc;
     if (napp) {
@@ -148,8 +151,11 @@ __device__ __forceinline__ void wave_finalize(const DS &d, uint32_t ol, const MA
     const int dping = wsum(acc.dping), ddc = wsum(acc.ddc), napp = wsum(acc.napp), nref = wsum(acc.nref);
     const int ev = wsum(acc.evict), np = wsum(acc.nproc), dl = wsum(acc.dlen), ml = wmax(acc.maxlast);
     const int inv = wmax(acc.inval);
+    unsigned long long dfp = acc.dfp;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) dfp += __shfl_xor(dfp, off, 64);
     if (lane_id() == 0) {
-        fold_row(d, ol, dping, ddc, napp, nref, ev, dl, ml, inv);
+        fold_row(d, ol, dping, ddc, napp, nref, ev, dl, ml, inv, dfp);
         if (np) ctr_add(d, C_X_MERGED, (unsigned long long)np);
         if (napp) ctr_add(d, C_X_APPLIED, (unsigned long long)napp);
     }
@@ -358,10 +364,12 @@ __global__ void k_init_rows(DS d, int mode, uint32_t e0) {
     const uint32_t ol = wave_gid();
     if (ol >= d.NL) return;
     const uint32_t o = d.lo + ol;
+    unsigned long long fp = 0;
     for (uint32_t m = lane_id(); m < d.NP; m += 64) {
         const size_t idx = (size_t)ol * d.NP + m;
         uint32_t w = ST_UNKNOWN;
         if (m < d.N && (mode == 0 || m == o)) w = (e0 << 3) | ST_ALIVE;
+        if (m < d.N) fp += fpmix(m, w);
         d.mw[idx] = w;
         d.dp[idx] = DP_NONE;
         d.tst[idx] = 0;
@@ -369,7 +377,10 @@ __global__ void k_init_rows(DS d, int mode, uint32_t e0) {
     }
     for (uint32_t b = lane_id(); b < d.NB; b += 64) d.tblk[(size_t)ol * d.NB + b] = NO_DEADLINE;
     for (uint32_t b = lane_id(); b < d.NBW; b += 64) d.dblk[(size_t)ol * d.NBW + b] = 0;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) fp += __shfl_xor(fp, off, 64);
     if (lane_id() == 0) {
+        d.fp[ol] = fp;
         const int32_t p = mode == 0 ? (int32_t)d.N - 1 : 0;
         const uint32_t rl = (uint32_t)reclen(d, ST_ALIVE, e0);
         d.clen[ol] = mode == 0 ? rl * d.N : rl;
@@ -390,9 +401,11 @@ __global__ void k_init_rows(DS d, int mode, uint32_t e0) {
 __global__ void k_recount(DS d, uint32_t ol) {
     const uint32_t o = d.lo + ol;
     int p = 0, c = 0, len = 0, last = -1;
+    unsigned long long fp = 0;
     for (uint32_t m = lane_id(); m < d.N; m += 64) {
         const size_t idx = (size_t)ol * d.NP + m;
         const uint32_t w = d.mw[idx];
+        fp += fpmix(m, w);
         if (m != o && is_pingable(w & 7u)) p++;
         if (d.dp[idx] != DP_NONE) c++;
         len += reclen(d, w & 7u, w >> 3);
@@ -402,7 +415,11 @@ __global__ void k_recount(DS d, uint32_t ol) {
     c = wsum(c);
     len = wsum(len);
     last = wmax(last);
-    if (lane_id() == 0) { d.ping[ol] = p; d.dcnt[ol] = c; d.dirty[ol] = 1; d.clen[ol] = (uint32_t)len; d.clast[ol] = last; }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) fp += __shfl_xor(fp, off, 64);
+    if (lane_id() == 0) {
+        d.ping[ol] = p; d.dcnt[ol] = c; d.dirty[ol] = 1; d.clen[ol] = (uint32_t)len; d.clast[ol] = last; d.fp[ol] = fp;
+    }
 }
 
 __global__ void k_clear_changes(DS d, uint32_t ol) {
@@ -419,7 +436,7 @@ __device__ int thread_make_change(const DS &d, uint32_t ol, uint32_t o, uint32_t
     MAcc acc;
     const uint32_t self_e = d.mw[(size_t)ol * d.NP + o] >> 3;   // MakeChange: SourceIncarnation = local inc
     merge_change(d, ol, o, m, st, e, o, self_e, r, r, acc);
-    fold_row(d, ol, acc.dping, acc.ddc, acc.napp, acc.nref, 0, acc.dlen, acc.maxlast, acc.inval);
+    fold_row(d, ol, acc.dping, acc.ddc, acc.napp, acc.nref, 0, acc.dlen, acc.maxlast, acc.inval, acc.dfp);
     return acc.napp;
 }
 
@@ -491,6 +508,7 @@ __global__ void k_timers(DS d, uint32_t r) {
                         if (is_pingable(w & 7u)) acc.dping--;
                         d.mw[idx] = (w & ~7u) | ST_UNKNOWN;
                         track_len(d, ol, m, w, (w & ~7u) | ST_UNKNOWN, acc);
+                        acc.dfp += fpmix(m, (w & ~7u) | ST_UNKNOWN) - fpmix(m, w);
                         acc.evict++;
                     }
                 }
@@ -738,7 +756,6 @@ __global__ void k_runs_info(const uint32_t *ukeys, const uint32_t *counts, const
 struct RecvArgs {
     const uint32_t *ukeys, *counts, *offs, *vals;   // run-length encoded sorted inbox
     uint32_t nruns_max;
-    uint32_t w;                                     // wave index
     int phase;                                      // 0: direct ping (phase D), 1: ping-req (Q2)
     const MsgDesc *sdesc;                           // sender snapshots (by global sender id)
     const uint32_t *sI, *sC;
@@ -794,15 +811,22 @@ __device__ void recv_one(const DS &d, const RecvArgs &a, uint32_t j, uint32_t se
     }
 }
 
+// One wave per receiver runs its whole inbox in sender order. Receivers are independent within the
+// phase: a receiver writes only its own row, dissemination buffer and timers, and reads only the
+// senders' issue-time snapshots (S_o, I_o, C_o). So this equals the wave-by-wave schedule of
+// docs/ROUND_SEMANTICS.md §4 D, without a launch per inbox position.
 __global__ void k_recv(DS d, RecvArgs a) {
     const uint32_t u = wave_gid();
     if (u >= a.nruns_max) return;
     const uint32_t key = a.ukeys[u];
-    if (key >= d.N || a.counts[u] <= a.w) return;
-    const uint32_t pair = a.offs[u] + a.w;
-    const uint32_t v = a.vals[pair];
-    if (a.phase == 0) recv_one(d, a, key, v, v, pair);
-    else recv_one(d, a, key, v / d.K, v, pair);
+    if (key >= d.N) return;
+    const uint32_t n = a.counts[u], off = a.offs[u];
+    for (uint32_t w = 0; w < n; w++) {
+        const uint32_t pair = off + w;
+        const uint32_t v = a.vals[pair];
+        if (a.phase == 0) recv_one(d, a, key, v, v, pair);
+        else recv_one(d, a, key, v / d.K, v, pair);
+    }
 }
 
 // resolve deferred full-sync decisions once the snapshot checksums exist (phase 2 = heal ping:
@@ -926,6 +950,73 @@ __global__ void k_jobs_reset(DS d, uint8_t *need) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < d.NL) d.njobs[i] = 0;
     if (i < d.N) need[i] = 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// phase C dedup: dirty rows with equal content have equal checksums. Rows are grouped by their
+// fingerprint (sorted), every row is compared word for word with the first row of its group, and
+// only group heads and rows that differ from their head are hashed; the others copy the head's
+// checksum. Exact: the fingerprint only proposes the pairs that the comparison checks.
+// ---------------------------------------------------------------------------------------------
+__global__ void k_fp_keys(DS d, const uint32_t *list, uint32_t n, unsigned long long *keys, uint32_t *vals) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    keys[i] = d.fp[list[i]];
+    vals[i] = list[i];
+}
+
+__global__ void k_fp_heads(const unsigned long long *keys, uint32_t n, uint32_t *headpos) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    headpos[i] = (i == 0 || keys[i] != keys[i - 1]) ? i : 0u;   // inclusive max-scan gives each row its group head
+}
+
+// one wave per sorted row: heads and rows unequal to their head are flagged for hashing (the hash
+// list is then rebuilt in row order: rows of one workgroup stay close in memory, few TLB pages)
+__global__ void k_fp_verify(DS d, const uint32_t *vals, const uint32_t *headpos, uint32_t n, uint8_t *hflag,
+                            uint32_t *dup_of) {
+    const uint32_t i = wave_gid();
+    if (i >= n) return;
+    const uint32_t row = vals[i], hp = headpos[i];
+    bool same = false;
+    if (hp != i) {
+        const uint4 *a = (const uint4 *)(d.mw + (size_t)vals[hp] * d.NP);
+        const uint4 *b = (const uint4 *)(d.mw + (size_t)row * d.NP);
+        bool diff = false;
+        for (uint32_t base = 0; base < d.NP / 4 && !__any(diff); base += 64 * MB) {
+            uint4 x[MB], y[MB];
+#pragma unroll
+            for (int u = 0; u < MB; u++) {
+                const uint32_t k = base + u * 64 + lane_id();
+                x[u] = k < d.NP / 4 ? a[k] : make_uint4(0, 0, 0, 0);
+                y[u] = k < d.NP / 4 ? b[k] : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < MB; u++) diff |= x[u].x != y[u].x || x[u].y != y[u].y || x[u].z != y[u].z || x[u].w != y[u].w;
+        }
+        same = !__any(diff);
+    }
+    if (lane_id() == 0) {
+        dup_of[row] = same ? vals[hp] : SRC_NONE;
+        hflag[row] = same ? 0 : 1;
+    }
+}
+
+__global__ void k_list_flagged(uint32_t nl, uint8_t *flag, uint32_t *list, uint32_t *cnt) {
+    const uint32_t ol = blockIdx.x * blockDim.x + threadIdx.x;
+    if (ol >= nl || !flag[ol]) return;
+    flag[ol] = 0;
+    list[atomicAdd(cnt, 1u)] = ol;
+}
+
+__global__ void k_fp_copy(DS d, const uint32_t *vals, uint32_t n, const uint32_t *dup_of) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t row = vals[i], h = dup_of[row];
+    if (h == SRC_NONE) return;
+    d.cs[row] = d.cs[h];
+    d.dirty[row] = 0;
+    ctr_add(d, C_X_CS_DUP, 1ull);
 }
 
 #include "swimsim_checksum.hip"
