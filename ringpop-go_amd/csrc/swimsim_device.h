@@ -7,8 +7,9 @@
 //                      unsigned compare.
 //   dp  u8  [NL][NP]   disseminator piggyback counter p (disseminator.go:39-42); 0xFF = no entry
 //   tst u8  [NL][NP]   timer state (suspect 1 / faulty 2 / tombstone 4) | 0x80 fired
-//   aux u32x4[NL][NP]  {dissem source, dissem source e, timer deadline round, timer subject e}
-//   dblk u64 [NL][NBW] bit b: 64-member block b may hold dissemination entries
+//   dsrc u32x2[NL][NP] dissemination entry {source, source e}
+//   tmr u32x2 [NL][NP] timer {deadline round, subject e}
+//   dbit u32 [NL][NBIT] bit m: member m has a dissemination entry (exactly: dp[m] != 0xFF)
 //   tblk u32 [NL][NB]  lower bound of the unfired timer deadlines in block b
 // Messages are pools of 16-byte change records {member | status<<24, e, source, source e}, or
 // dense row snapshots for MembershipAsChanges (disseminator.go:107-123).
@@ -53,12 +54,14 @@ struct DS {
     uint32_t *mw;
     uint8_t *dp;
     uint8_t *tst;
-    uint4 *aux;
+    uint2 *dsrc;            // {dissemination source, source e}
+    uint2 *tmr;             // {timer deadline round, timer subject e}
+    uint32_t *dbit;         // [NL][NBIT] dissemination presence bits
+    uint32_t NBIT;          // words per row of dbit (multiple of 4)
     int32_t *ping, *maxp, *dcnt;
     uint32_t *dirty, *cs;
     int32_t *it_idx;
     uint32_t *it_ep, *tmin, *njobs, *jobs;
-    unsigned long long *dblk;
     uint32_t *tblk;
     uint8_t *live;
     int32_t *part;

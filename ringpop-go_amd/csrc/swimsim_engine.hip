@@ -1072,19 +1072,21 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
     d.N = h->N; d.NP = h->NP; d.NL = h->NL; d.lo = h->lo;
     d.NB = h->NP / 64;
     d.NBW = (d.NB + 63) / 64;
+    d.NBIT = ((h->NP / 32) + 3) & ~3u;
     d.W = h->W; d.pfactor = h->pfactor; d.K = h->K; d.maxjobs = h->maxjobs;
     d.to_susp = h->to_susp; d.to_faulty = h->to_faulty; d.to_tomb = h->to_tomb;
     d.seed = h->seed;
     const size_t rows = (size_t)h->NL * h->NP;
     int rc = 0;
     if ((rc = dalloc(h, &d.mw, rows, "member words")) || (rc = dalloc(h, &d.dp, rows, "piggyback counters")) ||
-        (rc = dalloc(h, &d.tst, rows, "timer states")) || (rc = dalloc(h, &d.aux, rows, "aux")) ||
+        (rc = dalloc(h, &d.tst, rows, "timer states")) || (rc = dalloc(h, &d.dsrc, rows, "dissemination sources")) ||
+        (rc = dalloc(h, &d.tmr, rows, "timers")) ||
         (rc = dalloc(h, &d.ping, h->NL, "ping")) || (rc = dalloc(h, &d.maxp, h->NL, "maxp")) ||
         (rc = dalloc(h, &d.dcnt, h->NL, "dcnt")) || (rc = dalloc(h, &d.dirty, h->NL, "dirty")) ||
         (rc = dalloc(h, &d.cs, h->NL, "cs")) || (rc = dalloc(h, &d.it_idx, h->NL, "it_idx")) ||
         (rc = dalloc(h, &d.it_ep, h->NL, "it_ep")) || (rc = dalloc(h, &d.tmin, h->NL, "tmin")) ||
         (rc = dalloc(h, &d.njobs, h->NL, "njobs")) || (rc = dalloc(h, &d.jobs, (size_t)h->NL * h->maxjobs, "jobs")) ||
-        (rc = dalloc(h, &d.dblk, (size_t)h->NL * d.NBW, "dblk")) || (rc = dalloc(h, &d.tblk, (size_t)h->NL * d.NB, "tblk")) ||
+        (rc = dalloc(h, &d.dbit, (size_t)h->NL * d.NBIT, "dbit")) || (rc = dalloc(h, &d.tblk, (size_t)h->NL * d.NB, "tblk")) ||
         (rc = dalloc(h, &d.live, h->N, "live")) || (rc = dalloc(h, &d.part, h->N, "part")) ||
         (rc = dalloc(h, &d.ctr, (size_t)CTR_SHARDS * CTR_STRIDE, "counters")) || (rc = dalloc(h, &d.err, 4, "err")) ||
         (rc = dalloc(h, &d.clen, h->NL, "clen")) || (rc = dalloc(h, &d.clast, h->NL, "clast")))
@@ -1364,9 +1366,9 @@ int swimsim_changes(swimsim_t *h, uint32_t o, int32_t *member, int32_t *p, int32
     if (!h || !own(h, o)) return SWIMSIM_EINVAL;
     const size_t base = (size_t)(o - h->lo) * h->NP;
     std::vector<uint8_t> dp(h->NP);
-    std::vector<uint4> aux(h->NP);
+    std::vector<uint2> aux(h->NP);
     HIPCHK(h, hipMemcpyAsync(dp.data(), h->d.dp + base, h->NP, hipMemcpyDeviceToHost, h->s));
-    HIPCHK(h, hipMemcpyAsync(aux.data(), h->d.aux + base, h->NP * 16, hipMemcpyDeviceToHost, h->s));
+    HIPCHK(h, hipMemcpyAsync(aux.data(), h->d.dsrc + base, h->NP * 8, hipMemcpyDeviceToHost, h->s));
     HIPCHK(h, hipStreamSynchronize(h->s));
     size_t k = 0;
     for (uint32_t m = 0; m < h->N; m++) {
@@ -1388,9 +1390,9 @@ int swimsim_timers(swimsim_t *h, uint32_t o, int32_t *member, int32_t *state, in
     if (!h || !own(h, o)) return SWIMSIM_EINVAL;
     const size_t base = (size_t)(o - h->lo) * h->NP;
     std::vector<uint8_t> ts(h->NP);
-    std::vector<uint4> aux(h->NP);
+    std::vector<uint2> aux(h->NP);
     HIPCHK(h, hipMemcpyAsync(ts.data(), h->d.tst + base, h->NP, hipMemcpyDeviceToHost, h->s));
-    HIPCHK(h, hipMemcpyAsync(aux.data(), h->d.aux + base, h->NP * 16, hipMemcpyDeviceToHost, h->s));
+    HIPCHK(h, hipMemcpyAsync(aux.data(), h->d.tmr + base, h->NP * 8, hipMemcpyDeviceToHost, h->s));
     HIPCHK(h, hipStreamSynchronize(h->s));
     size_t k = 0;
     for (uint32_t m = 0; m < h->N; m++) {
@@ -1399,8 +1401,8 @@ int swimsim_timers(swimsim_t *h, uint32_t o, int32_t *member, int32_t *state, in
             if (member) member[k] = (int32_t)m;
             if (state) state[k] = ts[m] & 7;
             if (fired) fired[k] = (ts[m] >> 7) & 1;
-            if (deadline_ms) deadline_ms[k] = from_e(h, aux[m].z);
-            if (subject_inc_ms) subject_inc_ms[k] = from_e(h, aux[m].w);
+            if (deadline_ms) deadline_ms[k] = from_e(h, aux[m].x);
+            if (subject_inc_ms) subject_inc_ms[k] = from_e(h, aux[m].y);
         }
         k++;
     }

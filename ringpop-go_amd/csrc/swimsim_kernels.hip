@@ -96,12 +96,12 @@ __device__ __forceinline__ void merge_change_w(const DS &d, uint32_t ol, uint32_
     acc.dfp += fpmix(m, (ne << 3) | nst) - fpmix(m, cur);
     if (m != o) acc.dping += (int)is_pingable(nst) - (int)is_pingable(cur_st);
     // RecordChange (disseminator.go:223-227): entry = {p 0, source, source incarnation}
-    if (d.dp[idx] == DP_NONE) acc.ddc++;
+    if (d.dp[idx] == DP_NONE) {
+        acc.ddc++;
+        atomicOr(&d.dbit[(size_t)ol * d.NBIT + (m >> 5)], 1u << (m & 31));
+    }
     d.dp[idx] = 0;
-    uint4 a = d.aux[idx];
-    a.x = nsrc;
-    a.y = nsinc;
-    atomicOr(&d.dblk[(size_t)ol * d.NBW + (m >> 12)], 1ull << ((m >> 6) & 63));
+    d.dsrc[idx] = make_uint2(nsrc, nsinc);
     if (m != o) {                                                  // no timers for the local member
         const uint8_t ts = d.tst[idx];
         const uint32_t tstate = ts & 7u;
@@ -110,13 +110,11 @@ __device__ __forceinline__ void merge_change_w(const DS &d, uint32_t ol, uint32_
         } else if (tstate != nst) {                                // same state: no-op (130-136)
             const uint32_t dl = sched_r + timeout_rounds(d, nst);
             d.tst[idx] = (uint8_t)nst;
-            a.z = dl;
-            a.w = ne;                                              // subject = the applied change
+            d.tmr[idx] = make_uint2(dl, ne);                       // subject = the applied change
             atomicMin(&d.tblk[(size_t)ol * d.NB + (m >> 6)], dl);
             atomicMin(&d.tmin[ol], dl);
         }
     }
-    d.aux[idx] = a;
     acc.napp++;
 }
 
@@ -231,8 +229,13 @@ __device__ void wave_bump(const DS &d, uint32_t ol, const MsgDesc &md) {
 #pragma unroll
         for (int u = 0; u < MB; u++) {
             if (p[u] == DP_NONE) continue;
-            if ((int)(p[u] + 1) >= maxp) { dpr[m[u]] = DP_NONE; del++; }
-            else dpr[m[u]] = (uint8_t)(p[u] + 1);
+            if ((int)(p[u] + 1) >= maxp) {
+                dpr[m[u]] = DP_NONE;
+                atomicAnd(&d.dbit[(size_t)ol * d.NBIT + (m[u] >> 5)], ~(1u << (m[u] & 31)));
+                del++;
+            } else {
+                dpr[m[u]] = (uint8_t)(p[u] + 1);
+            }
         }
     }
     del = wsum(del);
@@ -251,10 +254,24 @@ __device__ __forceinline__ unsigned long long pool_alloc(const DS &d, uint32_t n
     return off;
 }
 
-// The dissemination buffer of row ol in member order, MB non-empty 64-member blocks (dblk bits) at a
-// time: dp loads of the group first, then the entries' row words and aux, then the records.
-// RECV = IssueAsReceiver (disseminator.go:156-199): drop entries from (sender, sinc), bump the rest
-// (p++, delete at maxP). Otherwise IssueAsSender (disseminator.go:128-133,201-215).
+__device__ __forceinline__ uint32_t wscan_excl(uint32_t v, uint32_t &total) {
+    uint32_t x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, off, 64);
+        if (lane_id() >= (uint32_t)off) x += y;
+    }
+    total = (uint32_t)__shfl((int)x, 63, 64);
+    return x - v;
+}
+
+// The dissemination buffer of row ol from its presence bitmap: each lane owns 4 bitmap words (128
+// members) per pass and walks its set bits MB at a time, so every gather of a pass is independent
+// of the others; a wave prefix sum places the records. Bitmap words are read through L2 (sc1):
+// merges set bits with atomics. RECV = IssueAsReceiver (disseminator.go:156-199): drop entries from
+// (sender, sinc), bump the rest (p++, delete at maxP). Otherwise IssueAsSender
+// (disseminator.go:128-133,201-215). Records are in member order within a lane's range; the order of
+// a message does not matter (its changes are distinct members).
 template <bool RECV>
 __device__ uint32_t wave_issue_t(const DS &d, uint32_t ol, uint32_t sender, uint32_t sinc, MsgDesc &out) {
     const uint32_t cnt = (uint32_t)d.dcnt[ol];
@@ -264,48 +281,73 @@ __device__ uint32_t wave_issue_t(const DS &d, uint32_t ol, uint32_t sender, uint
     if (off == ~0ull) return 0;
     const int maxp = RECV ? d.maxp[ol] : 0;
     const size_t rb = (size_t)ol * d.NP;
-    unsigned long long *bw = d.dblk + (size_t)ol * d.NBW;
+    uint32_t *bits = d.dbit + (size_t)ol * d.NBIT;
     uint32_t pos = 0;
     int del = 0;
-    for (uint32_t w = 0; w < d.NBW; w++) {
-        unsigned long long bits = bw[w];
-        while (bits) {
-            uint32_t blk[MB], p[MB];
+    for (uint32_t q0 = 0; q0 < d.NBIT; q0 += 256) {
+        const uint32_t q = q0 + lane_id() * 4;
+        unsigned long long lo = 0, hi = 0;                       // the lane's 128 presence bits
+        if (q < d.NBIT) {
+            const uint32_t *bp = bits + q;
+            const uint32_t w0 = __hip_atomic_load(bp + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t w1 = __hip_atomic_load(bp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t w2 = __hip_atomic_load(bp + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t w3 = __hip_atomic_load(bp + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            lo = ((unsigned long long)w1 << 32) | w0;
+            hi = ((unsigned long long)w3 << 32) | w2;
+        }
+        const uint32_t mbase = q * 32;
+        unsigned long long dlo = 0, dhi = 0;                     // deleted entries (RECV)
+        while (__any(lo != 0 || hi != 0)) {
+            uint32_t m[MB];
 #pragma unroll
             for (int k = 0; k < MB; k++) {
-                blk[k] = bits ? (uint32_t)(__ffsll((long long)bits) - 1) : 64u;
-                bits &= bits ? bits - 1 : 0ull;
+                if (lo) { m[k] = mbase + (uint32_t)(__ffsll((long long)lo) - 1); lo &= lo - 1; }
+                else if (hi) { m[k] = mbase + 64 + (uint32_t)(__ffsll((long long)hi) - 1); hi &= hi - 1; }
+                else m[k] = 0xFFFFFFFFu;
             }
-#pragma unroll
-            for (int k = 0; k < MB; k++) p[k] = blk[k] < 64u ? d.dp[rb + ((w * 64 + blk[k]) << 6) + lane_id()] : DP_NONE;
-            uint4 a[MB];
-            uint32_t wv[MB];
+            uint32_t p[MB], wv[MB];
+            uint2 sr[MB];
 #pragma unroll
             for (int k = 0; k < MB; k++) {
-                const uint32_t m = ((w * 64 + blk[k]) << 6) + lane_id();
-                a[k] = p[k] != DP_NONE ? d.aux[rb + m] : make_uint4(0, 0, 0, 0);
-                wv[k] = p[k] != DP_NONE ? d.mw[rb + m] : 0u;
+                const bool v = m[k] != 0xFFFFFFFFu;
+                p[k] = (RECV && v) ? d.dp[rb + m[k]] : 0u;
+                sr[k] = v ? d.dsrc[rb + m[k]] : make_uint2(0, 0);
+                wv[k] = v ? d.mw[rb + m[k]] : 0u;
             }
+            bool keep[MB];
+            uint32_t nk = 0;
 #pragma unroll
             for (int k = 0; k < MB; k++) {
-                if (blk[k] == 64u) continue;
-                const uint32_t m = ((w * 64 + blk[k]) << 6) + lane_id();
-                const bool present = p[k] != DP_NONE;
-                const bool keep = present && !(RECV && a[k].x == sender && a[k].y == sinc);   // filterChangesFromSender
-                const unsigned long long kmask = __ballot(keep);
-                bool remain = present;
-                if (keep) {
-                    const uint32_t rank = __popcll(kmask & lanemask_lt());
-                    const uint32_t st = (wv[k] & 7u) == ST_UNKNOWN ? ST_TOMB : (wv[k] & 7u);   // evicted: (tombstone, inc)
-                    if (pos + rank < cnt) d.pool[off + pos + rank] = make_uint4(m | (st << 24), wv[k] >> 3, a[k].x, a[k].y);
-                    if (RECV) {                                                   // bump
-                        if ((int)(p[k] + 1) >= maxp) { d.dp[rb + m] = DP_NONE; del++; remain = false; }
-                        else d.dp[rb + m] = (uint8_t)(p[k] + 1);
+                keep[k] = m[k] != 0xFFFFFFFFu && !(RECV && sr[k].x == sender && sr[k].y == sinc);   // filterChangesFromSender
+                nk += keep[k] ? 1u : 0u;
+            }
+            uint32_t tot;
+            uint32_t at = pos + wscan_excl(nk, tot);
+#pragma unroll
+            for (int k = 0; k < MB; k++) {
+                if (!keep[k]) continue;
+                const uint32_t st = (wv[k] & 7u) == ST_UNKNOWN ? ST_TOMB : (wv[k] & 7u);   // evicted: (tombstone, inc)
+                if (at < cnt) d.pool[off + at] = make_uint4(m[k] | (st << 24), wv[k] >> 3, sr[k].x, sr[k].y);
+                at++;
+                if (RECV) {                                                   // bump
+                    if ((int)(p[k] + 1) >= maxp) {
+                        d.dp[rb + m[k]] = DP_NONE;
+                        const uint32_t l = m[k] - mbase;
+                        if (l < 64) dlo |= 1ull << l; else dhi |= 1ull << (l - 64);
+                        del++;
+                    } else {
+                        d.dp[rb + m[k]] = (uint8_t)(p[k] + 1);
                     }
                 }
-                pos += __popcll(kmask);
-                if (!__ballot(remain) && lane_id() == 0) bw[w] &= ~(1ull << blk[k]);
             }
+            pos += tot;
+        }
+        if (RECV && (dlo | dhi)) {                               // the lane's own words
+            if (dlo & 0xFFFFFFFFull) atomicAnd(bits + q + 0, ~(uint32_t)dlo);
+            if (dlo >> 32) atomicAnd(bits + q + 1, ~(uint32_t)(dlo >> 32));
+            if (dhi & 0xFFFFFFFFull) atomicAnd(bits + q + 2, ~(uint32_t)dhi);
+            if (dhi >> 32) atomicAnd(bits + q + 3, ~(uint32_t)(dhi >> 32));
         }
     }
     if (RECV) {
@@ -373,10 +415,11 @@ __global__ void k_init_rows(DS d, int mode, uint32_t e0) {
         d.mw[idx] = w;
         d.dp[idx] = DP_NONE;
         d.tst[idx] = 0;
-        d.aux[idx] = make_uint4(0, 0, NO_DEADLINE, 0);
+        d.dsrc[idx] = make_uint2(0, 0);
+        d.tmr[idx] = make_uint2(NO_DEADLINE, 0);
     }
     for (uint32_t b = lane_id(); b < d.NB; b += 64) d.tblk[(size_t)ol * d.NB + b] = NO_DEADLINE;
-    for (uint32_t b = lane_id(); b < d.NBW; b += 64) d.dblk[(size_t)ol * d.NBW + b] = 0;
+    for (uint32_t b = lane_id(); b < d.NBIT; b += 64) d.dbit[(size_t)ol * d.NBIT + b] = 0;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) fp += __shfl_xor(fp, off, 64);
     if (lane_id() == 0) {
@@ -424,7 +467,7 @@ __global__ void k_recount(DS d, uint32_t ol) {
 
 __global__ void k_clear_changes(DS d, uint32_t ol) {
     for (uint32_t m = threadIdx.x; m < d.NP; m += blockDim.x) d.dp[(size_t)ol * d.NP + m] = DP_NONE;
-    for (uint32_t b = threadIdx.x; b < d.NBW; b += blockDim.x) d.dblk[(size_t)ol * d.NBW + b] = 0;
+    for (uint32_t b = threadIdx.x; b < d.NBIT; b += blockDim.x) d.dbit[(size_t)ol * d.NBIT + b] = 0;
     if (threadIdx.x == 0) d.dcnt[ol] = 0;
 }
 
@@ -496,12 +539,12 @@ __global__ void k_timers(DS d, uint32_t r) {
             const size_t idx = (size_t)ol * d.NP + m;
             const uint8_t ts = d.tst[idx];
             const uint32_t state = ts & 7u;
-            uint4 a = d.aux[idx];
-            if (state && !(ts & 0x80) && a.z <= r) {
+            uint2 a = d.tmr[idx];
+            if (state && !(ts & 0x80) && a.x <= r) {
                 d.tst[idx] = ts | 0x80;                             // fired; the entry stays
                 fired++;
-                if (state == ST_SUSPECT) merge_change(d, ol, o, m, ST_FAULTY, a.w, o, self_e, r, a.z, acc);   // MakeFaulty
-                else if (state == ST_FAULTY) merge_change(d, ol, o, m, ST_TOMB, a.w, o, self_e, r, a.z, acc); // MakeTombstone
+                if (state == ST_SUSPECT) merge_change(d, ol, o, m, ST_FAULTY, a.y, o, self_e, r, a.x, acc);   // MakeFaulty
+                else if (state == ST_FAULTY) merge_change(d, ol, o, m, ST_TOMB, a.y, o, self_e, r, a.x, acc); // MakeTombstone
                 else {                                              // Evict (memberlist.go:271-279)
                     const uint32_t w = d.mw[idx];
                     if ((w & 7u) != ST_UNKNOWN && m != o) {
@@ -512,10 +555,10 @@ __global__ void k_timers(DS d, uint32_t r) {
                         acc.evict++;
                     }
                 }
-                a = d.aux[idx];
+                a = d.tmr[idx];
             }
             const uint8_t ts2 = d.tst[idx];
-            const uint32_t v = ((ts2 & 7u) && !(ts2 & 0x80)) ? a.z : NO_DEADLINE;
+            const uint32_t v = ((ts2 & 7u) && !(ts2 & 0x80)) ? a.x : NO_DEADLINE;
             const uint32_t bmin = wmin(v);
             if (lane_id() == 0) d.tblk[(size_t)ol * d.NB + b] = bmin;
             newmin = min(newmin, bmin);
@@ -1125,15 +1168,16 @@ __global__ void k_digest(DS d, unsigned long long *out, uint32_t period_div) {
         const uint32_t w = d.mw[idx];
         r += mix4(o, m, w & 7u, w >> 3);
         const uint8_t p = d.dp[idx];
-        const uint4 a = d.aux[idx];
         if (p != DP_NONE) {
+            const uint2 a = d.dsrc[idx];
             const uint64_t se = a.x == SRC_NONE ? 0ull : (uint64_t)a.y;
             dd += mix4((uint64_t)o | (1ull << 40), m, (uint64_t)p | ((uint64_t)(uint32_t)(a.x + 1u) << 8), se);
         }
         const uint8_t ts = d.tst[idx];
         if (ts & 7u) {
+            const uint2 a = d.tmr[idx];
             const uint64_t state = ts & 7u, fired = (ts >> 7) & 1u;
-            t += mix4((uint64_t)o | (2ull << 40), m, state | (fired << 4) | ((uint64_t)a.z << 8), a.w);
+            t += mix4((uint64_t)o | (2ull << 40), m, state | (fired << 4) | ((uint64_t)a.x << 8), a.y);
         }
     }
 #pragma unroll
