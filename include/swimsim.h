@@ -172,6 +172,21 @@ int swimsim_comm_unique_id(uint8_t *out, size_t cap);   /* returns the id length
 int swimsim_comm_attach(swimsim_t *h, uint32_t nranks, uint32_t rank, const uint8_t *id, size_t len);
 int swimsim_shard_info(swimsim_t *h, uint32_t *nshards, uint32_t *rank, uint32_t *lo, uint32_t *hi,
                        uint64_t *exchanged_bytes, uint64_t *exchanges);
+/* one process per shard with a caller-supplied host transport (any process group: a test harness
+ * over gloo, an MPI job, ...). The library stages the packed parcels through host memory and calls:
+ *   alltoall_u64: k values to every shard; recv[s*k + i] = shard s's send[rank*k + i]
+ *   alltoallv:    segment p of sbuf ([soff[p], soff[p] + sbytes[p])) goes to shard p; the segment
+ *                 from shard s lands at rbuf + roff[s] (rbytes[s] bytes, known from a prior alltoall_u64)
+ *   bcast:        bytes of shard root to every shard
+ * Each returns 0 on success. Same collective call order as the RCCL transport. */
+typedef struct swimsim_host_transport {
+    void *ctx;
+    int (*alltoall_u64)(void *ctx, const uint64_t *send, uint64_t *recv, int32_t k);
+    int (*alltoallv)(void *ctx, const uint8_t *sbuf, const uint64_t *soff, const uint64_t *sbytes, uint8_t *rbuf,
+                     const uint64_t *roff, const uint64_t *rbytes);
+    int (*bcast)(void *ctx, void *buf, size_t bytes, uint32_t root);
+} swimsim_host_transport;
+int swimsim_comm_attach_host(swimsim_t *h, uint32_t nranks, uint32_t rank, const swimsim_host_transport *t);
 
 #ifdef __cplusplus
 }

@@ -173,6 +173,43 @@ struct RcclPort : Transport {
     }
 };
 
+// one process per shard, caller-supplied host collectives (swimsim_host_transport): parcels are
+// staged through pinned host memory
+struct HostPort : Transport {
+    swimsim_host_transport t{};
+    uint8_t *hs = nullptr, *hr = nullptr;
+    size_t hs_cap = 0, hr_cap = 0;
+    const char *name() const override { return "host"; }
+    ~HostPort() override {
+        if (hs) hipHostFree(hs);
+        if (hr) hipHostFree(hr);
+    }
+    static int grow(uint8_t **p, size_t *cap, size_t bytes) {
+        if (bytes <= *cap) return 0;
+        if (*p) hipHostFree(*p);
+        *cap = std::max<size_t>(bytes + bytes / 2, 1 << 16);
+        return hipHostMalloc((void **)p, *cap, 0) == hipSuccess ? 0 : SWIMSIM_ENOMEM;
+    }
+    int sizes(const uint64_t *send, uint64_t *recv, int k) override {
+        return t.alltoall_u64(t.ctx, send, recv, k) ? SWIMSIM_EHIP : 0;
+    }
+    int data(const uint8_t *sbuf, const uint64_t *soff, const uint64_t *sbytes, uint8_t *rbuf, const uint64_t *roff,
+             const uint64_t *rbytes, hipStream_t st) override {
+        size_t stot = 0, rtot = 0;
+        for (uint32_t p = 0; p < G; p++) {
+            stot = std::max<size_t>(stot, soff[p] + sbytes[p]);
+            rtot = std::max<size_t>(rtot, roff[p] + rbytes[p]);
+        }
+        if (grow(&hs, &hs_cap, stot) || grow(&hr, &hr_cap, rtot)) return SWIMSIM_ENOMEM;
+        if (stot && hipMemcpyAsync(hs, sbuf, stot, hipMemcpyDeviceToHost, st) != hipSuccess) return SWIMSIM_EHIP;
+        if (hipStreamSynchronize(st) != hipSuccess) return SWIMSIM_EHIP;
+        if (t.alltoallv(t.ctx, hs, soff, sbytes, hr, roff, rbytes)) return SWIMSIM_EHIP;
+        if (rtot && hipMemcpyAsync(rbuf, hr, rtot, hipMemcpyHostToDevice, st) != hipSuccess) return SWIMSIM_EHIP;
+        return hipStreamSynchronize(st) == hipSuccess ? 0 : SWIMSIM_EHIP;
+    }
+    int bcast(void *buf, size_t bytes, uint32_t root) override { return t.bcast(t.ctx, buf, bytes, root) ? SWIMSIM_EHIP : 0; }
+};
+
 }  // namespace
 
 struct swimsim {
@@ -1628,6 +1665,18 @@ int swimsim_comm_attach(swimsim_t *h, uint32_t nranks, uint32_t rank, const uint
     HIPCHK(h, hipSetDevice(h->device));
     const ncclResult_t nr = ncclCommInitRank(&port->comm, (int)nranks, uid, (int)rank);
     if (nr != ncclSuccess) return h->fail(SWIMSIM_EHIP, "ncclCommInitRank: %s", ncclGetErrorString(nr));
+    h->xp = std::move(port);
+    return SWIMSIM_OK;
+}
+
+int swimsim_comm_attach_host(swimsim_t *h, uint32_t nranks, uint32_t rank, const swimsim_host_transport *t) {
+    if (!h || !t || !t->alltoall_u64 || !t->alltoallv || !t->bcast || rank >= nranks || h->G != 1) return SWIMSIM_EINVAL;
+    const std::vector<uint32_t> lo = canonical_split(h->N, nranks);
+    if (int rc = set_shards(h, nranks, rank, lo)) return rc;
+    auto port = std::make_unique<HostPort>();
+    port->G = nranks;
+    port->rank = rank;
+    port->t = *t;
     h->xp = std::move(port);
     return SWIMSIM_OK;
 }

@@ -55,6 +55,17 @@ class Event(C.Structure):
     _fields_ = [("round", C.c_uint32), ("kind", C.c_uint32), ("a", C.c_int32), ("b", C.c_int32)]
 
 
+_U64P = C.POINTER(C.c_uint64)
+ALLTOALL_U64 = C.CFUNCTYPE(C.c_int, C.c_void_p, _U64P, _U64P, C.c_int32)
+ALLTOALLV = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, _U64P, _U64P, C.c_void_p, _U64P, _U64P)
+BCAST = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32)
+
+
+class HostTransport(C.Structure):
+    """swimsim_host_transport (include/swimsim.h): host collectives for one-process-per-shard runs"""
+    _fields_ = [("ctx", C.c_void_p), ("alltoall_u64", ALLTOALL_U64), ("alltoallv", ALLTOALLV), ("bcast", BCAST)]
+
+
 _lib = None
 
 
@@ -105,6 +116,7 @@ def load_library(path: str = LIB_PATH):
         "swimsim_comm_attach": (C.c_int, [P, u32, u32, P, sz]),
         "swimsim_shard_info": (C.c_int, [P, C.POINTER(u32), C.POINTER(u32), C.POINTER(u32), C.POINTER(u32),
                                          C.POINTER(u64), C.POINTER(u64)]),
+        "swimsim_comm_attach_host": (C.c_int, [P, u32, u32, C.POINTER(HostTransport)]),
     }
     for name, (res, args) in sigs.items():
         f = getattr(L, name)
@@ -163,7 +175,8 @@ class Cluster:
                  tombstone_ms=60_000, ping_request_size=3, max_rfs_jobs=5, p_factor=15, seed=1, addresses=None,
                  device=0, init="converged", max_rounds=0, message_pool_bytes=0, observer_range=None, comm=None):
         """comm = (nranks, rank, unique_id): attach this handle as shard `rank` of a cluster spread over
-        nranks processes (RCCL); observer_range then defaults to the canonical shard."""
+        nranks processes (RCCL); or comm = (nranks, rank, transport) with a swimsim.dist host transport
+        object (any process group). observer_range then defaults to the canonical shard."""
         L = load_library()
         self.n = n
         self.t0_ms, self.period_ms = t0_ms, period_ms
@@ -192,8 +205,12 @@ class Cluster:
         self.nl = (observer_range[1] - observer_range[0]) if observer_range else n
         if comm is not None:
             nranks, rank, uid = comm
-            idb = (C.c_uint8 * len(uid)).from_buffer_copy(uid)
-            self._chk(L.swimsim_comm_attach(self.h, nranks, rank, C.cast(idb, C.c_void_p), len(uid)))
+            if isinstance(uid, (bytes, bytearray)):
+                idb = (C.c_uint8 * len(uid)).from_buffer_copy(uid)
+                self._chk(L.swimsim_comm_attach(self.h, nranks, rank, C.cast(idb, C.c_void_p), len(uid)))
+            else:                                    # host transport: keep the callbacks alive with the handle
+                self._transport = uid
+                self._chk(L.swimsim_comm_attach_host(self.h, nranks, rank, C.byref(uid.c_struct())))
         if init == "converged":
             self._chk(L.swimsim_init_converged(self.h))
         elif init == "self":

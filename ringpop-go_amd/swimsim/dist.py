@@ -36,6 +36,65 @@ def sharded_cluster(n, group=None, **kw) -> Cluster:
     return Cluster(n, comm=(ws, rank, uid), **kw)
 
 
+class GlooTransport:
+    """swimsim_host_transport over a torch.distributed process group (e.g. gloo on CPU): lets one
+    process per shard run on any machine, e.g. several shards sharing one GPU in a test. Slow
+    (pickled all-gathers); the production path between GPUs is RCCL (sharded_cluster)."""
+
+    def __init__(self, group=None):
+        import ctypes as C
+        import torch.distributed as dist
+        from . import ALLTOALL_U64, ALLTOALLV, BCAST, HostTransport
+        self.C, self.dist, self.group = C, dist, group
+        self.ws, self.rank = dist.get_world_size(group), dist.get_rank(group)
+        self._cbs = (ALLTOALL_U64(self._alltoall_u64), ALLTOALLV(self._alltoallv), BCAST(self._bcast))
+        self._struct = HostTransport(None, *self._cbs)
+
+    def c_struct(self):
+        return self._struct
+
+    def _alltoall_u64(self, ctx, send, recv, k):
+        try:
+            ws, r = self.ws, self.rank
+            mine = np.ctypeslib.as_array(send, (ws * k,)).copy()
+            parts = [None] * ws
+            self.dist.all_gather_object(parts, mine, group=self.group)
+            out = np.ctypeslib.as_array(recv, (ws * k,))
+            for s in range(ws):
+                out[s * k:(s + 1) * k] = parts[s][r * k:(r + 1) * k]
+            return 0
+        except Exception:
+            return 1
+
+    def _alltoallv(self, ctx, sbuf, soff, sbytes, rbuf, roff, rbytes):
+        try:
+            C, ws, r = self.C, self.ws, self.rank
+            so, sb = np.ctypeslib.as_array(soff, (ws,)), np.ctypeslib.as_array(sbytes, (ws,))
+            ro, rb = np.ctypeslib.as_array(roff, (ws,)), np.ctypeslib.as_array(rbytes, (ws,))
+            segs = [C.string_at(sbuf + int(so[p]), int(sb[p])) if sb[p] else b"" for p in range(ws)]
+            parts = [None] * ws
+            self.dist.all_gather_object(parts, segs, group=self.group)
+            for s in range(ws):
+                data = parts[s][r]
+                if len(data) != int(rb[s]):
+                    return 1
+                if data:
+                    C.memmove(rbuf + int(ro[s]), data, len(data))
+            return 0
+        except Exception:
+            return 1
+
+    def _bcast(self, ctx, buf, nbytes, root):
+        try:
+            C = self.C
+            box = [C.string_at(buf, nbytes) if self.rank == root else None]
+            self.dist.broadcast_object_list(box, src=int(root), group=self.group)
+            C.memmove(buf, box[0], nbytes)
+            return 0
+        except Exception:
+            return 1
+
+
 def gather_rows(local: np.ndarray, group=None) -> np.ndarray:
     """per-observer arrays of every shard, concatenated in observer order"""
     import torch.distributed as dist
@@ -69,5 +128,5 @@ def max_over_ranks(x: float, group=None) -> float:
     return max(parts)
 
 
-__all__ = ["env", "broadcast_unique_id", "sharded_cluster", "gather_rows", "reduce_digest", "reduce_counters",
+__all__ = ["env", "broadcast_unique_id", "sharded_cluster", "GlooTransport", "gather_rows", "reduce_digest", "reduce_counters",
            "max_over_ranks", "shard_range"]
