@@ -5,14 +5,17 @@ Workload (BASELINE.json configs[2], the metric's "64k members"): 65,536 members,
 One "step" is one synchronous protocol round of every member (docs/ROUND_SEMANTICS.md §4).
 --warmup W rounds (default 10: rounds 0-9, steady state) run untimed. --steps K rounds (default
 90: rounds 10-99, the kill and both cascades) are timed between barrier+synchronize brackets.
-value = members x K x world_size / max-over-ranks time. With --gpus N>1 each rank simulates its own
-independent 65,536-member cluster (weak scaling, no data-path collective). Observer-row
-sharding of one cluster over several GPUs is future work.
+
+--gpus N > 1 (one process per GPU, launched by torch.distributed.run): the same 65,536-member
+cluster's observer rows are sharded over the N GPUs (rank r holds rows [N*r/G, N*(r+1)/G)) and every
+cross-shard message moves over RCCL point-to-point on xGMI inside libswimsim. Total work is fixed, so
+"scaling" is "strong". value = members x K / max-over-ranks time.
 
 The JSON line carries:
-  roofline     : for the kernel family with the most device time, its algorithmic bytes per launch /
-                 HIP-event-measured average launch time vs the 8 TB/s HBM peak.
-  cpu_baseline : the C oracle (single thread) on a bounded sample of the same protocol, rank 0 only.
+  roofline     : for the kernel family with the most device time (rank 0), its algorithmic bytes per
+                 launch / HIP-event-measured average launch time (events on the engine's stream) vs the
+                 8 TB/s HBM peak; merge_kernel_GBps is the same figure for the receive-merge family.
+  cpu_baseline : the C oracle (single thread) on a bounded sample of the same protocol, rank 0, N=1 only.
 """
 import argparse
 import json
@@ -67,18 +70,25 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--members", type=int, default=65536)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    # diagnostics: every rank on cuda:0, shards exchanging through the gloo host transport instead of
+    # RCCL (lets the multi-process path run on a one-GPU machine); never used for reported numbers
+    ap.add_argument("--host-transport", action="store_true")
     args = ap.parse_args()
 
     ws, rank, local = dist_env()
     import torch
 
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs an MI355X (no GPU visible)")
+    if args.host_transport:
+        local = 0
+    torch.cuda.set_device(local)
     if ws > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
-    dev = local if torch.cuda.is_available() else 0
-    if torch.cuda.is_available():
-        torch.cuda.set_device(dev)
+        # launcher plumbing only (RCCL id broadcast, barriers, max-over-ranks time); the data path is
+        # libswimsim's own RCCL communicator
+        dist.init_process_group("gloo")
 
     import swimsim
     from swimsim import workloads as W
@@ -86,15 +96,22 @@ def main():
     n = args.members
     total_rounds = args.warmup + args.steps
     wl = W.config3(n=n, rounds=total_rounds)
-    eng = swimsim.Cluster(n, device=dev)
+    if ws > 1:
+        from swimsim import dist as sd
+
+        if args.host_transport:
+            eng = swimsim.Cluster(n, device=0, comm=(ws, rank, sd.GlooTransport()))
+        else:
+            eng = sd.sharded_cluster(n, device=local)
+    else:
+        eng = swimsim.Cluster(n, device=local)
 
     def barrier():
         if ws > 1:
             import torch.distributed as dist
 
             dist.barrier()
-        if torch.cuda.is_available():
-            torch.cuda.synchronize()
+        torch.cuda.synchronize()
 
     for r in range(args.warmup):
         eng.step(1, wl.events_for(r))
@@ -106,18 +123,17 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     if ws > 1:
-        import torch.distributed as dist
+        from swimsim import dist as sd
 
-        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{dev}" if torch.cuda.is_available() else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+        dt = sd.max_over_ranks(dt)
 
     kt = eng.kernel_times()
     counters = eng.counters()
+    shard = eng.shard_info()
     eng.enable_timing(False)
+    if ws > 1:
+        counters = sd.reduce_counters(counters)
     dominant = max(kt.items(), key=lambda kv: kv[1]["avg_ms"] * kv[1]["launches"])
-    # the roofline is reported for the dominant family when it moves algorithmic bytes; the
-    # merge family (recv_merge) is the north-star kernel and is reported alongside in DESIGN.md
     fam, info = dominant
     per_launch_bytes = info["alg_bytes"] / max(1, info["launches"])
     achieved = per_launch_bytes / (info["avg_ms"] * 1e-3) / 1e9 if info["avg_ms"] > 0 else 0.0
@@ -126,7 +142,7 @@ def main():
         if merge.get("avg_ms", 0) > 0 else 0.0
 
     if rank == 0:
-        value = n * args.steps * ws / dt
+        value = n * args.steps / dt
         line = {
             "metric": "simulated member-rounds/sec at 64k members",
             "value": round(value, 1),
@@ -136,12 +152,14 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(dt * 1e3 / args.steps, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "u32",
-            "data": "synthetic (converged 65,536-member cluster; 655 members killed at round 10; Philox seed 11)",
-            "config": {"workload": "config3_cascade: 65536 members, 1% killed at r=10, rounds 10-99 timed",
-                       "members": n, "rounds_timed": args.steps, "parallelism": f"replicas x{ws}" if ws > 1 else "1 GPU"},
+            "data": f"synthetic (converged {n}-member cluster; {max(1, n // 100)} members killed at round 10; Philox seed 11)",
+            "config": {"workload": f"config3_cascade: {n} members, 1% killed at r={args.warmup}, rounds {args.warmup}-{total_rounds - 1} timed",
+                       "members": n, "rounds_timed": args.steps,
+                       "parallelism": (f"observer-row shards x{ws} over " + ("host transport (diagnostic)" if args.host_transport
+                                                                              else "RCCL")) if ws > 1 else "1 GPU"},
             "roofline": {"bound": "hbm", "kernel": fam, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": None,
                          "avg_launch_ms": round(info["avg_ms"], 5), "launches": info["launches"],
@@ -149,12 +167,15 @@ def main():
             "kernel_ms": {k: round(v["avg_ms"] * v["launches"], 3) for k, v in kt.items()},
             "counters": counters,
         }
-        if not args.no_cpu_baseline:
+        if ws > 1:
+            line["exchange"] = {"bytes_rank0": shard["exchanged_bytes"], "exchanges_rank0": shard["exchanges"]}
+        if ws == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline()
-        print(json.dumps(line))
+        print(json.dumps(line), flush=True)
     if ws > 1:
         import torch.distributed as dist
 
+        dist.barrier()
         dist.destroy_process_group()
 
 

@@ -25,6 +25,12 @@ for mode in "$@"; do
       -- python3 bench.py --no-cpu-baseline > gpurun_out/prof.log 2>&1
     rc=$?; echo "rocprof rc=$rc" >> gpurun_out/prof.log; [ $rc -eq 0 ] || exit $rc
     ;;
+  bench2)
+    timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+      --master-port 29511 bench.py --gpus 2 --members 2048 --steps 30 --warmup 10 --host-transport \
+      > gpurun_out/bench2.json 2> gpurun_out/bench2.err
+    rc=$?; echo "bench2 rc=$rc" >> gpurun_out/bench2.err; [ $rc -eq 0 ] || exit $rc
+    ;;
   csbench)
     timeout -k 10 300 python -u tools_cs_bench.py 65536 64,1024,16384,65536 2 > gpurun_out/csbench.json 2> gpurun_out/csbench.err
     rc=$?; echo "csbench rc=$rc" >> gpurun_out/csbench.err; [ $rc -eq 0 ] || exit $rc
