@@ -252,6 +252,8 @@ struct swimsim {
     MsgDesc *sdesc = nullptr, *rdesc = nullptr, *sdesc2 = nullptr, *rdesc2 = nullptr, *snapdesc = nullptr, *hdesc = nullptr;
     uint32_t *sI = nullptr, *sC = nullptr, *sI2 = nullptr, *sC2 = nullptr;
     uint32_t *sS = nullptr, *sS2 = nullptr;       // lazy sender checksums: dense slot of the sender's row or none
+    uint32_t *rcs = nullptr, *csreqcnt = nullptr; // remote lazy sender checksums (sharded)
+    uint4 *csreq = nullptr;
     uint32_t *fpv = nullptr, *fpv_s = nullptr, *fph = nullptr, *fph_s = nullptr, *fplist = nullptr, *fpcnt = nullptr,
              *dup_of = nullptr;                   // checksum dedup (rows by fingerprint)
     uint8_t *hflag = nullptr;
@@ -494,6 +496,8 @@ XArgs xargs(swimsim *h) {
     x.need = h->need;
     x.keys = h->keys; x.npairs = h->npairs; x.keycap = h->keycap;
     x.needlist = h->needlist; x.needcnt = h->needcnt; x.needcap = h->needcap;
+    x.sS = h->sS; x.sS2 = h->sS2; x.rcs = h->rcs;
+    x.csreq = h->csreq; x.csreqcnt = h->csreqcnt; x.csreqcap = h->keycap;
     return x;
 }
 
@@ -614,20 +618,43 @@ int checksum_dirty(swimsim *h, int mode) {
 
 // run the receive waves over a sorted inbox (phase D when phase==0, phase Q2 when phase==1), then
 // resolve the deferred full-sync decisions with one batched checksum of the receivers' snapshots
-void resolve_deferred(swimsim *h, int phase, MsgDesc *rdesc, uint32_t maxn) {
+// resolve the deferred full-sync decisions: one batched checksum of the snapshots they wait on (dirty
+// receivers, local pending senders and, when sharded, the pending senders other shards ask this
+// shard about). Sharded phases D and Q2 are collective: two exchanges carry the requests and answers.
+int resolve_deferred(swimsim *h, int phase, MsgDesc *rdesc, uint32_t maxn) {
+    const bool remote = h->G > 1 && phase != 2;
+    uint32_t maxlist = 2 * maxn;
     {
         Scope sc(h, F_CHECKSUM);
-        hipMemsetAsync(h->cnt, 0, 4, h->s);
+        HIPCHK(h, hipMemsetAsync(h->cnt, 0, 4, h->s));
         hipLaunchKernelGGL(k_defer_ids, dim3(blocks_for_threads(maxn)), dim3(256), 0, h->s, h->d, h->defer,
                            h->defer_cnt, h->list, h->cnt);
-        launch_checksum(h->d, h->list, h->cnt, 2 * maxn, h->fast_cs, h->s);
+    }
+    if (remote) {
+        HIPCHK(h, hipMemsetAsync(h->csreqcnt, 0, 4, h->s));
+        hipLaunchKernelGGL(k_x_csreq, dim3(blocks_for_threads(maxn)), dim3(256), 0, h->s, h->d, h->defer, h->defer_cnt,
+                           phase, h->xitems, h->xcnt, h->xcap);
+        if (int rc = xchg(h)) return rc;
+        hipLaunchKernelGGL(k_csreq_ids, dim3(blocks_for_threads(h->keycap)), dim3(256), 0, h->s, h->d, h->csreq,
+                           h->csreqcnt, h->list, h->cnt);
+        maxlist += h->keycap;
+    }
+    {
+        Scope sc(h, F_CHECKSUM);
+        launch_checksum(h->d, h->list, h->cnt, maxlist, h->fast_cs, h->s);
+    }
+    if (remote) {
+        hipLaunchKernelGGL(k_x_csresp, dim3(blocks_for_threads(h->keycap)), dim3(256), 0, h->s, h->d, h->csreq,
+                           h->csreqcnt, h->xitems, h->xcnt, h->xcap);
+        if (int rc = xchg(h)) return rc;
     }
     Scope sc(h, phase == 1 ? F_PINGREQ : F_RECV);
     hipLaunchKernelGGL(k_recv_finish, dim3(blocks_for_threads(maxn)), dim3(256), 0, h->s, h->d, h->defer,
-                       h->defer_cnt, rdesc, phase, h->fsflag);
+                       h->defer_cnt, rdesc, phase, h->fsflag, h->rcs);
+    return 0;
 }
 
-void run_waves(swimsim *h, int phase, uint32_t nruns_valid, uint32_t maxcount) {
+int run_waves(swimsim *h, int phase, uint32_t nruns_valid, uint32_t maxcount) {
     RecvArgs a{};
     a.ukeys = h->ukeys; a.counts = h->counts; a.offs = h->offs; a.vals = h->vals_out;
     a.nruns_max = nruns_valid;
@@ -635,7 +662,7 @@ void run_waves(swimsim *h, int phase, uint32_t nruns_valid, uint32_t maxcount) {
     a.sdesc = phase == 0 ? h->sdesc : h->sdesc2;
     a.sI = phase == 0 ? h->sI : h->sI2;
     a.sC = phase == 0 ? h->sC : h->sC2;
-    a.sS = h->G == 1 ? (phase == 0 ? h->sS : h->sS2) : nullptr;
+    a.sS = phase == 0 ? h->sS : h->sS2;
     a.rdesc = phase == 0 ? h->rdesc : h->rdesc2;
     a.defer = h->defer;
     a.defer_cnt = h->defer_cnt;
@@ -647,12 +674,13 @@ void run_waves(swimsim *h, int phase, uint32_t nruns_valid, uint32_t maxcount) {
         hipLaunchKernelGGL(k_recv, dim3(blocks_for_waves(nruns_valid)), dim3(256), 0, h->s, h->d, a);
     }
     const uint32_t maxdefer = std::min<uint64_t>((uint64_t)nruns_valid * maxcount, h->d.dense_cap);
-    resolve_deferred(h, phase, a.rdesc, maxdefer);
+    if (int rc = resolve_deferred(h, phase, a.rdesc, maxdefer)) return rc;
     if (phase == 0) {
         Scope sc(h, F_RECV);
         hipLaunchKernelGGL(k_build_jobs, dim3(blocks_for_threads(nruns_valid)), dim3(256), 0, h->s, h->d, h->ukeys,
                            h->counts, h->offs, h->vals_out, nruns_valid, h->fsflag);
     }
+    return 0;
 }
 
 int flush_events(swimsim *h, std::vector<uint4> &evs) {
@@ -709,7 +737,7 @@ int ping_with(swimsim *h, uint32_t o, uint32_t t, int slot) {
         hipMemsetAsync(h->defer_cnt, 0, 4, h->s);
         hipLaunchKernelGGL(k_ping_with, dim3(1), dim3(64), 0, h->s, h->d, t - h->lo, o, md, sics, h->hdesc + 8,
                            h->defer, h->defer_cnt, h->round);
-        resolve_deferred(h, 2, h->hdesc + 9, 1);
+        if (int rc = resolve_deferred(h, 2, h->hdesc + 9, 1)) return rc;
     }
     return 0;
 }
@@ -860,17 +888,15 @@ int step_one(swimsim *h, const swimsim_event *ev, size_t nev) {
                            h->exh_cnt);
         hipLaunchKernelGGL(k_select_exhaust, dim3(64), dim3(64), 0, h->s, h->d, h->exh_list, h->exh_cnt, h->scratch);
     }
-    // ---- I: issue (ping requests). One shard: C_o of dirty senders is lazy (k_issue). Shards: computed
-    //      here, since the value travels with the request to another shard. ----
-    const bool lazy = !sharded;
-    if (!lazy) checksum_dirty(h, 1);
+    // ---- I: issue (ping requests). C_o of a dirty sender is lazy (k_issue snapshots the row; it is
+    //      hashed only if a receiver, on any shard, compares it) ----
     uint32_t *hi = h->hinfo;
     uint32_t ninbox = h->NL;
     HIPCHK(h, hipMemsetAsync(h->d.dense_cur, 0, 4, h->s));         // dense snapshots live from here through R
     {
         Scope sc(h, F_ISSUE);
         hipLaunchKernelGGL(k_issue, dim3(blocks_for_waves(h->NL)), dim3(256), 0, h->s, h->d, 0, h->tgt, h->failed,
-                           h->sdesc, h->sI, h->sC, lazy ? h->sS : nullptr);
+                           h->sdesc, h->sI, h->sC, h->sS);
         HIPCHK(h, hipMemsetAsync(h->info + 2, 0, 4, h->s));
         hipLaunchKernelGGL(k_pairs_direct, dim3(blocks_for_threads(h->NL)), dim3(256), 0, h->s, h->d, h->tgt, h->keys,
                            h->failed, h->info, h->xitems, h->xcnt, h->xcap);
@@ -886,7 +912,7 @@ int step_one(swimsim *h, const swimsim_event *ev, size_t nev) {
     if (sharded) ninbox = std::min(hi[5], h->keycap);
     const uint32_t nfailed = hi[4];
     if (int rc = sort_inbox(h, ninbox, hi)) return rc;
-    run_waves(h, 0, hi[0], hi[1]);
+    if (int rc = run_waves(h, 0, hi[0], hi[1])) return rc;
     if (sharded) {                                                   // responses to senders on other shards
         hipLaunchKernelGGL(k_x_resp, dim3(blocks_for_threads(ninbox)), dim3(256), 0, h->s, h->d, h->keys, ninbox, 0,
                            h->xitems, h->xcnt, h->xcap);
@@ -907,12 +933,11 @@ int step_one(swimsim *h, const swimsim_event *ev, size_t nev) {
             hipLaunchKernelGGL(k_helpers, dim3(blocks_for_threads(h->NL)), dim3(256), 0, h->s, h->d, h->tgt, h->failed,
                                h->H, h->nh, r);
         }
-        if (!lazy) checksum_dirty(h, 2);
         HIPCHK(h, hipMemsetAsync(h->d.dense_cur, 0, 4, h->s));     // dense snapshots live from here through Q3
         {
             Scope sc(h, F_PINGREQ);
             hipLaunchKernelGGL(k_issue, dim3(blocks_for_waves(h->NL)), dim3(256), 0, h->s, h->d, 1, h->tgt, h->failed,
-                               h->sdesc2, h->sI2, h->sC2, lazy ? h->sS2 : nullptr);
+                               h->sdesc2, h->sI2, h->sC2, h->sS2);
             hipLaunchKernelGGL(k_pairs_helpers, dim3(blocks_for_threads(h->NL * h->K)), dim3(256), 0, h->s, h->d,
                                h->failed, h->H, h->nh, h->keys, h->xitems, h->xcnt, h->xcap);
         }
@@ -925,7 +950,7 @@ int step_one(swimsim *h, const swimsim_event *ev, size_t nev) {
             ninbox2 = std::min(hi[5], h->keycap);
         }
         if (int rc = sort_inbox(h, ninbox2, hi)) return rc;
-        run_waves(h, 1, hi[0], hi[1]);
+        if (int rc = run_waves(h, 1, hi[0], hi[1])) return rc;
         if (sharded) {
             hipLaunchKernelGGL(k_x_resp, dim3(blocks_for_threads(ninbox2)), dim3(256), 0, h->s, h->d, h->keys, ninbox2, 1,
                                h->xitems, h->xcnt, h->xcap);
@@ -1176,6 +1201,8 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
         (rc = dalloc(h, &h->sI, h->N, "sI")) || (rc = dalloc(h, &h->sC, h->N, "sC")) ||
         (rc = dalloc(h, &h->sI2, h->N, "sI2")) || (rc = dalloc(h, &h->sC2, h->N, "sC2")) ||
         (rc = dalloc(h, &h->sS, h->N, "sS")) || (rc = dalloc(h, &h->sS2, h->N, "sS2")) ||
+        (rc = dalloc(h, &h->rcs, h->N, "rcs")) || (rc = dalloc(h, &h->csreq, KC, "csreq")) ||
+        (rc = dalloc(h, &h->csreqcnt, 1, "csreqcnt")) ||
         (rc = dalloc(h, &h->fpv, h->NL, "fpv")) || (rc = dalloc(h, &h->fpv_s, h->NL, "fpv_s")) ||
         (rc = dalloc(h, &h->fph, h->NL, "fph")) || (rc = dalloc(h, &h->fph_s, h->NL, "fph_s")) ||
         (rc = dalloc(h, &h->fplist, h->NL, "fplist")) || (rc = dalloc(h, &h->fpcnt, 1, "fpcnt")) ||
@@ -1185,7 +1212,7 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
         (rc = dalloc(h, &h->keys_in, KC, "receivers")) || (rc = dalloc(h, &h->vals_out, KC, "vals_out")) ||
         (rc = dalloc(h, &h->ukeys, KC, "ukeys")) || (rc = dalloc(h, &h->counts, KC, "counts")) ||
         (rc = dalloc(h, &h->offs, KC, "offs")) || (rc = dalloc(h, &h->nruns, 1, "nruns")) ||
-        (rc = dalloc(h, &h->info, 8, "info")) || (rc = dalloc(h, &h->list, 2 * KC + 2 * (size_t)h->NL + 64, "list")) ||
+        (rc = dalloc(h, &h->info, 8, "info")) || (rc = dalloc(h, &h->list, 3 * KC + 2 * (size_t)h->NL + 64, "list")) ||
         (rc = dalloc(h, &h->cnt, 1, "cnt")) || (rc = dalloc(h, &h->defer, KC + 2 * (size_t)h->NL + 64, "defer")) ||
         (rc = dalloc(h, &h->defer_cnt, 1, "defer_cnt")) || (rc = dalloc(h, &h->exh_list, h->NL, "exh_list")) ||
         (rc = dalloc(h, &h->exh_cnt, 1, "exh_cnt")) || (rc = dalloc(h, &h->scratch, (size_t)64 * (h->NP / 32), "scratch")) ||

@@ -875,12 +875,14 @@ __global__ void k_recv(DS d, RecvArgs a) {
 // resolve deferred full-sync decisions once the snapshot checksums exist (phase 2 = heal ping:
 // the job is queued at once; heal runs in phase E, before any phase-D job of the round)
 __global__ void k_recv_finish(DS d, const uint4 *defer, const uint32_t *defer_cnt, MsgDesc *rdesc, int phase,
-                              uint8_t *fsflag) {
+                              uint8_t *fsflag, const uint32_t *rcs) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= *defer_cnt) return;
     const uint4 e = defer[i];
     const uint32_t slot = e.y, pair = e.w & 0x7FFFFFFFu;
-    const uint32_t scs = (e.w & 0x80000000u) ? d.dense_cs[e.z] : e.z;
+    const uint32_t ri = e.x & 0x7FFFFFFFu, sender = phase == 1 ? ri / d.K : ri;
+    // pending C_o: local snapshot (hashed in this resolution) or remote (answered by its owner shard)
+    const uint32_t scs = !(e.w & 0x80000000u) ? e.z : (e.z & 0x80000000u) ? rcs[sender] : d.dense_cs[e.z];
     MsgDesc resp;
     resp.kind = 0; resp.len = 0; resp.off_lo = resp.off_hi = 0;
     if (d.dense_cs[slot] != scs) {
@@ -894,7 +896,7 @@ __global__ void k_recv_finish(DS d, const uint4 *defer, const uint32_t *defer_cn
             fsflag[pair] = 1;
         }
     }
-    rdesc[e.x & 0x7FFFFFFFu] = resp;
+    rdesc[ri] = resp;
     if (phase != 2) ctr_add(d, C_MSG_CHANGES, (unsigned long long)resp.len);
 }
 
@@ -905,7 +907,7 @@ __global__ void k_defer_ids(DS d, const uint4 *defer, const uint32_t *defer_cnt,
     if (i >= *defer_cnt) return;
     const uint4 e = defer[i];
     if (e.x & 0x80000000u) list[atomicAdd(cnt, 1u)] = d.NL + e.y;
-    if (e.w & 0x80000000u) list[atomicAdd(cnt, 1u)] = d.NL + e.z;
+    if ((e.w & 0x80000000u) && !(e.z & 0x80000000u)) list[atomicAdd(cnt, 1u)] = d.NL + e.z;   // local pending
 }
 
 // tryStartReverseFullSync (disseminator.go:257-278) in inbox order: at most maxjobs per receiver

@@ -21,7 +21,9 @@ enum ParcelType : uint32_t {
     P_NEED = 5,     // reverse-full-sync source request (idx = source row, key = requesting shard)
     P_SNAP = 6,     // reverse-full-sync source snapshot (idx = source row)
     P_HEALROW = 7,  // heal: target's membership for the healing observer
-    P_PING = 8      // heal: ping-with-changes to a remote target (idx target, key sender)
+    P_PING = 8,     // heal: ping-with-changes to a remote target (idx target, key sender)
+    P_CSREQ = 9,    // lazy C_o: checksum of sender idx's issue-time snapshot (key = its dense slot on the owner)
+    P_CSRESP = 10   // lazy C_o: the answer (idx = sender, key = checksum)
 };
 
 struct Parcel {                 // 64 bytes
@@ -45,6 +47,11 @@ struct XArgs {
     uint2 *needlist;              // (source row, requesting shard) of imported P_NEED
     uint32_t *needcnt;
     uint32_t needcap;
+    uint32_t *sS, *sS2;           // lazy sender checksums: local slot, 0x80000000|remote slot, or none
+    uint32_t *rcs;                // [N] checksums of remote senders' snapshots (P_CSRESP)
+    uint4 *csreq;                 // imported P_CSREQ: {sender, slot, requesting shard, 0}
+    uint32_t *csreqcnt;
+    uint32_t csreqcap;
 };
 
 __device__ __forceinline__ const MsgDesc *item_desc(const DS &d, const XArgs &x, uint4 it) {
@@ -101,9 +108,15 @@ __global__ void k_x_pack(DS d, XArgs x, const uint4 *items, const uint32_t *cnt,
         h.kind = md ? md->kind : 2u;
         h.len = md ? md->len : 0u;
         h.pbytes = pb;
-        if (it.y == P_REQ) { h.sI = x.sI[it.z]; h.sC = x.sC[it.z]; }
-        if (it.y == P_REQ2) { h.sI = x.sI2[it.z / d.K]; h.sC = x.sC2[it.z / d.K]; }
+        // a dirty sender's C_o travels as "pending" (sI bit 31) with its snapshot slot on this shard
+        if (it.y == P_REQ || it.y == P_REQ2) {
+            const uint32_t o = it.y == P_REQ ? it.z : it.z / d.K;
+            const uint32_t slot = (it.y == P_REQ ? x.sS : x.sS2)[o];
+            h.sI = (it.y == P_REQ ? x.sI : x.sI2)[o] | (slot != SRC_NONE ? 0x80000000u : 0u);
+            h.sC = slot != SRC_NONE ? slot : (it.y == P_REQ ? x.sC : x.sC2)[o];
+        }
         if (it.y == P_PING) { h.sI = x.hsics[0]; h.sC = x.hsics[1]; }
+        if (it.y == P_CSREQ) h.sI = d.rank;                        // requesting shard
         if (md && md->kind == 1) {
             const uint32_t slot = md->off_lo;
             h.meta = d.dense_meta[slot];
@@ -164,8 +177,10 @@ __global__ void k_x_unpack(DS d, XArgs x, const uint8_t *buf, const ulonglong2 *
     switch (h.type) {
     case P_REQ:
     case P_REQ2: {
-        if (h.type == P_REQ) { x.sdesc[h.idx] = md; x.sI[h.idx] = h.sI; x.sC[h.idx] = h.sC; }
-        else { const uint32_t o = h.idx / d.K; x.sdesc2[o] = md; x.sI2[o] = h.sI; x.sC2[o] = h.sC; }
+        const uint32_t o = h.type == P_REQ ? h.idx : h.idx / d.K;
+        const uint32_t pend = (h.sI >> 31) ? (0x80000000u | h.sC) : SRC_NONE;
+        if (h.type == P_REQ) { x.sdesc[o] = md; x.sI[o] = h.sI & 0x7FFFFFFFu; x.sC[o] = h.sC; x.sS[o] = pend; }
+        else { x.sdesc2[o] = md; x.sI2[o] = h.sI & 0x7FFFFFFFu; x.sC2[o] = h.sC; x.sS2[o] = pend; }
         const uint32_t p = atomicAdd(x.npairs, 1u);
         if (p < x.keycap) x.keys[p] = ((unsigned long long)h.key << 32) | h.idx;
         else atomicOr(d.err, E_XCAP);
@@ -183,8 +198,42 @@ __global__ void k_x_unpack(DS d, XArgs x, const uint8_t *buf, const ulonglong2 *
     case P_SNAP: x.snapdesc[h.idx] = md; break;
     case P_HEALROW: x.hdesc[1] = md; break;
     case P_PING: x.hdesc[5] = md; x.hsics[2] = h.sI; x.hsics[3] = h.sC; break;
+    case P_CSREQ: {
+        const uint32_t p = atomicAdd(x.csreqcnt, 1u);
+        if (p < x.csreqcap) x.csreq[p] = make_uint4(h.idx, h.key, h.sI, 0);
+        else atomicOr(d.err, E_XCAP);
+        break;
+    }
+    case P_CSRESP: x.rcs[h.idx] = h.key; break;
     default: break;
     }
+}
+
+// deferred full-sync decisions waiting on a remote sender's lazy C_o: ask the owner shard
+__global__ void k_x_csreq(DS d, const uint4 *defer, const uint32_t *defer_cnt, int phase, uint4 *items, uint32_t *cnt,
+                          uint32_t cap) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= *defer_cnt) return;
+    const uint4 e = defer[i];
+    if (!(e.w & 0x80000000u) || !(e.z & 0x80000000u)) return;
+    const uint32_t ri = e.x & 0x7FFFFFFFu, o = phase == 0 ? ri : ri / d.K;
+    x_push(items, cnt, cap, d.err, make_uint4(owner_of(d, o), P_CSREQ, o, e.z & 0x7FFFFFFFu));
+}
+
+// requested snapshots → checksum list (after the local deferred ids)
+__global__ void k_csreq_ids(DS d, const uint4 *csreq, const uint32_t *csreqcnt, uint32_t *list, uint32_t *cnt) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= *csreqcnt) return;
+    list[atomicAdd(cnt, 1u)] = d.NL + csreq[i].y;
+}
+
+// answers to the requesting shards
+__global__ void k_x_csresp(DS d, const uint4 *csreq, const uint32_t *csreqcnt, uint4 *items, uint32_t *cnt,
+                           uint32_t cap) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= *csreqcnt) return;
+    const uint4 r = csreq[i];
+    x_push(items, cnt, cap, d.err, make_uint4(r.z, P_CSRESP, r.x, d.dense_cs[r.y]));
 }
 
 // responses of local receivers to remote senders (after the receive waves resolved them)
