@@ -27,6 +27,21 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "ringpop-go_amd"))
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+# kernel family (swimsim_kernel_times) -> kernel symbol in the rocprofv3 PMC summary
+FAMILY_KERNEL = {"checksum": "swimdev::k_checksum<19, 11, 9, 0>", "recv_merge": "swimdev::k_recv",
+                 "issue": "swimdev::k_issue", "resp_merge": "swimdev::k_resp", "timers": "swimdev::k_timers"}
+PMC_SUMMARY = os.path.join(REPO, "profiles", "r01_pmc_traffic.json")
+
+
+def pmc_traffic(family):
+    """HBM bytes per launch of the family's main kernel from the committed PMC pass of this bench
+    (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate runs; tools/pmc_summary.py), or None."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            t = json.load(f)[FAMILY_KERNEL[family]]
+        return round(t["fetch_bytes_per_launch"] + t["write_bytes_per_launch"], 1)
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 def dist_env():
@@ -161,7 +176,8 @@ def main():
                        "parallelism": (f"observer-row shards x{ws} over " + ("host transport (diagnostic)" if args.host_transport
                                                                               else "RCCL")) if ws > 1 else "1 GPU"},
             "roofline": {"bound": "hbm", "kernel": fam, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": None,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": pmc_traffic(fam),
+                         "traffic_unit": "bytes per launch (FETCH_SIZE + WRITE_SIZE, " + os.path.basename(PMC_SUMMARY) + ")",
                          "avg_launch_ms": round(info["avg_ms"], 5), "launches": info["launches"],
                          "merge_kernel_GBps": round(merge_gbps, 2)},
             "kernel_ms": {k: round(v["avg_ms"] * v["launches"], 3) for k, v in kt.items()},
