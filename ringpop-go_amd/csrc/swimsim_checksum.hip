@@ -94,7 +94,8 @@ __device__ __forceinline__ uint32_t fh_fold(uint32_t h, uint32_t mx, uint32_t ad
 // NO = ring words one record can touch (record of at most W + max tail bytes, shifted by <= 3).
 // Waves: 0 h chain, 1 g/f chain, 2 and 3 formatters.
 // MODE 0: normal; 1: hashers only (formatter skips its stores); 2: formatter only; 3: the g/f wave
-// also dumps every block it hashes to dbg (lane 0's row; diagnostics).
+// also dumps every block it hashes to dbg (lane 0's row; diagnostics); 4: barrier skeleton (no
+// loads, no hashing); 5: formatter loads and positions only. Modes 1, 2, 4, 5 time parts of the kernel.
 // JMIN = words every record fills completely (shortest record >> 2): their writes need no mask.
 template <int W, int NO, int JMIN, int MODE>
 __global__ void __launch_bounds__(256) k_checksum(DS d, const uint32_t *list, const uint32_t *count,
@@ -167,8 +168,10 @@ __global__ void __launch_bounds__(256) k_checksum(DS d, const uint32_t *list, co
             for (int u = 0; u < 4; u++) {
                 const int b = u & 1, nb_ = b ^ 1;
                 const uint32_t mb = sc * CS_SUP + u * CS_IT;
-                tails(u < 3 ? cur[u + 1] : pre[0], ta[nb_], tb[nb_]);   // next interval's tails and addresses
-                addrs(mb + CS_IT, A[nb_]);
+                if (MODE != 4) {
+                    tails(u < 3 ? cur[u + 1] : pre[0], ta[nb_], tb[nb_]);   // next interval's tails and addresses
+                    addrs(mb + CS_IT, A[nb_]);
+                }
                 const uint4 q4 = cur[u];
                 const uint32_t ws[4] = {q4.x, q4.y, q4.z, q4.w};
                 // positions of the interval's 4 records (a short prefix chain), then the own records'
@@ -178,7 +181,7 @@ __global__ void __launch_bounds__(256) k_checksum(DS d, const uint32_t *list, co
 #pragma unroll
                 for (int k = 0; k < CS_IT; k++) {
                     const uint32_t c6 = tb[b][k].z, c7 = tb[b][k].w;
-                    const uint32_t L = ((ws[k] & 7u) < 4u && mb + k < N) ? (c6 >> 24) : 0u;
+                    const uint32_t L = MODE == 4 ? 38u : ((ws[k] & 7u) < 4u && mb + k < N) ? (c6 >> 24) : 0u;
                     const uint32_t sh = pos & 3u;
                     Lk[k] = L; sk[k] = sh; pk[k] = phys; hk[k] = hc;
                     uint32_t np = phys + ((sh + L) >> 2);
@@ -216,7 +219,7 @@ __global__ void __launch_bounds__(256) k_checksum(DS d, const uint32_t *list, co
                         }
                     }
                 };
-                if (MODE != 1) {
+                if (MODE != 1 && MODE != 4 && MODE != 5) {
                     if (f == 0) emit(std::integral_constant<int, 0>{});
                     else emit(std::integral_constant<int, 1>{});
                 }
@@ -260,7 +263,8 @@ __global__ void __launch_bounds__(256) k_checksum(DS d, const uint32_t *list, co
     const uint32_t iters = ok ? (len - 1) / 20 : 0;
     const uint32_t *rb = ring + CS_PRE * CS_ROWS + lane;
     uint32_t done = 0, rq = 0;
-    // hash blocks [done, lim) in groups of 4: all loads of a group first, then the arithmetic with
+    // hash blocks [done, lim) in groups of 4: all loads of a group first, then the arithmetic. While
+    // every lane has a whole group left the groups run unpredicated; the last groups of a step use
     // branch-free predication (lanes have different limits)
     auto advance = [&](uint32_t lim) {
         const uint32_t n = done < lim ? min(lim - done, 4u) : 0u;
@@ -269,6 +273,21 @@ __global__ void __launch_bounds__(256) k_checksum(DS d, const uint32_t *list, co
         rq = rq >= CS_RING ? rq - CS_RING : rq;
     };
     auto run_h = [&](uint32_t lim) {
+        while (__all(done + 4 <= lim)) {                           // every lane has a whole group left
+            uint32_t a[4], dd[4], e[4];
+            uint32_t q = rq;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t *p = rb + q * CS_ROWS;
+                a[k] = p[0]; dd[k] = p[3 * CS_ROWS]; e[k] = p[4 * CS_ROWS];
+                q += 5;
+                q = q >= CS_RING ? q - CS_RING : q;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++) h = fh_fold(h + a[k], fh_m(dd[k]), e[k]);
+            done += 4;
+            rq = q;
+        }
         while (__any(done < lim)) {
             uint32_t a[4], dd[4], e[4];
             uint32_t q = rq;
@@ -288,6 +307,28 @@ __global__ void __launch_bounds__(256) k_checksum(DS d, const uint32_t *list, co
         }
     };
     auto run_gf = [&](uint32_t lim) {
+        if (MODE != 3)
+            while (__all(done + 4 <= lim)) {                       // every lane has a whole group left
+                uint32_t v[4][5];
+                uint32_t q = rq;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t *p = rb + q * CS_ROWS;
+#pragma unroll
+                    for (int i = 0; i < 5; i++) v[k][i] = p[i * CS_ROWS];
+                    q += 5;
+                    q = q >= CS_RING ? q - CS_RING : q;
+                }
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t a = v[k][0], b = v[k][1], c = v[k][2], dd = v[k][3], e = v[k][4];
+                    g = fh_fold(g + b, fh_m(c), a);
+                    f = fh_fold(f + c, fh_m(b + e * FH_C1), dd);
+                    f += g; g += f;
+                }
+                done += 4;
+                rq = q;
+            }
         while (__any(done < lim)) {
             uint32_t v[4][5];
             uint32_t q = rq;
@@ -317,18 +358,18 @@ __global__ void __launch_bounds__(256) k_checksum(DS d, const uint32_t *list, co
     uint32_t avail = 0;
     if (wave == 0) {
         for (uint32_t t = 0; t < nit; t++) {
-            if (MODE != 2) run_h(MODE == 1 ? min(iters, t * 8u) : min(iters, avail));
+            if (MODE < 2 || MODE == 3) run_h(MODE == 1 ? min(iters, t * 8u) : min(iters, avail));
             lds_barrier();
             avail = wp[t & 1][lane] / 20;
         }
-        if (MODE != 2) run_h(iters);
+        if (MODE < 2 || MODE == 3) run_h(iters);
     } else {
         for (uint32_t t = 0; t < nit; t++) {
-            if (MODE != 2) run_gf(MODE == 1 ? min(iters, t * 8u) : min(iters, avail));
+            if (MODE < 2 || MODE == 3) run_gf(MODE == 1 ? min(iters, t * 8u) : min(iters, avail));
             lds_barrier();
             avail = wp[t & 1][lane] / 20;
         }
-        if (MODE != 2) run_gf(iters);
+        if (MODE < 2 || MODE == 3) run_gf(iters);
     }
     if (wave == 1) { xgf[0][lane] = g; xgf[1][lane] = f; }
     lds_barrier();
@@ -384,5 +425,7 @@ void launch_checksum_mode(const DS &d, const uint32_t *list, const uint32_t *cou
     if (grid == 0 || d.W != 19) return;
     if (mode == 1) launch_cs_w<19, 1>(d, list, count, grid, s);
     else if (mode == 2) launch_cs_w<19, 2>(d, list, count, grid, s);
+    else if (mode == 4) launch_cs_w<19, 4>(d, list, count, grid, s);
+    else if (mode == 5) launch_cs_w<19, 5>(d, list, count, grid, s);
     else launch_cs_w<19, 0>(d, list, count, grid, s);
 }

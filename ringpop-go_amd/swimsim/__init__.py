@@ -21,7 +21,8 @@ from dataclasses import dataclass
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libswimsim.so")
+# SWIMSIM_LIB (diagnostics only): load another build of the library, e.g. a kernel variant under test
+LIB_PATH = os.environ.get("SWIMSIM_LIB") or os.path.join(_HERE, "libswimsim.so")
 
 ALIVE, SUSPECT, FAULTY, LEAVE, TOMBSTONE, UNKNOWN = 0, 1, 2, 3, 4, 7
 STATUS_NAMES = {ALIVE: "alive", SUSPECT: "suspect", FAULTY: "faulty", LEAVE: "leave", TOMBSTONE: "tombstone"}

@@ -32,7 +32,7 @@ for mode in "$@"; do
     rc=$?; echo "bench2 rc=$rc" >> gpurun_out/bench2.err; [ $rc -eq 0 ] || exit $rc
     ;;
   csbench)
-    timeout -k 10 300 python -u tools_cs_bench.py 65536 64,1024,16384,65536 2 > gpurun_out/csbench.json 2> gpurun_out/csbench.err
+    timeout -k 10 300 python -u tools_cs_bench.py 65536 64,1024,16384,65536 2 ${CS_MODES:-0,1,2} > gpurun_out/csbench.json 2> gpurun_out/csbench.err
     rc=$?; echo "csbench rc=$rc" >> gpurun_out/csbench.err; [ $rc -eq 0 ] || exit $rc
     ;;
   pmc)
