@@ -128,8 +128,7 @@ __device__ __forceinline__ bool cs_prologue(const DS &d, uint32_t id, bool is_ro
 // Waves: 0 h chain, 1 g/f chain, 2 and 3 formatters.
 // MODE 0: normal; 1: hashers only (formatter skips its stores); 2: formatter only; 3: the g/f wave
 // also dumps every block it hashes to dbg (lane 0's row; diagnostics); 4: barrier skeleton (no
-// loads, no hashing); 5: formatter loads and positions only. Modes 1, 2, 4, 5 time parts of the kernel
-// (swimsim_bench_checksum modes 6, 7, 8 run k_checksum_lat: normal, no formatter stores, formatters only).
+// loads, no hashing); 5: formatter loads and positions only. Modes 1, 2, 4, 5 time parts of the kernel.
 // JMIN = words every record fills completely (shortest record >> 2): their writes need no mask.
 template <int W, int NO, int JMIN, int MODE>
 __global__ void __launch_bounds__(256) k_checksum(DS d, const uint32_t *list, const uint32_t *count,
@@ -396,299 +395,12 @@ __global__ void __launch_bounds__(256) k_checksum(DS d, const uint32_t *list, co
     }
 }
 
-// ---------------------------------------------------------------------------------------------
-// Latency variant, for launches of a few rows (one workgroup per CU or fewer). The chain of one row
-// is the whole launch time there, so the work of a block is spread over more waves: 8 waves, two per
-// SIMD (wave w runs on SIMD w % 4):
-//   waves 2, 3, 6, 7: formatters, one record of each step's four each (two per SIMD, so the
-//                     dependent instruction chains of a record interleave);
-//   wave 5 (premix) : the chain-independent half of every block, M(c), M(d) and M(b + e c1)
-//                     (5 of the 7 multiplies), into a per-row ring of 32 blocks;
-//   wave 1 (h)      : h = mur(d, h + a) + e with M(d) precomputed;
-//   wave 0 (g/f)    : the coupled g and f lanes with M(c), M(b + e c1) precomputed;
-//   wave 4          : idle (keeps SIMD 0 to the g/f wave).
-// Pipeline: at step t the formatters write step t, the premix wave takes the blocks completed by
-// step t-1, the hashers the blocks the premix wave took at step t-1. The string ring (150 words)
-// holds 3 steps of 4 records of at most 40 bytes plus a partial block.
-// ---------------------------------------------------------------------------------------------
-constexpr int CL_RING = 150;
-constexpr int CL_PHYS = CS_PRE + CL_RING + CS_POST;
-constexpr int CL_SINK = CL_PHYS;
-constexpr int CL_LDSW = CL_PHYS + 12;
-
-template <int W, int NO, int JMIN, int MODE = 0>
-__global__ void __launch_bounds__(512) k_checksum_lat(DS d, const uint32_t *list, const uint32_t *count,
-                                                      const uint32_t *__restrict__ addrw, const uint4 *__restrict__ rtail) {
-    __shared__ uint32_t ring[CL_LDSW * CS_ROWS];
-    __shared__ uint32_t mring[3][CL_RING / 5][CS_ROWS];           // M(c), M(d), M(b + e c1) per ring block
-    __shared__ uint32_t wp[4][CS_ROWS];
-    __shared__ uint32_t xgf[2][CS_ROWS];
-    constexpr int Q = W / 4;
-    static_assert(NO <= CS_PRE + 1 && NO <= CS_POST + 1, "spill areas too small");
-    static_assert(NO <= Q + 8, "record tail table holds 7 words after the address words");
-    static_assert(CL_RING % 5 == 0, "blocks must tile the ring");
-    static_assert(CL_RING * 4 >= 3 * 4 * 40 + 24, "ring too small for three steps");
-    const uint32_t cnt = *count;
-    if (blockIdx.x * CS_ROWS >= cnt) return;                       // uniform per workgroup
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
-    const uint32_t gi = blockIdx.x * CS_ROWS + lane;
-    const bool valid = gi < cnt;
-    const uint32_t id = list[valid ? gi : blockIdx.x * CS_ROWS];
-    const bool is_row = id < d.NL;
-    const uint32_t *row = is_row ? d.mw + (size_t)id * d.NP : d.dense + (size_t)(id - d.NL) * d.NP;
-    const uint32_t N = d.N, ecap1 = d.ecap - 1;
-    const uint32_t nsup = (N + CS_SUP - 1) / CS_SUP;
-    const uint32_t nit = nsup * (CS_SUP / CS_IT);
-    const uint32_t nsteps = nit + 2;                               // two drain steps
-
-    if (wave == 4) {
-        for (uint32_t t = 0; t <= nsteps; t++) lds_barrier();
-        return;
-    }
-    if (wave >= 2 && wave != 5) {
-        // ------------------------------- formatters -------------------------------
-        // formatter f formats member 4i + f of interval i and tracks the length and last bytes of the
-        // other three (see k_checksum)
-        const uint32_t f = (wave & 1u) | ((wave >> 2) << 1);
-        uint32_t pos = 0, phys = 0, hc = 0;
-        uint4 pre[4], cur[4];
-        uint4 ta[2], tb[2][CS_IT];
-        uint32_t A[2][Q + 1];
-        auto tails = [&](const uint4 &q4, uint4 &xa, uint4 (&xb)[CS_IT]) {
-            const uint32_t ws[4] = {q4.x, q4.y, q4.z, q4.w};
-            const uint32_t own = f == 0 ? ws[0] : f == 1 ? ws[1] : f == 2 ? ws[2] : ws[3];
-            xa = rtail[((size_t)min(own >> 3, ecap1) * 4 + (own & 3u)) * 2];
-#pragma unroll
-            for (int k = 0; k < CS_IT; k++) xb[k] = rtail[((size_t)min(ws[k] >> 3, ecap1) * 4 + (ws[k] & 3u)) * 2 + 1];
-        };
-        auto addrs = [&](uint32_t mb, uint32_t (&xA)[Q + 1]) {
-            const uint32_t *ap = addrw + (size_t)min(mb + f, N - 1) * 6;
-#pragma unroll
-            for (int i = 0; i <= Q; i++) xA[i] = ap[i];
-        };
-#pragma unroll
-        for (int k = 0; k < 4; k++) pre[k] = *(const uint4 *)(row + 4 * k);
-        tails(pre[0], ta[0], tb[0]);
-        addrs(0, A[0]);
-        for (uint32_t sc = 0; sc < nsup; sc++) {
-#pragma unroll
-            for (int k = 0; k < 4; k++) cur[k] = pre[k];
-            if (sc + 1 < nsup) {
-#pragma unroll
-                for (int k = 0; k < 4; k++) pre[k] = *(const uint4 *)(row + (sc + 1) * CS_SUP + 4 * k);
-            }
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int b = u & 1, nb_ = b ^ 1;
-                const uint32_t mb = sc * CS_SUP + u * CS_IT;
-                tails(u < 3 ? cur[u + 1] : pre[0], ta[nb_], tb[nb_]);
-                addrs(mb + CS_IT, A[nb_]);
-                const uint4 q4 = cur[u];
-                const uint32_t ws[4] = {q4.x, q4.y, q4.z, q4.w};
-                uint32_t Lk[CS_IT], sk[CS_IT], pk[CS_IT], hk[CS_IT];
-#pragma unroll
-                for (int k = 0; k < CS_IT; k++) {
-                    const uint32_t c6 = tb[b][k].z, c7 = tb[b][k].w;
-                    const uint32_t L = ((ws[k] & 7u) < 4u && mb + k < N) ? (c6 >> 24) : 0u;
-                    const uint32_t sh = pos & 3u;
-                    Lk[k] = L; sk[k] = sh; pk[k] = phys; hk[k] = hc;
-                    uint32_t np = phys + ((sh + L) >> 2);
-                    np = np >= CL_RING ? np - CL_RING : np;
-                    phys = np;
-                    hc = L ? c7 : hc;
-                    pos += L;
-                }
-                auto emit = [&](auto F) {
-                    constexpr int k = decltype(F)::value;
-                    const uint32_t L = Lk[k], sh = sk[k], ph = pk[k];
-                    const uint4 &t0 = ta[b];
-                    const uint32_t C[7] = {t0.x, t0.y, t0.z, t0.w, tb[b][k].x, tb[b][k].y, tb[b][k].z};
-                    const uint32_t sel = 0x07060504u - sh * 0x01010101u;
-                    const uint32_t nw = (sh + L) >> 2;
-                    uint32_t R[NO], O[NO];
-#pragma unroll
-                    for (int i = 0; i < NO; i++)
-                        R[i] = i < Q ? A[b][i] : (i == Q ? (A[b][Q] | C[0]) : (i - Q < 7 ? C[i - Q] : 0u));
-#pragma unroll
-                    for (int j = 0; j < NO; j++) O[j] = __builtin_amdgcn_perm(R[j], j ? R[j - 1] : hk[k], sel);
-                    const uint32_t sink = CL_SINK * CS_ROWS + lane;
-                    const uint32_t i0 = L ? (CS_PRE + ph) * CS_ROWS + lane : sink;
-#pragma unroll
-                    for (int j = 0; j < NO; j++)
-                        ring[(j < JMIN || (uint32_t)j < nw ? i0 : sink) + j * CS_ROWS] = O[j];
-                    if (L && ph + nw > CL_RING) {
-                        const uint32_t i1 = (CS_PRE + ph - CL_RING) * CS_ROWS + lane;
-#pragma unroll
-                        for (int j = 0; j < NO; j++)
-                            ring[(j < JMIN || (uint32_t)j < nw ? i1 : sink) + j * CS_ROWS] = O[j];
-                    }
-                };
-                if (MODE != 1) {
-                    if (f == 0) emit(std::integral_constant<int, 0>{});
-                    else if (f == 1) emit(std::integral_constant<int, 1>{});
-                    else if (f == 2) emit(std::integral_constant<int, 2>{});
-                    else emit(std::integral_constant<int, 3>{});
-                }
-                if (f == 0) wp[(sc * 4 + u) & 3][lane] = pos;
-                lds_barrier();
-            }
-        }
-        lds_barrier();                                             // the two drain steps
-        lds_barrier();
-        lds_barrier();                                             // final g/f hand-over
-        return;
-    }
-
-    // Block j of the string sits at ring block j mod 30 (words 5j..5j+4 mod CL_RING); its premixed
-    // words sit at the same block index of mring. A group reads blocks done..done+3 at constant
-    // offsets from one of two bases (before / after the ring end): one compare and two selects a block.
-    const uint32_t *rb = ring + CS_PRE * CS_ROWS + lane;
-    FH fh{0, 0, 0};
-    uint32_t iters = 0;
-    const bool ok = cs_prologue<W>(d, id, is_row, row, fh, iters);
-    auto lim_premix = [&](uint32_t s) -> uint32_t {               // blocks premixed by the end of step s
-        if (s == 0) return 0u;
-        if (s >= nit) return iters;
-        return min(iters, wp[(s - 1) & 3][lane] / 20u);
-    };
-    constexpr uint32_t NBLK = CL_RING / 5;
-    uint32_t done = 0, bq = 0;                                     // bq = done mod NBLK
-    auto next = [&](uint32_t n) {
-        done += n;
-        bq += n;
-        bq = bq >= NBLK ? bq - NBLK : bq;
-    };
-    // pointers to block k of the group: string words (stride CS_ROWS) and premixed words
-    auto sblk = [&](int k) -> const uint32_t * {
-        const uint32_t *p0 = rb + bq * 5u * CS_ROWS;
-        return bq + (uint32_t)k < NBLK ? p0 : p0 - CL_RING * CS_ROWS;
-    };
-    auto mblk = [&](int a, int k) -> uint32_t * {
-        uint32_t *m0 = &mring[a][bq][lane];
-        return bq + (uint32_t)k < NBLK ? m0 : m0 - NBLK * CS_ROWS;
-    };
-    auto take = [&](uint32_t lim, bool pred) { next(pred ? (done < lim ? min(lim - done, 4u) : 0u) : 4u); };
-
-    if (wave == 5) {
-        // ------------------------------- premix -------------------------------
-        auto group = [&](uint32_t lim, bool pred) {
-            uint32_t v[4][4];
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const uint32_t *sp = sblk(k) + 5 * k * CS_ROWS;
-#pragma unroll
-                for (int i = 0; i < 4; i++) v[k][i] = sp[(1 + i) * CS_ROWS];     // b, c, d, e
-            }
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const uint32_t b = v[k][0], c = v[k][1], dd = v[k][2], e = v[k][3];
-                uint32_t ec;
-                asm("v_mul_lo_u32 %0, %1, %2" : "=v"(ec) : "v"(e), "s"(FH_C1));
-                // blocks past the limit write future slots that are rewritten before they are read
-                mblk(0, k)[k * CS_ROWS] = fh_m(c);
-                mblk(1, k)[k * CS_ROWS] = fh_m(dd);
-                mblk(2, k)[k * CS_ROWS] = fh_m(b + ec);
-            }
-            take(lim, pred);
-        };
-        for (uint32_t t = 0; t < nsteps; t++) {
-            const uint32_t lim = MODE == 2 ? 0u : lim_premix(t);
-            while (__all(done + 4 <= lim)) group(lim, false);
-            while (__any(done < lim)) group(lim, true);
-            lds_barrier();
-        }
-        lds_barrier();
-        return;
-    }
-
-    uint32_t h = fh.h, g = fh.g, fv = fh.f;
-    if (!ok && valid && wave == 0) atomicOr(d.err, E_SHORT);
-    if (wave == 1) {
-        // ------------------------------- h chain -------------------------------
-        auto group = [&](uint32_t lim, bool pred) {
-            uint32_t a[4], e[4], md[4];
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const uint32_t *sp = sblk(k) + 5 * k * CS_ROWS;
-                a[k] = sp[0];
-                e[k] = sp[4 * CS_ROWS];
-                md[k] = mblk(1, k)[k * CS_ROWS];
-            }
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const uint32_t hn = fh_fold(h + a[k], md[k], e[k]);
-                h = (!pred || done + k < lim) ? hn : h;
-            }
-            take(lim, pred);
-        };
-        for (uint32_t t = 0; t < nsteps; t++) {
-            const uint32_t lim = (t == 0 || MODE == 2) ? 0u : lim_premix(t - 1);
-            while (__all(done + 4 <= lim)) group(lim, false);
-            while (__any(done < lim)) group(lim, true);
-            lds_barrier();
-        }
-    } else {
-        // ------------------------------- g/f chain -------------------------------
-        auto group = [&](uint32_t lim, bool pred) {
-            uint32_t v[4][4], mc[4], mbe[4];
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const uint32_t *sp = sblk(k) + 5 * k * CS_ROWS;
-#pragma unroll
-                for (int i = 0; i < 4; i++) v[k][i] = sp[i * CS_ROWS];              // a, b, c, d
-                mc[k] = mblk(0, k)[k * CS_ROWS];
-                mbe[k] = mblk(2, k)[k * CS_ROWS];
-            }
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const uint32_t gn = fh_fold(g + v[k][1], mc[k], v[k][0]);
-                uint32_t fn = fh_fold(fv + v[k][2], mbe[k], v[k][3]);
-                fn += gn;
-                const bool act = !pred || done + k < lim;
-                g = act ? gn + fn : g;
-                fv = act ? fn : fv;
-            }
-            take(lim, pred);
-        };
-        for (uint32_t t = 0; t < nsteps; t++) {
-            const uint32_t lim = (t == 0 || MODE == 2) ? 0u : lim_premix(t - 1);
-            while (__all(done + 4 <= lim)) group(lim, false);
-            while (__any(done < lim)) group(lim, true);
-            lds_barrier();
-        }
-        xgf[0][lane] = g;
-        xgf[1][lane] = fv;
-    }
-    lds_barrier();
-    if (wave == 1 && valid) {
-        fh.h = h; fh.g = xgf[0][lane]; fh.f = xgf[1][lane];
-        const uint32_t hv = ok ? fh.fin() : 0u;
-        if (is_row) {
-            d.cs[id] = hv;
-            d.dirty[id] = 0;
-            ctr_add(d, C_X_CS_ROWS, 1ull);
-        } else {
-            d.dense_cs[id - d.NL] = hv;
-        }
-    }
-}
-
 // NO for the address width W and the longest record tail of the handle's incarnation table
 constexpr int cs_no(int W, int maxtail) { return (3 + W + maxtail + 3) / 4; }
 
 template <int W, int MODE>
 void launch_cs_w(const DS &d, const uint32_t *list, const uint32_t *count, uint32_t grid, hipStream_t s,
-                 uint32_t *dbg = nullptr, uint32_t cap = 0, bool lat = false) {
-    if (lat && (MODE == 0 || MODE == 7 || MODE == 8)) {           // few rows: the latency variant
-        constexpr int LM = MODE == 7 ? 1 : MODE == 8 ? 2 : 0;
-        if (W == 19 && d.max_tail <= 21 && d.min_tail >= 19)
-            hipLaunchKernelGGL((k_checksum_lat<W, cs_no(W, 21), (W + 19) / 4, LM>), dim3(grid), dim3(512), 0, s, d, list,
-                               count, d.addrw, (const uint4 *)d.rtail);
-        else
-            hipLaunchKernelGGL((k_checksum_lat<W, cs_no(W, 24), (W + 7) / 4>), dim3(grid), dim3(512), 0, s, d, list,
-                               count, d.addrw, (const uint4 *)d.rtail);
-        return;
-    }
+                 uint32_t *dbg = nullptr, uint32_t cap = 0) {
     // the common case: 13-digit incarnations (t0 = 1.5e12 ms): tails of 19..21 bytes
     if (W == 19 && d.max_tail <= 21 && d.min_tail >= 19)
         hipLaunchKernelGGL((k_checksum<W, cs_no(W, 21), (W + 19) / 4, MODE>), dim3(grid), dim3(256), 0, s, d, list, count,
@@ -698,19 +410,11 @@ void launch_cs_w(const DS &d, const uint32_t *list, const uint32_t *count, uint3
                            d.addrw, (const uint4 *)d.rtail, dbg, cap);
 }
 
-// rows <= CS_LAT_ROWS: k_checksum_lat (8 waves per 64 rows, two workgroups per CU); above, the
-// throughput kernel (4 waves per 64 rows, four per CU)
-constexpr uint32_t CS_LAT_ROWS = 16384;
-
-// maxn bounds the count on the device; nrows (when known on the host, else ~0u) picks the variant
-void launch_checksum(const DS &d, const uint32_t *list, const uint32_t *count, uint32_t maxn, uint32_t nrows,
-                     hipStream_t s) {
-    const uint32_t n = std::min(maxn, nrows);
-    const uint32_t grid = (n + CS_ROWS - 1) / CS_ROWS;
+void launch_checksum(const DS &d, const uint32_t *list, const uint32_t *count, uint32_t maxn, hipStream_t s) {
+    const uint32_t grid = (maxn + CS_ROWS - 1) / CS_ROWS;
     if (grid == 0) return;
-    const bool lat = n <= CS_LAT_ROWS;
     switch (d.W) {
-#define CS_CASE(Wv) case Wv: launch_cs_w<Wv, 0>(d, list, count, grid, s, nullptr, 0, lat); break;
+#define CS_CASE(Wv) case Wv: launch_cs_w<Wv, 0>(d, list, count, grid, s); break;
         CS_CASE(13) CS_CASE(14) CS_CASE(15) CS_CASE(16) CS_CASE(17) CS_CASE(18) CS_CASE(19) CS_CASE(20)
 #undef CS_CASE
     default: break;
@@ -727,10 +431,7 @@ void launch_checksum_dump(const DS &d, const uint32_t *list, const uint32_t *cou
 void launch_checksum_mode(const DS &d, const uint32_t *list, const uint32_t *count, uint32_t maxn, int mode, hipStream_t s) {
     const uint32_t grid = (maxn + CS_ROWS - 1) / CS_ROWS;
     if (grid == 0 || d.W != 19) return;
-    if (mode == 6) launch_cs_w<19, 0>(d, list, count, grid, s, nullptr, 0, true);
-    else if (mode == 7) launch_cs_w<19, 7>(d, list, count, grid, s, nullptr, 0, true);
-    else if (mode == 8) launch_cs_w<19, 8>(d, list, count, grid, s, nullptr, 0, true);
-    else if (mode == 1) launch_cs_w<19, 1>(d, list, count, grid, s);
+    if (mode == 1) launch_cs_w<19, 1>(d, list, count, grid, s);
     else if (mode == 2) launch_cs_w<19, 2>(d, list, count, grid, s);
     else if (mode == 4) launch_cs_w<19, 4>(d, list, count, grid, s);
     else if (mode == 5) launch_cs_w<19, 5>(d, list, count, grid, s);
