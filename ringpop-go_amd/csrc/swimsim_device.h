@@ -5,11 +5,12 @@
 //                      statePrecedence (swim/member.go:112-128), 7 = not in the memberlist.
 //                      (e,status) as one integer makes nonLocalOverride (member.go:79-93) a single
 //                      unsigned compare.
-//   dp  u8  [NL][NP]   disseminator piggyback counter p (disseminator.go:39-42); 0xFF = no entry
+//   dent u32x4[NL][NP] dissemination entry (disseminator.go:39-42): {source | p << 24, source e,
+//                      member word, 0}; p = 0xFF: no entry. The member word is a copy of mw kept
+//                      equal while the entry exists, so issuing an entry is one 16-byte gather.
 //   tst u8  [NL][NP]   timer state (suspect 1 / faulty 2 / tombstone 4) | 0x80 fired
-//   dsrc u32x2[NL][NP] dissemination entry {source, source e}
 //   tmr u32x2 [NL][NP] timer {deadline round, subject e}
-//   dbit u32 [NL][NBIT] bit m: member m has a dissemination entry (exactly: dp[m] != 0xFF)
+//   dbit u32 [NL][NBIT] bit m: member m has a dissemination entry (exactly: p != 0xFF)
 //   tblk u32 [NL][NB]  lower bound of the unfired timer deadlines in block b
 // Messages are pools of 16-byte change records {member | status<<24, e, source, source e}, or
 // dense row snapshots for MembershipAsChanges (disseminator.go:107-123).
@@ -23,6 +24,11 @@ constexpr uint32_t ST_ALIVE = 0, ST_SUSPECT = 1, ST_FAULTY = 2, ST_LEAVE = 3, ST
 constexpr uint32_t SRC_NONE = 0xFFFFFFFFu;
 constexpr uint32_t NO_DEADLINE = 0xFFFFFFFFu;
 constexpr uint8_t DP_NONE = 0xFF;
+// dissemination entry word 0: source (24 bits, 0xFFFFFF = none) | p << 24
+constexpr uint32_t DE_NONE = 0xFFFFFFFFu;                      // no entry, no source
+__host__ __device__ inline uint32_t de_p(uint32_t x) { return x >> 24; }
+__host__ __device__ inline uint32_t de_src(uint32_t x) { return (x & 0xFFFFFFu) == 0xFFFFFFu ? SRC_NONE : (x & 0xFFFFFFu); }
+__host__ __device__ inline uint32_t de_x(uint32_t src, uint32_t p) { return (src & 0xFFFFFFu) | (p << 24); }
 
 enum Counter {
     C_ROUNDS, C_PINGS, C_PINGS_OK, C_PINGREQS, C_HELPER_CALLS, C_HELPER_ERRORS, C_INCONCLUSIVE,
@@ -52,9 +58,8 @@ struct DS {
     uint32_t ecap;
     uint64_t seed;
     uint32_t *mw;
-    uint8_t *dp;
+    uint4 *dent;            // {source | p << 24, source e, member word, 0}
     uint8_t *tst;
-    uint2 *dsrc;            // {dissemination source, source e}
     uint2 *tmr;             // {timer deadline round, timer subject e}
     uint32_t *dbit;         // [NL][NBIT] dissemination presence bits
     uint32_t NBIT;          // words per row of dbit (multiple of 4)

@@ -1140,8 +1140,8 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
     d.seed = h->seed;
     const size_t rows = (size_t)h->NL * h->NP;
     int rc = 0;
-    if ((rc = dalloc(h, &d.mw, rows, "member words")) || (rc = dalloc(h, &d.dp, rows, "piggyback counters")) ||
-        (rc = dalloc(h, &d.tst, rows, "timer states")) || (rc = dalloc(h, &d.dsrc, rows, "dissemination sources")) ||
+    if ((rc = dalloc(h, &d.mw, rows, "member words")) || (rc = dalloc(h, &d.dent, rows, "dissemination entries")) ||
+        (rc = dalloc(h, &d.tst, rows, "timer states")) ||
         (rc = dalloc(h, &d.tmr, rows, "timers")) ||
         (rc = dalloc(h, &d.ping, h->NL, "ping")) || (rc = dalloc(h, &d.maxp, h->NL, "maxp")) ||
         (rc = dalloc(h, &d.dcnt, h->NL, "dcnt")) || (rc = dalloc(h, &d.dirty, h->NL, "dirty")) ||
@@ -1429,19 +1429,18 @@ int swimsim_changes(swimsim_t *h, uint32_t o, int32_t *member, int32_t *p, int32
                     size_t cap, size_t *n) {
     if (!h || !own(h, o)) return SWIMSIM_EINVAL;
     const size_t base = (size_t)(o - h->lo) * h->NP;
-    std::vector<uint8_t> dp(h->NP);
-    std::vector<uint2> aux(h->NP);
-    HIPCHK(h, hipMemcpyAsync(dp.data(), h->d.dp + base, h->NP, hipMemcpyDeviceToHost, h->s));
-    HIPCHK(h, hipMemcpyAsync(aux.data(), h->d.dsrc + base, h->NP * 8, hipMemcpyDeviceToHost, h->s));
+    std::vector<uint4> ent(h->NP);
+    HIPCHK(h, hipMemcpyAsync(ent.data(), h->d.dent + base, h->NP * 16, hipMemcpyDeviceToHost, h->s));
     HIPCHK(h, hipStreamSynchronize(h->s));
     size_t k = 0;
     for (uint32_t m = 0; m < h->N; m++) {
-        if (dp[m] == DP_NONE) continue;
+        const uint32_t pm = de_p(ent[m].x), src = de_src(ent[m].x);
+        if (pm == DP_NONE) continue;
         if (k < cap) {
             if (member) member[k] = (int32_t)m;
-            if (p) p[k] = dp[m];
-            if (source) source[k] = aux[m].x == SRC_NONE ? -1 : (int32_t)aux[m].x;
-            if (source_inc_ms) source_inc_ms[k] = aux[m].x == SRC_NONE ? 0 : from_e(h, aux[m].y);
+            if (p) p[k] = (int32_t)pm;
+            if (source) source[k] = src == SRC_NONE ? -1 : (int32_t)src;
+            if (source_inc_ms) source_inc_ms[k] = src == SRC_NONE ? 0 : from_e(h, ent[m].y);
         }
         k++;
     }

@@ -91,17 +91,17 @@ __device__ __forceinline__ void merge_change_w(const DS &d, uint32_t ol, uint32_
     } else {
         return;
     }
-    d.mw[idx] = (ne << 3) | nst;
-    track_len(d, ol, m, cur, (ne << 3) | nst, acc);
+    const uint32_t nw_ = (ne << 3) | nst;
+    d.mw[idx] = nw_;
+    track_len(d, ol, m, cur, nw_, acc);
     acc.dfp += fpmix(m, (ne << 3) | nst) - fpmix(m, cur);
     if (m != o) acc.dping += (int)is_pingable(nst) - (int)is_pingable(cur_st);
     // RecordChange (disseminator.go:223-227): entry = {p 0, source, source incarnation}
-    if (d.dp[idx] == DP_NONE) {
+    if (de_p(((const uint32_t *)(d.dent + idx))[0]) == DP_NONE) {
         acc.ddc++;
         atomicOr(&d.dbit[(size_t)ol * d.NBIT + (m >> 5)], 1u << (m & 31));
     }
-    d.dp[idx] = 0;
-    d.dsrc[idx] = make_uint2(nsrc, nsinc);
+    d.dent[idx] = make_uint4(de_x(nsrc, 0), nsinc, nw_, 0);
     if (m != o) {                                                  // no timers for the local member
         const uint8_t ts = d.tst[idx];
         const uint32_t tstate = ts & 7u;
@@ -215,26 +215,27 @@ __device__ void wave_bump(const DS &d, uint32_t ol, const MsgDesc &md) {
     if (md.kind != 0) return;
     const unsigned long long off = ((unsigned long long)md.off_hi << 32) | md.off_lo;
     const int maxp = d.maxp[ol];
-    uint8_t *dpr = d.dp + (size_t)ol * d.NP;
+    uint32_t *dx = (uint32_t *)(d.dent + (size_t)ol * d.NP);       // word 0 of each entry, stride 4
     int del = 0;
     for (uint32_t base = 0; base < md.len; base += 64 * MB) {
-        uint32_t m[MB], p[MB];
+        uint32_t m[MB], x[MB];
 #pragma unroll
         for (int u = 0; u < MB; u++) {
             const uint32_t i = base + u * 64 + lane_id();
             m[u] = i < md.len ? (d.pool[off + i].x & 0xFFFFFFu) : 0xFFFFFFFFu;
         }
 #pragma unroll
-        for (int u = 0; u < MB; u++) p[u] = m[u] != 0xFFFFFFFFu ? dpr[m[u]] : DP_NONE;
+        for (int u = 0; u < MB; u++) x[u] = m[u] != 0xFFFFFFFFu ? dx[(size_t)m[u] * 4] : DE_NONE;
 #pragma unroll
         for (int u = 0; u < MB; u++) {
-            if (p[u] == DP_NONE) continue;
-            if ((int)(p[u] + 1) >= maxp) {
-                dpr[m[u]] = DP_NONE;
+            const uint32_t p = de_p(x[u]);
+            if (p == DP_NONE) continue;
+            if ((int)(p + 1) >= maxp) {
+                dx[(size_t)m[u] * 4] = x[u] | 0xFF000000u;
                 atomicAnd(&d.dbit[(size_t)ol * d.NBIT + (m[u] >> 5)], ~(1u << (m[u] & 31)));
                 del++;
             } else {
-                dpr[m[u]] = (uint8_t)(p[u] + 1);
+                dx[(size_t)m[u] * 4] = x[u] + (1u << 24);
             }
         }
     }
@@ -306,14 +307,16 @@ __device__ uint32_t wave_issue_t(const DS &d, uint32_t ol, uint32_t sender, uint
                 else if (hi) { m[k] = mbase + 64 + (uint32_t)(__ffsll((long long)hi) - 1); hi &= hi - 1; }
                 else m[k] = 0xFFFFFFFFu;
             }
+            uint4 ce[MB];                                        // one 16-byte gather per entry
+#pragma unroll
+            for (int k = 0; k < MB; k++) ce[k] = m[k] != 0xFFFFFFFFu ? d.dent[rb + m[k]] : make_uint4(DE_NONE, 0, 0, 0);
             uint32_t p[MB], wv[MB];
             uint2 sr[MB];
 #pragma unroll
             for (int k = 0; k < MB; k++) {
-                const bool v = m[k] != 0xFFFFFFFFu;
-                p[k] = (RECV && v) ? d.dp[rb + m[k]] : 0u;
-                sr[k] = v ? d.dsrc[rb + m[k]] : make_uint2(0, 0);
-                wv[k] = v ? d.mw[rb + m[k]] : 0u;
+                p[k] = de_p(ce[k].x);
+                sr[k] = make_uint2(de_src(ce[k].x), ce[k].y);
+                wv[k] = ce[k].z;
             }
             bool keep[MB];
             uint32_t nk = 0;
@@ -331,13 +334,14 @@ __device__ uint32_t wave_issue_t(const DS &d, uint32_t ol, uint32_t sender, uint
                 if (at < cnt) d.pool[off + at] = make_uint4(m[k] | (st << 24), wv[k] >> 3, sr[k].x, sr[k].y);
                 at++;
                 if (RECV) {                                                   // bump
+                    uint32_t *dxk = (uint32_t *)(d.dent + rb + m[k]);
                     if ((int)(p[k] + 1) >= maxp) {
-                        d.dp[rb + m[k]] = DP_NONE;
+                        *dxk = ce[k].x | 0xFF000000u;
                         const uint32_t l = m[k] - mbase;
                         if (l < 64) dlo |= 1ull << l; else dhi |= 1ull << (l - 64);
                         del++;
                     } else {
-                        d.dp[rb + m[k]] = (uint8_t)(p[k] + 1);
+                        *dxk = ce[k].x + (1u << 24);
                     }
                 }
             }
@@ -413,9 +417,8 @@ __global__ void k_init_rows(DS d, int mode, uint32_t e0) {
         if (m < d.N && (mode == 0 || m == o)) w = (e0 << 3) | ST_ALIVE;
         if (m < d.N) fp += fpmix(m, w);
         d.mw[idx] = w;
-        d.dp[idx] = DP_NONE;
+        d.dent[idx] = make_uint4(DE_NONE, 0, w, 0);
         d.tst[idx] = 0;
-        d.dsrc[idx] = make_uint2(0, 0);
         d.tmr[idx] = make_uint2(NO_DEADLINE, 0);
     }
     for (uint32_t b = lane_id(); b < d.NB; b += 64) d.tblk[(size_t)ol * d.NB + b] = NO_DEADLINE;
@@ -450,7 +453,9 @@ __global__ void k_recount(DS d, uint32_t ol) {
         const uint32_t w = d.mw[idx];
         fp += fpmix(m, w);
         if (m != o && is_pingable(w & 7u)) p++;
-        if (d.dp[idx] != DP_NONE) c++;
+        uint32_t *de = (uint32_t *)(d.dent + idx);
+        if (de_p(de[0]) != DP_NONE) c++;
+        de[2] = w;                                                   // re-mirror the member word
         len += reclen(d, w & 7u, w >> 3);
         if ((w & 7u) < 4u) last = (int)m;
     }
@@ -466,7 +471,7 @@ __global__ void k_recount(DS d, uint32_t ol) {
 }
 
 __global__ void k_clear_changes(DS d, uint32_t ol) {
-    for (uint32_t m = threadIdx.x; m < d.NP; m += blockDim.x) d.dp[(size_t)ol * d.NP + m] = DP_NONE;
+    for (uint32_t m = threadIdx.x; m < d.NP; m += blockDim.x) ((uint32_t *)(d.dent + (size_t)ol * d.NP + m))[0] = DE_NONE;
     for (uint32_t b = threadIdx.x; b < d.NBIT; b += blockDim.x) d.dbit[(size_t)ol * d.NBIT + b] = 0;
     if (threadIdx.x == 0) d.dcnt[ol] = 0;
 }
@@ -550,6 +555,7 @@ __global__ void k_timers(DS d, uint32_t r) {
                     if ((w & 7u) != ST_UNKNOWN && m != o) {
                         if (is_pingable(w & 7u)) acc.dping--;
                         d.mw[idx] = (w & ~7u) | ST_UNKNOWN;
+                        ((uint32_t *)(d.dent + idx))[2] = (w & ~7u) | ST_UNKNOWN;   // entry mirror
                         track_len(d, ol, m, w, (w & ~7u) | ST_UNKNOWN, acc);
                         acc.dfp += fpmix(m, (w & ~7u) | ST_UNKNOWN) - fpmix(m, w);
                         acc.evict++;
@@ -1169,9 +1175,10 @@ __global__ void k_digest(DS d, unsigned long long *out, uint32_t period_div) {
         const size_t idx = (size_t)ol * d.NP + m;
         const uint32_t w = d.mw[idx];
         r += mix4(o, m, w & 7u, w >> 3);
-        const uint8_t p = d.dp[idx];
+        const uint4 ce = d.dent[idx];
+        const uint32_t p = de_p(ce.x);
         if (p != DP_NONE) {
-            const uint2 a = d.dsrc[idx];
+            const uint2 a = make_uint2(de_src(ce.x), ce.y);
             const uint64_t se = a.x == SRC_NONE ? 0ull : (uint64_t)a.y;
             dd += mix4((uint64_t)o | (1ull << 40), m, (uint64_t)p | ((uint64_t)(uint32_t)(a.x + 1u) << 8), se);
         }
