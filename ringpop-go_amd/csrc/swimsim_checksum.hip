@@ -128,7 +128,8 @@ __device__ __forceinline__ bool cs_prologue(const DS &d, uint32_t id, bool is_ro
 // Waves: 0 h chain, 1 g/f chain, 2 and 3 formatters.
 // MODE 0: normal; 1: hashers only (formatter skips its stores); 2: formatter only; 3: the g/f wave
 // also dumps every block it hashes to dbg (lane 0's row; diagnostics); 4: barrier skeleton (no
-// loads, no hashing); 5: formatter loads and positions only. Modes 1, 2, 4, 5 time parts of the kernel.
+// loads, no hashing); 5: formatter loads and positions only. Modes 1, 2, 4, 5 time parts of the kernel
+// (swimsim_bench_checksum mode 6 runs k_checksum_n16).
 // JMIN = words every record fills completely (shortest record >> 2): their writes need no mask.
 template <int W, int NO, int JMIN, int MODE>
 __global__ void __launch_bounds__(256) k_checksum(DS d, const uint32_t *list, const uint32_t *count,
@@ -395,12 +396,305 @@ __global__ void __launch_bounds__(256) k_checksum(DS d, const uint32_t *list, co
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Narrow variant for launches of few rows (latency-bound: the launch time is one row's chain).
+// 16 rows per workgroup. The per-block work that does not depend on the chain runs across lanes
+// instead of rows:
+//   waves 2, 3 (formatters): lane = (row r, record k) for the 8 records of each step of 8 rows; a
+//                            segmented prefix sum of the record lengths places a row's 8 records;
+//   wave 1 (premix)        : lane = (row r, block slot s): M(c), M(d), M(b + e c1) of every block,
+//                            5 of the block's 7 multiplies, into a per-row ring of premixed words;
+//   wave 4 (h)             : lane r < 16: h = mur(d, h + a) + e with M(d) read;
+//   wave 0 (g/f)           : lane r < 16: g, f with M(c), M(b + e c1) read.
+// (wave w runs on the SIMD of wave w % 4: the light h chain shares the g/f wave's SIMD.)
+// At step t the formatters write step t, premix takes the blocks completed by step t-1 and the
+// hashers the blocks premixed at step t-1. Rows are stored row-major in LDS with an odd stride, so
+// the hashers' 16 lanes hit 16 banks; ring words [0, 20) and premixed blocks [0, 4) are mirrored
+// behind the ring end, so a hasher group of 4 blocks reads at constant offsets.
+// ---------------------------------------------------------------------------------------------
+constexpr int CN_ROWS = 16;
+constexpr int CN_IT = 8;                        // records per row per step
+constexpr int CN_RING = 250;                    // ring words per row (50 blocks): 3 steps of 8 records
+constexpr int CN_NBLK = CN_RING / 5;
+constexpr int CN_MIR = 20;
+constexpr int CN_MBLK = 4;
+constexpr int CN_SINK = CS_PRE + CN_RING + CN_MIR;
+constexpr int CN_STRIDE = CN_SINK + 13;         // landing area + ring + mirror + sink; odd
+static_assert(CN_STRIDE % 2 == 1, "row stride must be odd");
+constexpr int CN_MSTRIDE = (CN_NBLK + CN_MBLK) * 3;
+
+// NMODE (diagnostics): 0 normal; 1 formatters without stores; 2 formatters only (premix and hashers
+// idle); 3 no formatter work at all (fixed 38-byte records; premix and hashers on garbage); 4 as 3
+// with premix idle; 5 as 3 with the hashers idle; 6 as 4 with the h wave idle; 7 as 4 with the g/f
+// wave idle
+template <int W, int NO, int JMIN, int NMODE = 0>
+__global__ void __launch_bounds__(320) k_checksum_n16(DS d, const uint32_t *list, const uint32_t *count,
+                                                      const uint32_t *__restrict__ addrw, const uint4 *__restrict__ rtail) {
+    __shared__ uint32_t ring[CN_ROWS * CN_STRIDE];
+    __shared__ uint32_t mring[CN_ROWS * CN_MSTRIDE];                // [row][block][M(c), M(d), M(b + e c1)]
+    __shared__ uint32_t wp[4][CN_ROWS];
+    __shared__ uint32_t xgf[2][CN_ROWS];
+    constexpr int Q = W / 4;
+    static_assert(NO <= CS_PRE + 1 && NO <= 13, "spill areas too small");
+    static_assert(CS_PRE + CN_MIR - 1 + CN_RING + NO - 1 < CN_STRIDE, "mirror pass overruns the row");
+    static_assert(NO <= Q + 8, "record tail table holds 7 words after the address words");
+    static_assert(CN_RING * 4 >= 3 * CN_IT * 40 + 24, "ring too small for three steps");
+    const uint32_t cnt = *count;
+    const uint32_t b0 = blockIdx.x * CN_ROWS;
+    if (b0 >= cnt) return;                                         // uniform per workgroup
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    const uint32_t N = d.N, ecap1 = d.ecap - 1;
+    const uint32_t nit = (N + CN_IT - 1) / CN_IT;
+    const uint32_t nsteps = nit + 2;
+    auto row_of = [&](uint32_t r, uint32_t &id, bool &is_row) -> const uint32_t * {
+        const uint32_t gi = b0 + r;
+        id = list[gi < cnt ? gi : b0];
+        is_row = id < d.NL;
+        return is_row ? d.mw + (size_t)id * d.NP : d.dense + (size_t)(id - d.NL) * d.NP;
+    };
+
+    if (wave == 2 || wave == 3) {
+        // ------------------------------- formatters -------------------------------
+        const uint32_t r = (wave - 2) * 8 + (lane >> 3), k = lane & 7u;
+        uint32_t id; bool is_row;
+        const uint32_t *row = row_of(r, id, is_row);
+        uint32_t *rrow = ring + r * CN_STRIDE;
+        uint32_t pos = 0, phys = 0, hc = 0;                        // per row, kept in all 8 lanes of a segment
+        // prefetch: row words two steps ahead, tails and addresses one step ahead
+        auto ldw = [&](uint32_t t) { const uint32_t m = CN_IT * t + k; return m < N ? row[m] : (uint32_t)ST_UNKNOWN; };
+        uint32_t w0 = ldw(0), w1 = ldw(1);
+        auto ldt = [&](uint32_t w, uint4 &xa, uint4 &xb) {
+            const size_t ti = ((size_t)min(w >> 3, ecap1) * 4 + (w & 3u)) * 2;
+            xa = rtail[ti];
+            xb = rtail[ti + 1];
+        };
+        auto lda = [&](uint32_t t, uint32_t (&xA)[Q + 1]) {
+            const uint32_t *ap = addrw + (size_t)min(CN_IT * t + k, N - 1) * 6;
+#pragma unroll
+            for (int i = 0; i <= Q; i++) xA[i] = ap[i];
+        };
+        uint4 ta[2], tb[2];
+        uint32_t A[2][Q + 1];
+        ldt(w0, ta[0], tb[0]);
+        lda(0, A[0]);
+        auto step = [&](uint32_t t, auto B) {
+            constexpr int b = decltype(B)::value, nb_ = b ^ 1;
+            if (NMODE >= 3) {
+                pos += CN_IT * 38;
+                if (k == 0) wp[t & 3][r] = pos;
+                lds_barrier();
+                return;
+            }
+            const uint32_t w = w0;
+            w0 = w1;
+            w1 = ldw(t + 2);
+            ldt(w0, ta[nb_], tb[nb_]);                              // next step's tail and address
+            lda(t + 1, A[nb_]);
+            const uint32_t m = CN_IT * t + k;
+            const uint32_t L = ((w & 7u) < 4u && m < N) ? (tb[b].z >> 24) : 0u;
+            // segmented prefix sums over the row's 8 records: bytes before this record within the step,
+            // and the last bytes of the nearest non-empty record before it (the carry its first word
+            // is aligned against)
+            uint32_t inc = L, hv = L ? tb[b].w : 0u, hh = L ? 1u : 0u;
+#pragma unroll
+            for (int off = 1; off < CN_IT; off <<= 1) {
+                const uint32_t y = (uint32_t)__shfl_up((int)inc, off, CN_IT);
+                const uint32_t v2 = (uint32_t)__shfl_up((int)hv, off, CN_IT), h2 = (uint32_t)__shfl_up((int)hh, off, CN_IT);
+                if (k >= (uint32_t)off) {
+                    inc += y;
+                    if (!hh) { hv = v2; hh = h2; }
+                }
+            }
+            const uint32_t ex = inc - L, total = (uint32_t)__shfl((int)inc, CN_IT - 1, CN_IT);
+            const uint32_t cv = (uint32_t)__shfl_up((int)hv, 1, CN_IT), ch = (uint32_t)__shfl_up((int)hh, 1, CN_IT);
+            const uint32_t carry = (k >= 1 && ch) ? cv : hc;
+            const uint32_t lastv = (uint32_t)__shfl((int)hv, CN_IT - 1, CN_IT), lasth = (uint32_t)__shfl((int)hh, CN_IT - 1, CN_IT);
+            const uint32_t sh0 = pos & 3u;
+            const uint32_t sh = (sh0 + ex) & 3u;
+            uint32_t ph = phys + ((sh0 + ex) >> 2);
+            ph = ph >= CN_RING ? ph - CN_RING : ph;
+            if (NMODE != 1) {
+                const uint32_t C[7] = {ta[b].x, ta[b].y, ta[b].z, ta[b].w, tb[b].x, tb[b].y, tb[b].z};
+                const uint32_t sel = 0x07060504u - sh * 0x01010101u;
+                const uint32_t nw = (sh + L) >> 2;
+                uint32_t R[NO], O[NO];
+#pragma unroll
+                for (int i = 0; i < NO; i++)
+                    R[i] = i < Q ? A[b][i] : (i == Q ? (A[b][Q] | C[0]) : (i - Q < 7 ? C[i - Q] : 0u));
+#pragma unroll
+                for (int j = 0; j < NO; j++) O[j] = __builtin_amdgcn_perm(R[j], j ? R[j - 1] : carry, sel);
+                const uint32_t i0 = L ? CS_PRE + ph : (uint32_t)CN_SINK;
+#pragma unroll
+                for (int j = 0; j < NO; j++) rrow[(j < JMIN || (uint32_t)j < nw ? i0 : (uint32_t)CN_SINK) + j] = O[j];
+                // second pass: a record crossing the ring end is also written one ring length earlier
+                // (its words past the end land at the front), one starting in [0, CN_MIR) one ring
+                // length later (the mirror; words past the mirror land in the sink)
+                if (L && (ph < CN_MIR || ph + nw > CN_RING)) {
+                    const uint32_t i1 = CS_PRE + (ph < CN_MIR ? ph + CN_RING : ph - CN_RING);
+#pragma unroll
+                    for (int j = 0; j < NO; j++) rrow[(j < JMIN || (uint32_t)j < nw ? i1 : (uint32_t)CN_SINK) + j] = O[j];
+                }
+            }
+            uint32_t np = phys + ((sh0 + total) >> 2);
+            phys = np >= CN_RING ? np - CN_RING : np;
+            pos += total;
+            hc = lasth ? lastv : hc;
+            if (k == 0) wp[t & 3][r] = pos;
+            lds_barrier();
+        };
+        uint32_t t = 0;
+        for (; t + 1 < nit; t += 2) {
+            step(t, std::integral_constant<int, 0>{});
+            step(t + 1, std::integral_constant<int, 1>{});
+        }
+        if (t < nit) step(t, std::integral_constant<int, 0>{});
+        lds_barrier();                                             // the two drain steps
+        lds_barrier();
+        lds_barrier();                                             // final g/f hand-over
+        return;
+    }
+
+    if (wave == 1) {
+        // ------------------------------- premix -------------------------------
+        const uint32_t r = lane >> 2, s = lane & 3u;
+        uint32_t id; bool is_row;
+        (void)row_of(r, id, is_row);
+        const uint32_t len = is_row ? d.clen[id] : d.dense_len[id - d.NL];
+        const uint32_t iters = len > 24 ? (len - 1) / 20 : 0u;
+        const uint32_t *rrow = ring + r * CN_STRIDE + CS_PRE;
+        uint32_t *mrow = mring + r * CN_MSTRIDE;
+        uint32_t blk = s, q = s;                                    // next block of this lane, its ring block
+        for (uint32_t t = 0; t < nsteps; t++) {
+            const uint32_t lim = (t == 0 || NMODE == 2 || NMODE == 4 || NMODE >= 6) ? 0u : t >= nit ? iters : min(iters, wp[(t - 1) & 3][r] / 20u);
+            for (; __any(blk < lim);) {
+                if (blk < lim) {
+                    const uint32_t *bp = rrow + 5 * q;
+                    const uint32_t b = bp[1], c = bp[2], dd = bp[3], e = bp[4];
+                    uint32_t ec;
+                    asm("v_mul_lo_u32 %0, %1, %2" : "=v"(ec) : "v"(e), "s"(FH_C1));
+                    const uint32_t m0 = fh_m(c), m1 = fh_m(dd), m2 = fh_m(b + ec);
+                    uint32_t *mp = mrow + 3 * q;
+                    mp[0] = m0; mp[1] = m1; mp[2] = m2;
+                    if (q < CN_MBLK) { mp[3 * CN_NBLK] = m0; mp[3 * CN_NBLK + 1] = m1; mp[3 * CN_NBLK + 2] = m2; }
+                    blk += 4;
+                    q += 4;
+                    q = q >= CN_NBLK ? q - CN_NBLK : q;
+                }
+            }
+            lds_barrier();
+        }
+        lds_barrier();
+        return;
+    }
+
+    // ------------------------------- hashers -------------------------------
+    const uint32_t r = lane & (CN_ROWS - 1);                       // lanes >= 16 shadow lane & 15
+    uint32_t id; bool is_row;
+    const uint32_t *row = row_of(r, id, is_row);
+    const bool valid = lane < CN_ROWS && b0 + r < cnt;
+    FH fh{0, 0, 0};
+    uint32_t iters = 0;
+    const bool ok = cs_prologue<W>(d, id, is_row, row, fh, iters);
+    if (!ok && valid && wave == 0) atomicOr(d.err, E_SHORT);
+    const uint32_t *rrow = ring + r * CN_STRIDE + CS_PRE;
+    const uint32_t *mrow = mring + r * CN_MSTRIDE;
+    auto lim_h = [&](uint32_t t) -> uint32_t {                     // blocks premixed by the end of step t-1
+        if (t < 2 || NMODE == 2 || NMODE == 5 || (NMODE == 6 && wave == 4) || (NMODE == 7 && wave == 0)) return 0u;
+        if (t - 1 >= nit) return iters;
+        return min(iters, wp[(t - 2) & 3][r] / 20u);
+    };
+    uint32_t done = 0, bq = 0;                                     // bq = done mod CN_NBLK
+    auto take = [&](uint32_t lim, bool pred) {
+        const uint32_t n = pred ? (done < lim ? min(lim - done, 4u) : 0u) : 4u;
+        done += n;
+        bq += n;
+        bq = bq >= CN_NBLK ? bq - CN_NBLK : bq;
+    };
+    uint32_t h = fh.h, g = fh.g, fv = fh.f;
+    // per step: whole groups of 4 blocks while every lane has them, then predicated groups
+    if (wave == 4) {
+        auto group = [&](uint32_t lim, bool pred) {
+            const uint32_t *sp = rrow + 5 * bq, *mp = mrow + 3 * bq;
+            uint32_t a[4], e[4], md[4];
+#pragma unroll
+            for (int kk = 0; kk < 4; kk++) {
+                a[kk] = sp[5 * kk];
+                e[kk] = sp[5 * kk + 4];
+                md[kk] = mp[3 * kk + 1];
+            }
+#pragma unroll
+            for (int kk = 0; kk < 4; kk++) {
+                const uint32_t hn = fh_fold(h + a[kk], md[kk], e[kk]);
+                h = (!pred || done + kk < lim) ? hn : h;
+            }
+            take(lim, pred);
+        };
+        for (uint32_t t = 0; t < nsteps; t++) {
+            const uint32_t lim = lim_h(t);
+            while (__all(done + 4 <= lim)) group(lim, false);
+            while (__any(done < lim)) group(lim, true);
+            lds_barrier();
+        }
+    } else {
+        auto group = [&](uint32_t lim, bool pred) {
+            const uint32_t *sp = rrow + 5 * bq, *mp = mrow + 3 * bq;
+            uint32_t v[4][4], mc[4], mbe[4];
+#pragma unroll
+            for (int kk = 0; kk < 4; kk++) {
+#pragma unroll
+                for (int i = 0; i < 4; i++) v[kk][i] = sp[5 * kk + i];              // a, b, c, d
+                mc[kk] = mp[3 * kk];
+                mbe[kk] = mp[3 * kk + 2];
+            }
+#pragma unroll
+            for (int kk = 0; kk < 4; kk++) {
+                const uint32_t gn = fh_fold(g + v[kk][1], mc[kk], v[kk][0]);
+                uint32_t fn = fh_fold(fv + v[kk][2], mbe[kk], v[kk][3]);
+                fn += gn;
+                const bool act = !pred || done + kk < lim;
+                g = act ? gn + fn : g;
+                fv = act ? fn : fv;
+            }
+            take(lim, pred);
+        };
+        for (uint32_t t = 0; t < nsteps; t++) {
+            const uint32_t lim = lim_h(t);
+            while (__all(done + 4 <= lim)) group(lim, false);
+            while (__any(done < lim)) group(lim, true);
+            lds_barrier();
+        }
+        if (lane < CN_ROWS) { xgf[0][lane] = g; xgf[1][lane] = fv; }
+    }
+    lds_barrier();
+    if (wave == 4 && valid) {
+        fh.h = h; fh.g = xgf[0][lane]; fh.f = xgf[1][lane];
+        const uint32_t hv = ok ? fh.fin() : 0u;
+        if (is_row) {
+            d.cs[id] = hv;
+            d.dirty[id] = 0;
+            ctr_add(d, C_X_CS_ROWS, 1ull);
+        } else {
+            d.dense_cs[id - d.NL] = hv;
+        }
+    }
+}
+
 // NO for the address width W and the longest record tail of the handle's incarnation table
 constexpr int cs_no(int W, int maxtail) { return (3 + W + maxtail + 3) / 4; }
 
 template <int W, int MODE>
 void launch_cs_w(const DS &d, const uint32_t *list, const uint32_t *count, uint32_t grid, hipStream_t s,
-                 uint32_t *dbg = nullptr, uint32_t cap = 0) {
+                 uint32_t *dbg = nullptr, uint32_t cap = 0, uint32_t narrow_grid = 0) {
+    if (narrow_grid && (MODE == 0 || MODE >= 7)) {              // few rows: 16 rows per workgroup
+        constexpr int NM = MODE >= 7 ? MODE - 6 : 0;           // diagnostics modes 7..13
+        if (W == 19 && d.max_tail <= 21 && d.min_tail >= 19)
+            hipLaunchKernelGGL((k_checksum_n16<W, cs_no(W, 21), (W + 19) / 4, NM>), dim3(narrow_grid), dim3(320), 0, s, d,
+                               list, count, d.addrw, (const uint4 *)d.rtail);
+        else
+            hipLaunchKernelGGL((k_checksum_n16<W, cs_no(W, 24), (W + 7) / 4>), dim3(narrow_grid), dim3(320), 0, s, d,
+                               list, count, d.addrw, (const uint4 *)d.rtail);
+        return;
+    }
     // the common case: 13-digit incarnations (t0 = 1.5e12 ms): tails of 19..21 bytes
     if (W == 19 && d.max_tail <= 21 && d.min_tail >= 19)
         hipLaunchKernelGGL((k_checksum<W, cs_no(W, 21), (W + 19) / 4, MODE>), dim3(grid), dim3(256), 0, s, d, list, count,
@@ -410,11 +704,18 @@ void launch_cs_w(const DS &d, const uint32_t *list, const uint32_t *count, uint3
                            d.addrw, (const uint4 *)d.rtail, dbg, cap);
 }
 
-void launch_checksum(const DS &d, const uint32_t *list, const uint32_t *count, uint32_t maxn, hipStream_t s) {
-    const uint32_t grid = (maxn + CS_ROWS - 1) / CS_ROWS;
+// up to CS_NARROW_ROWS rows the launch is latency-bound (one row's chain): k_checksum_n16 (16 rows per
+// workgroup, ~40 % shorter); above, the 64-row throughput kernel
+constexpr uint32_t CS_NARROW_ROWS = 8192;
+
+void launch_checksum(const DS &d, const uint32_t *list, const uint32_t *count, uint32_t maxn, uint32_t nrows,
+                     hipStream_t s) {
+    const uint32_t n = std::min(maxn, nrows);
+    const uint32_t grid = (n + CS_ROWS - 1) / CS_ROWS;
     if (grid == 0) return;
+    const uint32_t ngrid = n <= CS_NARROW_ROWS ? (n + CN_ROWS - 1) / CN_ROWS : 0u;
     switch (d.W) {
-#define CS_CASE(Wv) case Wv: launch_cs_w<Wv, 0>(d, list, count, grid, s); break;
+#define CS_CASE(Wv) case Wv: launch_cs_w<Wv, 0>(d, list, count, grid, s, nullptr, 0, ngrid); break;
         CS_CASE(13) CS_CASE(14) CS_CASE(15) CS_CASE(16) CS_CASE(17) CS_CASE(18) CS_CASE(19) CS_CASE(20)
 #undef CS_CASE
     default: break;
@@ -431,7 +732,16 @@ void launch_checksum_dump(const DS &d, const uint32_t *list, const uint32_t *cou
 void launch_checksum_mode(const DS &d, const uint32_t *list, const uint32_t *count, uint32_t maxn, int mode, hipStream_t s) {
     const uint32_t grid = (maxn + CS_ROWS - 1) / CS_ROWS;
     if (grid == 0 || d.W != 19) return;
-    if (mode == 1) launch_cs_w<19, 1>(d, list, count, grid, s);
+    const uint32_t ngrid = (maxn + CN_ROWS - 1) / CN_ROWS;
+    if (mode == 6) launch_cs_w<19, 0>(d, list, count, grid, s, nullptr, 0, ngrid);
+    else if (mode == 7) launch_cs_w<19, 7>(d, list, count, grid, s, nullptr, 0, ngrid);
+    else if (mode == 8) launch_cs_w<19, 8>(d, list, count, grid, s, nullptr, 0, ngrid);
+    else if (mode == 9) launch_cs_w<19, 9>(d, list, count, grid, s, nullptr, 0, ngrid);
+    else if (mode == 10) launch_cs_w<19, 10>(d, list, count, grid, s, nullptr, 0, ngrid);
+    else if (mode == 11) launch_cs_w<19, 11>(d, list, count, grid, s, nullptr, 0, ngrid);
+    else if (mode == 12) launch_cs_w<19, 12>(d, list, count, grid, s, nullptr, 0, ngrid);
+    else if (mode == 13) launch_cs_w<19, 13>(d, list, count, grid, s, nullptr, 0, ngrid);
+    else if (mode == 1) launch_cs_w<19, 1>(d, list, count, grid, s);
     else if (mode == 2) launch_cs_w<19, 2>(d, list, count, grid, s);
     else if (mode == 4) launch_cs_w<19, 4>(d, list, count, grid, s);
     else if (mode == 5) launch_cs_w<19, 5>(d, list, count, grid, s);

@@ -588,7 +588,7 @@ int checksum_dirty(swimsim *h, int mode) {
     hipLaunchKernelGGL(k_list, dim3(blocks_for_threads(h->NL)), dim3(256), 0, h->s, h->d, mode, h->tgt, h->failed,
                        h->list, h->cnt);
     if (mode != 0) {
-        launch_checksum(h->d, h->list, h->cnt, h->NL, h->s);
+        launch_checksum(h->d, h->list, h->cnt, h->NL, ~0u, h->s);
         return 0;
     }
     uint32_t *hn = h->hinfo + 8;
@@ -596,7 +596,7 @@ int checksum_dirty(swimsim *h, int mode) {
     HIPCHK(h, hipStreamSynchronize(h->s));
     const uint32_t n = *hn;
     if (n < 2) {
-        launch_checksum(h->d, h->list, h->cnt, n, h->s);
+        launch_checksum(h->d, h->list, h->cnt, n, n, h->s);
         return 0;
     }
     hipLaunchKernelGGL(k_fp_keys, dim3(blocks_for_threads(n)), dim3(256), 0, h->s, h->d, h->list, n, h->keys, h->fpv);
@@ -611,7 +611,9 @@ int checksum_dirty(swimsim *h, int mode) {
                        h->dup_of);
     hipLaunchKernelGGL(k_list_flagged, dim3(blocks_for_threads(h->NL)), dim3(256), 0, h->s, h->NL, h->hflag, h->fplist,
                        h->fpcnt);
-    launch_checksum(h->d, h->fplist, h->fpcnt, n, h->s);
+    HIPCHK(h, hipMemcpyAsync(hn + 1, h->fpcnt, 4, hipMemcpyDeviceToHost, h->s));   // rows left after dedup:
+    HIPCHK(h, hipStreamSynchronize(h->s));                                         // picks the variant
+    launch_checksum(h->d, h->fplist, h->fpcnt, n, hn[1], h->s);
     hipLaunchKernelGGL(k_fp_copy, dim3(blocks_for_threads(n)), dim3(256), 0, h->s, h->d, h->fpv_s, n, h->dup_of);
     return 0;
 }
@@ -641,7 +643,10 @@ int resolve_deferred(swimsim *h, int phase, MsgDesc *rdesc, uint32_t maxn) {
     }
     {
         Scope sc(h, F_CHECKSUM);
-        launch_checksum(h->d, h->list, h->cnt, maxlist, h->s);
+        uint32_t *hc = h->hinfo + 10;
+        HIPCHK(h, hipMemcpyAsync(hc, h->cnt, 4, hipMemcpyDeviceToHost, h->s));
+        HIPCHK(h, hipStreamSynchronize(h->s));
+        launch_checksum(h->d, h->list, h->cnt, maxlist, *hc, h->s);
     }
     if (remote) {
         hipLaunchKernelGGL(k_x_csresp, dim3(blocks_for_threads(h->keycap)), dim3(256), 0, h->s, h->d, h->csreq,
@@ -703,7 +708,7 @@ bool host_reach(swimsim *h, uint32_t a, uint32_t b) { return h->live[a] && h->li
 
 int ensure_clean_checksum(swimsim *h, uint32_t ol) {
     hipLaunchKernelGGL(k_list_one, dim3(1), dim3(64), 0, h->s, h->list, h->cnt, ol, h->d);
-    launch_checksum(h->d, h->list, h->cnt, 1, h->s);
+    launch_checksum(h->d, h->list, h->cnt, 1, 1, h->s);
     return 0;
 }
 

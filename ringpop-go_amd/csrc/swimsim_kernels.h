@@ -3,8 +3,10 @@
 #include "swimsim_device.h"
 
 namespace swimdev {
-// maxn bounds the row count on the device
-void launch_checksum(const DS &d, const uint32_t *list, const uint32_t *count, uint32_t maxn, hipStream_t s);
+// maxn bounds the row count on the device; nrows is the count when the host knows it (else ~0u): it
+// picks the latency (few rows) or the throughput variant
+void launch_checksum(const DS &d, const uint32_t *list, const uint32_t *count, uint32_t maxn, uint32_t nrows,
+                     hipStream_t s);
 void launch_checksum_dump(const DS &d, const uint32_t *list, const uint32_t *count, uint32_t *dbg, uint32_t cap,
                           hipStream_t s);
 void launch_checksum_mode(const DS &d, const uint32_t *list, const uint32_t *count, uint32_t maxn, int mode,
