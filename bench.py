@@ -27,21 +27,30 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "ringpop-go_amd"))
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-# kernel family (swimsim_kernel_times) -> kernel symbol in the rocprofv3 PMC summary
-FAMILY_KERNEL = {"checksum": "swimdev::k_checksum<19, 11, 9, 0>", "recv_merge": "swimdev::k_recv",
-                 "issue": "swimdev::k_issue", "resp_merge": "swimdev::k_resp", "timers": "swimdev::k_timers"}
-PMC_SUMMARY = os.path.join(REPO, "profiles", "r01_pmc_traffic.json")
+VALU_PEAK_GINST = 256 * 4 * 2.4 / 2  # wave-instructions/ns: 1024 SIMDs, one wave64 VALU op per 2 cycles at 2.4 GHz
+# kernel family (swimsim_kernel_times) -> kernel symbols in the rocprofv3 PMC summary
+FAMILY_KERNELS = {"checksum": ["swimdev::k_checksum<19, 11, 9, 0>", "swimdev::k_checksum_n16<19, 11, 9, 0>"],
+                  "recv_merge": ["swimdev::k_recv"], "issue": ["swimdev::k_issue"], "resp_merge": ["swimdev::k_resp"],
+                  "timers": ["swimdev::k_timers"]}
+PMC_SUMMARY = os.path.join(REPO, "profiles", "r01_pmc_summary.json")
 
 
-def pmc_traffic(family):
-    """HBM bytes per launch of the family's main kernel from the committed PMC pass of this bench
-    (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate runs; tools/pmc_summary.py), or None."""
+def pmc_family(family):
+    """Per-launch PMC figures of the family's kernels (launch-weighted over the committed PMC passes of this
+    bench: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / SQ_INSTS_VALU..., separate runs; tools/pmc_summary.py),
+    or None."""
     try:
         with open(PMC_SUMMARY) as f:
-            t = json.load(f)[FAMILY_KERNEL[family]]
-        return round(t["fetch_bytes_per_launch"] + t["write_bytes_per_launch"], 1)
+            t = json.load(f)
+        ks = [t[k] for k in FAMILY_KERNELS[family] if k in t]
     except (OSError, KeyError, ValueError):
         return None
+    n = sum(k["launches"] for k in ks)
+    if not n:
+        return None
+    tot = lambda key: sum(k.get(key, 0.0) * k["launches"] for k in ks) / n
+    return {"traffic": round(tot("fetch_bytes_per_launch") + tot("write_bytes_per_launch"), 1),
+            "valu_insts": tot("sq_insts_valu_per_launch"), "lds_insts": tot("sq_insts_lds_per_launch")}
 
 
 def dist_env():
@@ -152,6 +161,7 @@ def main():
     fam, info = dominant
     per_launch_bytes = info["alg_bytes"] / max(1, info["launches"])
     achieved = per_launch_bytes / (info["avg_ms"] * 1e-3) / 1e9 if info["avg_ms"] > 0 else 0.0
+    pmc = pmc_family(fam)
     merge = kt.get("recv_merge", {})
     merge_gbps = (merge.get("alg_bytes", 0) / max(1, merge.get("launches", 1))) / (merge.get("avg_ms", 1) * 1e-3) / 1e9 \
         if merge.get("avg_ms", 0) > 0 else 0.0
@@ -176,13 +186,21 @@ def main():
                        "parallelism": (f"observer-row shards x{ws} over " + ("host transport (diagnostic)" if args.host_transport
                                                                               else "RCCL")) if ws > 1 else "1 GPU"},
             "roofline": {"bound": "hbm", "kernel": fam, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": pmc_traffic(fam),
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5),
+                         "traffic": pmc["traffic"] if pmc else None,
                          "traffic_unit": "bytes per launch (FETCH_SIZE + WRITE_SIZE, " + os.path.basename(PMC_SUMMARY) + ")",
                          "avg_launch_ms": round(info["avg_ms"], 5), "launches": info["launches"],
                          "merge_kernel_GBps": round(merge_gbps, 2)},
             "kernel_ms": {k: round(v["avg_ms"] * v["launches"], 3) for k, v in kt.items()},
             "counters": counters,
         }
+        if pmc and pmc["valu_insts"] and info["avg_ms"] > 0:
+            # the checksum is integer-VALU work: its instruction rate against the chip's VALU issue peak
+            rate = pmc["valu_insts"] / (info["avg_ms"] * 1e6)
+            line["roofline"]["valu"] = {"achieved": round(rate, 2), "peak": VALU_PEAK_GINST, "unit": "G wave-instr/s",
+                                        "frac": round(rate / VALU_PEAK_GINST, 4),
+                                        "valu_insts_per_launch": round(pmc["valu_insts"]),
+                                        "lds_insts_per_launch": round(pmc["lds_insts"])}
         if ws > 1:
             line["exchange"] = {"bytes_rank0": shard["exchanged_bytes"], "exchanges_rank0": shard["exchanges"]}
         if ws == 1 and not args.no_cpu_baseline:

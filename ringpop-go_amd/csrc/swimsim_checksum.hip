@@ -704,9 +704,9 @@ void launch_cs_w(const DS &d, const uint32_t *list, const uint32_t *count, uint3
                            d.addrw, (const uint4 *)d.rtail, dbg, cap);
 }
 
-// up to CS_NARROW_ROWS rows the launch is latency-bound (one row's chain): k_checksum_n16 (16 rows per
+// up to CS_NARROW_ROWS rows (measured crossover) the launch is latency-bound: k_checksum_n16 (16 rows per
 // workgroup, ~40 % shorter); above, the 64-row throughput kernel
-constexpr uint32_t CS_NARROW_ROWS = 8192;
+constexpr uint32_t CS_NARROW_ROWS = 12288;
 
 void launch_checksum(const DS &d, const uint32_t *list, const uint32_t *count, uint32_t maxn, uint32_t nrows,
                      hipStream_t s) {

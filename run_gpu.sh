@@ -42,6 +42,10 @@ for mode in "$@"; do
     timeout -k 10 -s KILL 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run \
       --output-format csv -- python3 bench.py --no-cpu-baseline > gpurun_out/pmc_write.log 2>&1
     rc=$?; echo "pmc write rc=$rc" >> gpurun_out/pmc_write.log; [ $rc -eq 0 ] || exit $rc
+    timeout -k 10 -s KILL 400 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVES GRBM_GUI_ACTIVE --kernel-trace \
+      -d gpurun_out/pmc_valu -o run --output-format csv -- python3 bench.py --no-cpu-baseline > gpurun_out/pmc_valu.log 2>&1
+    rc=$?; echo "pmc valu rc=$rc" >> gpurun_out/pmc_valu.log; [ $rc -eq 0 ] || exit $rc
+    python3 tools/pmc_summary.py gpurun_out/pmc_summary.json gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc_valu
     ;;
   esac
 done

@@ -1,9 +1,11 @@
-"""Per-kernel, per-launch HBM traffic from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py.
+"""Per-kernel, per-launch PMC figures from rocprofv3 --pmc passes of bench.py (one directory per pass).
 
-usage: python tools/pmc_summary.py <fetch_dir> <write_dir> <out.json>
-FETCH_SIZE and WRITE_SIZE are in KiB (TCC_EA0_RDREQ/WRREQ-derived). MI355X_MICROARCH.md §HBM: on gfx950
+usage: python tools/pmc_summary.py <out.json> <pass_dir> [<pass_dir> ...]
+Every counter of every pass is averaged per launch of each kernel. FETCH_SIZE and WRITE_SIZE are in
+KiB (TCC_EA0_RDREQ/WRREQ-derived) and are reported as bytes. MI355X_MICROARCH.md §HBM: on gfx950
 FETCH_SIZE reports half the bytes of a wide coalesced 16-B/lane streaming read (doubled here as
 fetch_bytes_wide_corrected); other access widths are uncalibrated, so the raw figure is kept beside it.
+SQ_INSTS_* count wave-instructions; GRBM_GUI_ACTIVE is summed over the 8 XCDs (÷ 8 = GPU cycles).
 """
 import collections
 import csv
@@ -11,26 +13,33 @@ import json
 import sys
 
 
-def load(path):
-    agg = collections.defaultdict(lambda: [0, 0.0])
+def load(path, agg):
     for x in csv.DictReader(open(f"{path}/run_counter_collection.csv")):
         k = x["Kernel_Name"].split("(")[0].replace("void ", "").strip()
-        agg[k][0] += 1
-        agg[k][1] += float(x["Counter_Value"]) * 1024.0
-    return agg
+        c = x["Counter_Name"]
+        agg[k][c][0].add(x["Dispatch_Id"])
+        agg[k][c][1] += float(x["Counter_Value"])
 
 
 def main():
-    fetch, write = load(sys.argv[1]), load(sys.argv[2])
+    agg = collections.defaultdict(lambda: collections.defaultdict(lambda: [set(), 0.0]))
+    for p in sys.argv[2:]:
+        load(p, agg)
     out = {}
-    for k in sorted(set(fetch) | set(write)):
-        nf, vf = fetch.get(k, [0, 0.0])
-        nw, vw = write.get(k, [0, 0.0])
-        n = max(nf, nw, 1)
-        out[k] = {"launches": n, "fetch_bytes_per_launch": vf / max(nf, 1),
-                  "fetch_bytes_wide_corrected_per_launch": 2 * vf / max(nf, 1),
-                  "write_bytes_per_launch": vw / max(nw, 1)}
-    json.dump(out, open(sys.argv[3], "w"), indent=1)
+    for k in sorted(agg):
+        e = {}
+        for c, (ids, v) in agg[k].items():
+            n = max(len(ids), 1)
+            e["launches"] = max(e.get("launches", 0), n)
+            if c == "FETCH_SIZE":
+                e["fetch_bytes_per_launch"] = v * 1024.0 / n
+                e["fetch_bytes_wide_corrected_per_launch"] = 2 * v * 1024.0 / n
+            elif c == "WRITE_SIZE":
+                e["write_bytes_per_launch"] = v * 1024.0 / n
+            else:
+                e[c.lower() + "_per_launch"] = v / n
+        out[k] = e
+    json.dump(out, open(sys.argv[1], "w"), indent=1)
 
 
 if __name__ == "__main__":
