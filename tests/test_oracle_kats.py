@@ -620,3 +620,45 @@ def test_checksum_faithful_equals_static_order():
     assert a.checksum_string(0) == b.checksum_string(0)
     s = b.checksum_string(0).decode()
     assert s.startswith("10.000.000.000:7000alive1500000000000;")
+
+
+# ---------------------------------------------------------------------------------------------
+# Fingerprint32 values as the reference's hashring tests see them. hashring.New wraps the hash as
+# int(Fingerprint32(s)) (hashring/hashring.go:76-85); replicas are hash(server + decimal(i))
+# (hashring.go:148-155); the tree keeps the first node of a value (rbtree.go:122-126) and
+# LookupNUniqueAt walks values >= hash, then wraps to 0 (hashring.go:287-301, rbtree.go:262-286).
+# These assertions depend on the actual hash values, so they pin the restated FarmHash (weakly: a
+# random function passes TestLookupDistribution with probability ~0.46).
+# ---------------------------------------------------------------------------------------------
+def _ring(servers, replicas):
+    nodes = {}
+    for s in servers:
+        for i in range(replicas):
+            nodes.setdefault(fingerprint32(f"{s}{i}".encode()), s)
+    return sorted(nodes.items())
+
+
+def _lookup(ring, key):
+    h = fingerprint32(key.encode())
+    for v, s in ring:
+        if v >= h:
+            return s
+    return ring[0][1]
+
+
+def _gen_addresses(host, lo, hi):   # hashring_test.go:325-331
+    return [f"127.0.0.{host}:{3000 + i}" for i in range(lo, hi + 1)]
+
+
+def test_hashring_lookup_distribution_kat():
+    """hashring_test.go:180-199: keys "0".."39" on 1000 servers x 5 replicas land on 40 distinct servers."""
+    ring = _ring(_gen_addresses(1, 1, 1000), 5)
+    owners = {_lookup(ring, str(i)) for i in range(40)}
+    assert len(owners) == 40
+
+
+def test_hashring_lookup_loop_around_kat():
+    """hashring_test.go:266-285: with 10 servers x 1 replica, "a random key" does not land on the first
+    tree node (the test's precondition, asserted there)."""
+    ring = _ring(_gen_addresses(1, 1, 10), 1)
+    assert _lookup(ring, "a random key") != ring[0][1]
