@@ -88,6 +88,9 @@ struct DS {
     uint32_t *dense_len;    // checksum-string length of each snapshot
     int32_t *dense_last;    // last included member of each snapshot (-2: rescan)
     uint32_t *dense_cs;     // checksum of each snapshot (deferred full-sync decisions)
+    // slots [dense_cap, dense_cap + snap_cap) of the dense arrays hold the round-end snapshots whose
+    // checksums are hashed on the side stream while the next round runs
+    uint32_t *cpslot;       // [NL] dense slot whose dense_cs will hold the row's checksum, or SRC_NONE
     uint32_t *clen;         // [NL] checksum-string length of each row
     int32_t *clast;         // [NL] last included member (-2: rescan)
     unsigned long long *fp; // [NL] row fingerprint: sum over members of fpmix(m, member word), kept by the merges

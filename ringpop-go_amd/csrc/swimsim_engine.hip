@@ -226,6 +226,13 @@ struct swimsim {
     bool fast_cs = false;
     int device = 0;
     hipStream_t s = nullptr;
+    // phase C of a round can hash its rows on a side stream while the next round runs
+    hipStream_t side = nullptr;
+    hipEvent_t ev_snap = nullptr, ev_side = nullptr;
+    bool cs_async = true, side_pending = false;
+    uint32_t snap_cap = 0;
+    uint32_t *side_ids = nullptr, *side_cnt = nullptr;
+    uint2 *side_map = nullptr;
     DS d{};
     // host mirrors
     std::vector<uint8_t> live;
@@ -329,17 +336,18 @@ hipEvent_t take_event(swimsim *h) {
 struct Scope {
     swimsim *h;
     int fam;
+    hipStream_t st;
     hipEvent_t a{}, b{};
-    Scope(swimsim *h_, int f) : h(h_), fam(f) {
+    Scope(swimsim *h_, int f, hipStream_t st_ = nullptr) : h(h_), fam(f), st(st_ ? st_ : h_->s) {
         if (h->timing) {
             a = take_event(h);
-            hipEventRecord(a, h->s);
+            hipEventRecord(a, st);
         }
     }
     ~Scope() {
         if (h->timing) {
             b = take_event(h);
-            hipEventRecord(b, h->s);
+            hipEventRecord(b, st);
             h->pending.push_back(Timed{fam, a, b});
         }
     }
@@ -587,13 +595,25 @@ int shard_sum(swimsim *h, uint64_t v, uint64_t *out) {
 // row, and equal rows copy its checksum (k_fp_*).
 // one FarmHash dispatch over the rows listed (count on the device; nrows = the count if the host
 // knows it, else ~0u), timed as F_CHECKSUM
-void hash_rows(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t maxn, uint32_t nrows) {
+void hash_rows(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t maxn, uint32_t nrows,
+               hipStream_t st = nullptr) {
     if (std::min(maxn, nrows) == 0) return;
-    Scope sc(h, F_CHECKSUM);
-    launch_checksum(h->d, list, cnt, maxn, nrows, h->s);
+    Scope sc(h, F_CHECKSUM, st);
+    launch_checksum(h->d, list, cnt, maxn, nrows, st ? st : h->s);
 }
 
-int checksum_dirty(swimsim *h, int mode) {
+// order the main stream after the side-stream checksums of the previous phase C; from here on every
+// row's cs[] is current and no row refers to a side slot
+int sync_side(swimsim *h) {
+    if (!h->side_pending) return 0;
+    HIPCHK(h, hipStreamWaitEvent(h->s, h->ev_side, 0));
+    HIPCHK(h, hipMemsetAsync(h->d.cpslot, 0xFF, (size_t)h->NL * 4, h->s));
+    h->side_pending = false;
+    return 0;
+}
+
+int checksum_dirty(swimsim *h, int mode, bool async = false) {
+    if (int rc = sync_side(h)) return rc;
     HIPCHK(h, hipMemsetAsync(h->cnt, 0, 4, h->s));
     {
         Scope sc(h, F_CSPREP);
@@ -608,7 +628,27 @@ int checksum_dirty(swimsim *h, int mode) {
     HIPCHK(h, hipMemcpyAsync(hn, h->cnt, 4, hipMemcpyDeviceToHost, h->s));
     HIPCHK(h, hipStreamSynchronize(h->s));
     const uint32_t n = *hn;
+    // async: snapshot the rows to hash, mark every dirty row clean (cpslot = the slot carrying its
+    // checksum) and hash the snapshots on the side stream; the round reads cs[] only after sync_side
+    auto go_side = [&](const uint32_t *rows, uint32_t n2, const uint32_t *vals, const uint32_t *dups) -> int {
+        {
+            Scope sc(h, F_CSPREP);
+            hipLaunchKernelGGL(k_snap_rows, dim3(blocks_for_waves(std::max(n2, 1u))), dim3(256), 0, h->s, h->d, rows, n2,
+                               h->side_ids, h->side_cnt);
+            hipLaunchKernelGGL(k_snap_dups, dim3(blocks_for_threads(n)), dim3(256), 0, h->s, h->d, vals, n, dups,
+                               h->side_map);
+        }
+        HIPCHK(h, hipEventRecord(h->ev_snap, h->s));
+        HIPCHK(h, hipStreamWaitEvent(h->side, h->ev_snap, 0));
+        hash_rows(h, h->side_ids, h->side_cnt, n2, n2, h->side);
+        hipLaunchKernelGGL(k_side_scatter, dim3(blocks_for_threads(n)), dim3(256), 0, h->side, h->d, h->side_map, n, n2);
+        HIPCHK(h, hipEventRecord(h->ev_side, h->side));
+        h->side_pending = true;
+        return 0;
+    };
+    const bool side_ok = async && h->cs_async;
     if (n < 2) {
+        if (n == 1 && side_ok && h->snap_cap >= 1) return go_side(h->list, 1, h->list, nullptr);
         hash_rows(h, h->list, h->cnt, n, n);
         return 0;
     }
@@ -629,6 +669,7 @@ int checksum_dirty(swimsim *h, int mode) {
         HIPCHK(h, hipMemcpyAsync(hn + 1, h->fpcnt, 4, hipMemcpyDeviceToHost, h->s));   // rows left after dedup:
     }
     HIPCHK(h, hipStreamSynchronize(h->s));                                         // picks the variant
+    if (side_ok && hn[1] <= h->snap_cap) return go_side(h->fplist, hn[1], h->fpv_s, h->dup_of);
     hash_rows(h, h->fplist, h->fpcnt, n, hn[1]);
     Scope sc(h, F_CSPREP);
     hipLaunchKernelGGL(k_fp_copy, dim3(blocks_for_threads(n)), dim3(256), 0, h->s, h->d, h->fpv_s, n, h->dup_of);
@@ -642,6 +683,10 @@ int checksum_dirty(swimsim *h, int mode) {
 // shard about). Sharded phases D and Q2 are collective: two exchanges carry the requests and answers.
 int resolve_deferred(swimsim *h, int phase, MsgDesc *rdesc, uint32_t maxn) {
     const bool remote = h->G > 1 && phase != 2;
+    // k_recv_finish and k_x_csresp read checksums the side stream may still be computing (clean
+    // receivers and pending senders refer to side slots): wait for it unless nothing was deferred
+    if (remote || phase == 2)
+        if (int rc = sync_side(h)) return rc;
     uint32_t maxlist = 2 * maxn;
     {
         Scope sc(h, F_CSPREP);
@@ -661,7 +706,10 @@ int resolve_deferred(swimsim *h, int phase, MsgDesc *rdesc, uint32_t maxn) {
     {
         uint32_t *hc = h->hinfo + 10;
         HIPCHK(h, hipMemcpyAsync(hc, h->cnt, 4, hipMemcpyDeviceToHost, h->s));
+        HIPCHK(h, hipMemcpyAsync(hc + 1, h->defer_cnt, 4, hipMemcpyDeviceToHost, h->s));
         HIPCHK(h, hipStreamSynchronize(h->s));
+        if (hc[1])
+            if (int rc = sync_side(h)) return rc;
         hash_rows(h, h->list, h->cnt, maxlist, *hc);
     }
     if (remote) {
@@ -766,6 +814,7 @@ int ping_with(swimsim *h, uint32_t o, uint32_t t, int slot) {
 // discoverProviderHealer.Heal on observer o (heal_via_discover_provider.go:120-177). o's shard
 // decides; the target's membership comes from the target's shard. Collective when sharded.
 int do_heal(swimsim *h, uint32_t o, std::vector<int32_t> *ret) {
+    if (int rc = sync_side(h)) return rc;
     const uint32_t root = owner_host(h, o);
     const bool me = h->rank == root;
     const uint32_t ol = o - h->lo;
@@ -1011,8 +1060,8 @@ int step_one(swimsim *h, const swimsim_event *ev, size_t nev) {
         hipLaunchKernelGGL(k_jobs_reset, dim3(blocks_for_threads(std::max(h->NL, h->N))), dim3(256), 0, h->s, h->d,
                            h->need);
     }
-    // ---- C: checksums of dirty rows ----
-    if (int rc = checksum_dirty(h, 0)) return rc;
+    // ---- C: checksums of dirty rows (on the side stream when few rows remain after dedup) ----
+    if (int rc = checksum_dirty(h, 0, true)) return rc;
     h->round++;
     h->host_ctr[SWIMSIM_C_ROUNDS]++;
     HIPCHK(h, hipGetLastError());
@@ -1147,10 +1196,14 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
         h->err = "hipSetDevice failed (no usable MI355X device)";
         return bail(SWIMSIM_EHIP);
     }
-    if (hipStreamCreateWithFlags(&h->s, hipStreamNonBlocking) != hipSuccess) {
-        h->err = "hipStreamCreate failed";
+    if (hipStreamCreateWithFlags(&h->s, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&h->ev_snap, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&h->ev_side, hipEventDisableTiming) != hipSuccess) {
+        h->err = "hipStreamCreate / hipEventCreate failed";
         return bail(SWIMSIM_EHIP);
     }
+    if (const char *v = getenv("SWIMSIM_CS_ASYNC")) h->cs_async = atoi(v) != 0;
     DS &d = h->d;
     d.N = h->N; d.NP = h->NP; d.NL = h->NL; d.lo = h->lo;
     d.NB = h->NP / 64;
@@ -1172,8 +1225,10 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
         (rc = dalloc(h, &d.dbit, (size_t)h->NL * d.NBIT, "dbit")) || (rc = dalloc(h, &d.tblk, (size_t)h->NL * d.NB, "tblk")) ||
         (rc = dalloc(h, &d.live, h->N, "live")) || (rc = dalloc(h, &d.part, h->N, "part")) ||
         (rc = dalloc(h, &d.ctr, (size_t)CTR_SHARDS * CTR_STRIDE, "counters")) || (rc = dalloc(h, &d.err, 4, "err")) ||
-        (rc = dalloc(h, &d.clen, h->NL, "clen")) || (rc = dalloc(h, &d.clast, h->NL, "clast")))
+        (rc = dalloc(h, &d.clen, h->NL, "clen")) || (rc = dalloc(h, &d.clast, h->NL, "clast")) ||
+        (rc = dalloc(h, &d.cpslot, h->NL, "cpslot")))
         return bail(rc);
+    hipMemset(d.cpslot, 0xFF, (size_t)h->NL * 4);
     // address words
     {
         std::vector<uint32_t> aw((size_t)h->N * 6, 0u);
@@ -1204,11 +1259,17 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
         hipMemGetInfo(&freeb, &totalb);
         const uint64_t by_mem = (uint64_t)(freeb / 3) / (4ull * h->NP);
         d.dense_cap = (uint32_t)std::max<uint64_t>(64, std::min<uint64_t>(2ull * h->NL + 64, by_mem));
+        // side-stream checksum snapshots (latency-bound phase C launches only), up to 1/8 of the free HBM
+        const uint64_t snap_mem = (uint64_t)(freeb / 8) / (4ull * h->NP);
+        h->snap_cap = h->cs_async ? (uint32_t)std::min<uint64_t>(std::min<uint64_t>(CS_NARROW_ROWS, h->NL), snap_mem) : 0u;
     }
-    if ((rc = dalloc(h, &d.dense, (size_t)d.dense_cap * h->NP, "dense snapshots")) ||
-        (rc = dalloc(h, &d.dense_meta, d.dense_cap, "dense meta")) || (rc = dalloc(h, &d.dense_cur, 1, "dense cursor")) ||
-        (rc = dalloc(h, &d.dense_len, d.dense_cap, "dense len")) || (rc = dalloc(h, &d.dense_last, d.dense_cap, "dense last")) ||
-        (rc = dalloc(h, &d.dense_cs, d.dense_cap, "dense cs")))
+    const size_t nslots = (size_t)d.dense_cap + h->snap_cap;
+    if ((rc = dalloc(h, &d.dense, nslots * h->NP, "dense snapshots")) ||
+        (rc = dalloc(h, &d.dense_meta, nslots, "dense meta")) || (rc = dalloc(h, &d.dense_cur, 1, "dense cursor")) ||
+        (rc = dalloc(h, &d.dense_len, nslots, "dense len")) || (rc = dalloc(h, &d.dense_last, nslots, "dense last")) ||
+        (rc = dalloc(h, &d.dense_cs, nslots, "dense cs")) ||
+        (rc = dalloc(h, &h->side_ids, std::max<uint32_t>(h->snap_cap, 1), "side ids")) ||
+        (rc = dalloc(h, &h->side_cnt, 1, "side count")) || (rc = dalloc(h, &h->side_map, h->NL, "side map")))
         return bail(rc);
     // work buffers. Message descriptors are indexed by global observer id (a shard imports the
     // messages of remote senders there); inbox arrays hold local pairs plus imported ones.
@@ -1282,6 +1343,7 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
 
 int swimsim_destroy(swimsim_t *h) {
     if (!h) return SWIMSIM_OK;
+    if (h->side) hipStreamSynchronize(h->side);
     if (h->s) hipStreamSynchronize(h->s);
     for (auto &t : h->pending) { hipEventDestroy(t.a); hipEventDestroy(t.b); }
     for (auto e : h->evpool) hipEventDestroy(e);
@@ -1290,6 +1352,9 @@ int swimsim_destroy(swimsim_t *h) {
     if (h->rbuf) hipFree(h->rbuf);
     h->xp.reset();
     if (h->hinfo) hipHostFree(h->hinfo);
+    if (h->ev_snap) hipEventDestroy(h->ev_snap);
+    if (h->ev_side) hipEventDestroy(h->ev_side);
+    if (h->side) hipStreamDestroy(h->side);
     if (h->s) hipStreamDestroy(h->s);
     delete h;
     return SWIMSIM_OK;
@@ -1362,6 +1427,7 @@ int swimsim_step(swimsim_t *h, uint32_t nrounds, const swimsim_event *events, si
         if (int rc = ensure_ecap(h, h->round + 1)) return rc;
         if (int rc = step_one(h, events, nevents)) return rc;
     }
+    if (int rc = sync_side(h)) return rc;    // a step call returns with every checksum current
     if (int rc = check_err(h)) return rc;
     drain_timing(h);
     return SWIMSIM_OK;

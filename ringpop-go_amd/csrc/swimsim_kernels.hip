@@ -677,11 +677,13 @@ __global__ void k_issue(DS d, int mode, const int32_t *tgt, const uint8_t *faile
     if (sS && d.dirty[ol]) {
         MsgDesc sn;
         if (wave_snapshot(d, ol, o, sn)) slot = sn.off_lo;
+    } else if (sS) {
+        slot = d.cpslot[ol];                                     // clean, checksum still on the side stream
     }
     if (lane_id() == 0) {
         sdesc[o] = md;                                               // message descriptors are indexed by
         sI[o] = d.mw[(size_t)ol * d.NP + o] >> 3;                    // global sender id (remote senders'
-        sC[o] = d.cs[ol];                                            // messages are imported there)
+        sC[o] = slot == SRC_NONE ? d.cs[ol] : 0u;                    // messages are imported there)
         if (sS) sS[o] = slot;
         if (mode == 0) {
             ctr_add(d, C_PINGS, 1ull);
@@ -832,11 +834,13 @@ __device__ void recv_one(const DS &d, const RecvArgs &a, uint32_t j, uint32_t se
         const uint32_t scs = a.sC[sender_row];
         const uint32_t sslot = a.sS ? a.sS[sender_row] : SRC_NONE;
         const bool rdirty = d.dirty[ol] != 0;
-        if (rdirty || sslot != SRC_NONE) {
+        const uint32_t rpend = rdirty ? SRC_NONE : d.cpslot[ol];   // clean; its checksum is on the side stream
+        if (rdirty || rpend != SRC_NONE || sslot != SRC_NONE) {
             // a checksum is not known yet: snapshot the receiver (the full-sync payload if the decision goes that
             // way) and decide after the batched checksum of every deferred snapshot
             if (wave_snapshot(d, ol, j, resp) && lane_id() == 0) {
-                if (!rdirty) d.dense_cs[resp.off_lo] = d.cs[ol];
+                if (rpend != SRC_NONE) d.dense_meta[resp.off_lo].w = rpend + 1u;   // read after the side stream
+                else if (!rdirty) d.dense_cs[resp.off_lo] = d.cs[ol];
                 a.defer[atomicAdd(a.defer_cnt, 1u)] =
                     make_uint4(resp_idx | (rdirty ? 0x80000000u : 0u), resp.off_lo, sslot != SRC_NONE ? sslot : scs,
                                pair | (sslot != SRC_NONE ? 0x80000000u : 0u));
@@ -891,6 +895,8 @@ __global__ void k_recv_finish(DS d, const uint4 *defer, const uint32_t *defer_cn
     const uint32_t scs = !(e.w & 0x80000000u) ? e.z : (e.z & 0x80000000u) ? rcs[sender] : d.dense_cs[e.z];
     MsgDesc resp;
     resp.kind = 0; resp.len = 0; resp.off_lo = resp.off_hi = 0;
+    const uint32_t alias = d.dense_meta[slot].w;                   // receiver clean, hashed on the side stream
+    if (alias) d.dense_cs[slot] = d.dense_cs[alias - 1u];
     if (d.dense_cs[slot] != scs) {
         resp.kind = 1; resp.off_lo = slot; resp.len = d.dense_meta[slot].z;
         ctr_add(d, phase == 1 ? C_FULL_SYNCS_PINGREQ : C_FULL_SYNCS, 1ull);
@@ -913,7 +919,8 @@ __global__ void k_defer_ids(DS d, const uint4 *defer, const uint32_t *defer_cnt,
     if (i >= *defer_cnt) return;
     const uint4 e = defer[i];
     if (e.x & 0x80000000u) list[atomicAdd(cnt, 1u)] = d.NL + e.y;
-    if ((e.w & 0x80000000u) && !(e.z & 0x80000000u)) list[atomicAdd(cnt, 1u)] = d.NL + e.z;   // local pending
+    if ((e.w & 0x80000000u) && !(e.z & 0x80000000u) && e.z < d.dense_cap)                  // local pending
+        list[atomicAdd(cnt, 1u)] = d.NL + e.z;                     // (slots >= dense_cap: side stream)
 }
 
 // tryStartReverseFullSync (disseminator.go:257-278) in inbox order: at most maxjobs per receiver
@@ -1068,6 +1075,61 @@ __global__ void k_fp_copy(DS d, const uint32_t *vals, uint32_t n, const uint32_t
     d.cs[row] = d.cs[h];
     d.dirty[row] = 0;
     ctr_add(d, C_X_CS_DUP, 1ull);
+}
+
+// ---------------------------------------------------------------------------------------------
+// phase C on the side stream: the rows left after dedup are copied into dense slots
+// [dense_cap, dense_cap + n) (one wave per row) and hashed there while the next round runs on the main
+// stream; every listed row (dedup heads and duplicates) is marked clean with cpslot = the slot whose
+// dense_cs carries its checksum. k_side_scatter writes cs[] when the hash is done.
+// ---------------------------------------------------------------------------------------------
+__global__ void k_snap_rows(DS d, const uint32_t *rows, uint32_t n, uint32_t *ids, uint32_t *idcnt) {
+    const uint32_t k = wave_gid();
+    if (k == 0 && lane_id() == 0) *idcnt = n;
+    if (k >= n) return;
+    const uint32_t ol = rows[k], slot = d.dense_cap + k;
+    const uint4 *src = (const uint4 *)(d.mw + (size_t)ol * d.NP);
+    uint4 *dst = (uint4 *)(d.dense + (size_t)slot * d.NP);
+    for (uint32_t i = lane_id(); i < d.NP / 4; i += 64 * MB) {
+        uint4 v[MB];
+#pragma unroll
+        for (int u = 0; u < MB; u++) v[u] = i + u * 64 < d.NP / 4 ? src[i + u * 64] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int u = 0; u < MB; u++)
+            if (i + u * 64 < d.NP / 4) dst[i + u * 64] = v[u];
+    }
+    if (lane_id() == 0) {
+        d.dense_meta[slot] = make_uint4(d.lo + ol, 0, 0, 0);
+        d.dense_len[slot] = d.clen[ol];
+        d.dense_last[slot] = d.clast[ol];
+        d.cpslot[ol] = slot;
+        d.dirty[ol] = 0;
+        ids[k] = d.NL + slot;
+    }
+}
+
+// dedup duplicates (vals = the dirty rows sorted by fingerprint, dup_of from k_fp_verify) take their
+// head's slot; map[i] = {row, slot} for every dirty row, consumed by k_side_scatter
+__global__ void k_snap_dups(DS d, const uint32_t *vals, uint32_t n, const uint32_t *dup_of, uint2 *map) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t row = vals[i], h = dup_of ? dup_of[row] : SRC_NONE;
+    if (h != SRC_NONE) {
+        d.cpslot[row] = d.cpslot[h];
+        d.dirty[row] = 0;
+    }
+    map[i] = make_uint2(row, h != SRC_NONE ? d.cpslot[h] : d.cpslot[row]);
+}
+
+__global__ void k_side_scatter(DS d, const uint2 *map, uint32_t n, uint32_t nhashed) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) {
+        ctr_add(d, C_X_CS_ROWS, (unsigned long long)nhashed);
+        ctr_add(d, C_X_CS_DUP, (unsigned long long)(n - nhashed));
+    }
+    if (i >= n) return;
+    const uint2 e = map[i];
+    d.cs[e.x] = d.dense_cs[e.y];
 }
 
 #include "swimsim_checksum.hip"

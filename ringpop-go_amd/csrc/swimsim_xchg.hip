@@ -165,7 +165,7 @@ __global__ void k_x_unpack(DS d, XArgs x, const uint8_t *buf, const ulonglong2 *
         uint4 *dst = (uint4 *)(d.dense + (size_t)slot * d.NP);
         for (uint32_t q = lane_id(); q < d.NP / 4; q += 64) dst[q] = payload[q];
         if (lane_id() == 0) {
-            d.dense_meta[slot] = h.meta;
+            d.dense_meta[slot] = make_uint4(h.meta.x, h.meta.y, h.meta.z, 0u);   // w: a local alias only
             d.dense_len[slot] = h.dlen;
             d.dense_last[slot] = h.dlast;
             d.dense_cs[slot] = h.dcs;
@@ -224,7 +224,7 @@ __global__ void k_x_csreq(DS d, const uint4 *defer, const uint32_t *defer_cnt, i
 __global__ void k_csreq_ids(DS d, const uint4 *csreq, const uint32_t *csreqcnt, uint32_t *list, uint32_t *cnt) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= *csreqcnt) return;
-    list[atomicAdd(cnt, 1u)] = d.NL + csreq[i].y;
+    if (csreq[i].y < d.dense_cap) list[atomicAdd(cnt, 1u)] = d.NL + csreq[i].y;   // else hashed on the side stream
 }
 
 // answers to the requesting shards
