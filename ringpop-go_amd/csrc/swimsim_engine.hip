@@ -275,6 +275,7 @@ struct swimsim {
     uint32_t *list = nullptr, *cnt = nullptr;
     uint4 *defer = nullptr;
     uint32_t *defer_cnt = nullptr;
+    uint8_t *defer_eq = nullptr;                  // deferred decision settled by row equality
     uint32_t *exh_list = nullptr, *exh_cnt = nullptr, *scratch = nullptr;
     uint8_t *need = nullptr, *fsflag = nullptr;
     uint4 *evbuf = nullptr;
@@ -690,9 +691,11 @@ int resolve_deferred(swimsim *h, int phase, MsgDesc *rdesc, uint32_t maxn) {
     uint32_t maxlist = 2 * maxn;
     {
         Scope sc(h, F_CSPREP);
-        HIPCHK(h, hipMemsetAsync(h->cnt, 0, 4, h->s));
+        HIPCHK(h, hipMemsetAsync(h->cnt, 0, 8, h->s));
+        hipLaunchKernelGGL(k_defer_eq, dim3(blocks_for_waves(maxn)), dim3(256), 0, h->s, h->d, h->defer, h->defer_cnt,
+                           phase, h->defer_eq);
         hipLaunchKernelGGL(k_defer_ids, dim3(blocks_for_threads(maxn)), dim3(256), 0, h->s, h->d, h->defer,
-                           h->defer_cnt, h->list, h->cnt);
+                           h->defer_cnt, h->defer_eq, h->list, h->cnt);
     }
     if (remote) {
         HIPCHK(h, hipMemsetAsync(h->csreqcnt, 0, 4, h->s));
@@ -706,7 +709,7 @@ int resolve_deferred(swimsim *h, int phase, MsgDesc *rdesc, uint32_t maxn) {
     {
         uint32_t *hc = h->hinfo + 10;
         HIPCHK(h, hipMemcpyAsync(hc, h->cnt, 4, hipMemcpyDeviceToHost, h->s));
-        HIPCHK(h, hipMemcpyAsync(hc + 1, h->defer_cnt, 4, hipMemcpyDeviceToHost, h->s));
+        HIPCHK(h, hipMemcpyAsync(hc + 1, h->cnt + 1, 4, hipMemcpyDeviceToHost, h->s));
         HIPCHK(h, hipStreamSynchronize(h->s));
         if (hc[1])
             if (int rc = sync_side(h)) return rc;
@@ -719,7 +722,7 @@ int resolve_deferred(swimsim *h, int phase, MsgDesc *rdesc, uint32_t maxn) {
     }
     Scope sc(h, phase == 1 ? F_PINGREQ : F_RECV);
     hipLaunchKernelGGL(k_recv_finish, dim3(blocks_for_threads(maxn)), dim3(256), 0, h->s, h->d, h->defer,
-                       h->defer_cnt, rdesc, phase, h->fsflag, h->rcs);
+                       h->defer_cnt, rdesc, phase, h->fsflag, h->rcs, h->defer_eq);
     return 0;
 }
 
@@ -1261,7 +1264,9 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
         d.dense_cap = (uint32_t)std::max<uint64_t>(64, std::min<uint64_t>(2ull * h->NL + 64, by_mem));
         // side-stream checksum snapshots (latency-bound phase C launches only), up to 1/8 of the free HBM
         const uint64_t snap_mem = (uint64_t)(freeb / 8) / (4ull * h->NP);
-        h->snap_cap = h->cs_async ? (uint32_t)std::min<uint64_t>(std::min<uint64_t>(CS_NARROW_ROWS, h->NL), snap_mem) : 0u;
+        uint64_t async_rows = CS_NARROW_ROWS;
+        if (const char *v = getenv("SWIMSIM_CS_ASYNC_ROWS")) async_rows = strtoull(v, nullptr, 10);
+        h->snap_cap = h->cs_async ? (uint32_t)std::min<uint64_t>(std::min<uint64_t>(async_rows, h->NL), snap_mem) : 0u;
     }
     const size_t nslots = (size_t)d.dense_cap + h->snap_cap;
     if ((rc = dalloc(h, &d.dense, nslots * h->NP, "dense snapshots")) ||
@@ -1295,7 +1300,8 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
         (rc = dalloc(h, &h->ukeys, KC, "ukeys")) || (rc = dalloc(h, &h->counts, KC, "counts")) ||
         (rc = dalloc(h, &h->offs, KC, "offs")) || (rc = dalloc(h, &h->nruns, 1, "nruns")) ||
         (rc = dalloc(h, &h->info, 8, "info")) || (rc = dalloc(h, &h->list, 3 * KC + 2 * (size_t)h->NL + 64, "list")) ||
-        (rc = dalloc(h, &h->cnt, 1, "cnt")) || (rc = dalloc(h, &h->defer, KC + 2 * (size_t)h->NL + 64, "defer")) ||
+        (rc = dalloc(h, &h->cnt, 2, "cnt")) || (rc = dalloc(h, &h->defer, KC + 2 * (size_t)h->NL + 64, "defer")) ||
+        (rc = dalloc(h, &h->defer_eq, KC + 2 * (size_t)h->NL + 64, "defer eq")) ||
         (rc = dalloc(h, &h->defer_cnt, 1, "defer_cnt")) || (rc = dalloc(h, &h->exh_list, h->NL, "exh_list")) ||
         (rc = dalloc(h, &h->exh_cnt, 1, "exh_cnt")) || (rc = dalloc(h, &h->scratch, (size_t)64 * (h->NP / 32), "scratch")) ||
         (rc = dalloc(h, &h->need, h->N, "need")) || (rc = dalloc(h, &h->digest_buf, 4, "digest")) ||

@@ -884,20 +884,61 @@ __global__ void k_recv(DS d, RecvArgs a) {
 
 // resolve deferred full-sync decisions once the snapshot checksums exist (phase 2 = heal ping:
 // the job is queued at once; heal runs in phase E, before any phase-D job of the round)
+// Equal rows have equal checksums: a deferred decision whose receiver snapshot equals the sender's
+// issue-time row (word for word) is "no full sync" without hashing either side. The sender's
+// issue-time row is its issue snapshot (pending C_o, local or side slot) or, for a sender that was
+// clean at issue and is still clean, its current row. Remote senders and heal pings are not checked.
+__global__ void k_defer_eq(DS d, const uint4 *defer, const uint32_t *defer_cnt, int phase, uint8_t *eq) {
+    const uint32_t i = wave_gid();
+    if (i >= *defer_cnt) return;
+    const uint4 e = defer[i];
+    const uint32_t ri = e.x & 0x7FFFFFFFu, sender = phase == 1 ? ri / d.K : ri;
+    const uint32_t *srow = nullptr;
+    if (phase != 2) {
+        if (e.w & 0x80000000u) {
+            if (!(e.z & 0x80000000u)) srow = d.dense + (size_t)e.z * d.NP;
+        } else if (sender >= d.lo && sender < d.lo + d.NL && !d.dirty[sender - d.lo]) {
+            srow = d.mw + (size_t)(sender - d.lo) * d.NP;
+        }
+    }
+    bool same = false;
+    if (srow) {
+        const uint4 *a = (const uint4 *)(d.dense + (size_t)e.y * d.NP), *b = (const uint4 *)srow;
+        bool diff = false;
+        for (uint32_t base = 0; base < d.NP / 4 && !__any(diff); base += 64 * MB) {
+            uint4 x[MB], y[MB];
+#pragma unroll
+            for (int u = 0; u < MB; u++) {
+                const uint32_t k = base + u * 64 + lane_id();
+                x[u] = k < d.NP / 4 ? a[k] : make_uint4(0, 0, 0, 0);
+                y[u] = k < d.NP / 4 ? b[k] : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < MB; u++) diff |= x[u].x != y[u].x || x[u].y != y[u].y || x[u].z != y[u].z || x[u].w != y[u].w;
+        }
+        same = !__any(diff);
+    }
+    if (lane_id() == 0) eq[i] = same ? 1 : 0;
+}
+
 __global__ void k_recv_finish(DS d, const uint4 *defer, const uint32_t *defer_cnt, MsgDesc *rdesc, int phase,
-                              uint8_t *fsflag, const uint32_t *rcs) {
+                              uint8_t *fsflag, const uint32_t *rcs, const uint8_t *eq) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= *defer_cnt) return;
     const uint4 e = defer[i];
     const uint32_t slot = e.y, pair = e.w & 0x7FFFFFFFu;
     const uint32_t ri = e.x & 0x7FFFFFFFu, sender = phase == 1 ? ri / d.K : ri;
     // pending C_o: local snapshot (hashed in this resolution) or remote (answered by its owner shard)
-    const uint32_t scs = !(e.w & 0x80000000u) ? e.z : (e.z & 0x80000000u) ? rcs[sender] : d.dense_cs[e.z];
     MsgDesc resp;
     resp.kind = 0; resp.len = 0; resp.off_lo = resp.off_hi = 0;
-    const uint32_t alias = d.dense_meta[slot].w;                   // receiver clean, hashed on the side stream
-    if (alias) d.dense_cs[slot] = d.dense_cs[alias - 1u];
-    if (d.dense_cs[slot] != scs) {
+    bool differ = false;
+    if (!eq[i]) {
+        const uint32_t scs = !(e.w & 0x80000000u) ? e.z : (e.z & 0x80000000u) ? rcs[sender] : d.dense_cs[e.z];
+        const uint32_t alias = d.dense_meta[slot].w;               // receiver clean, hashed on the side stream
+        if (alias) d.dense_cs[slot] = d.dense_cs[alias - 1u];
+        differ = d.dense_cs[slot] != scs;
+    }
+    if (differ) {
         resp.kind = 1; resp.off_lo = slot; resp.len = d.dense_meta[slot].z;
         ctr_add(d, phase == 1 ? C_FULL_SYNCS_PINGREQ : C_FULL_SYNCS, 1ull);
         if (phase == 2) {
@@ -914,9 +955,11 @@ __global__ void k_recv_finish(DS d, const uint4 *defer, const uint32_t *defer_cn
 
 // defer list → checksum list of the dense snapshots that need a hash (NL + slot): dirty receivers and
 // pending senders (a sender referenced by several deferred decisions is hashed once per reference)
-__global__ void k_defer_ids(DS d, const uint4 *defer, const uint32_t *defer_cnt, uint32_t *list, uint32_t *cnt) {
+__global__ void k_defer_ids(DS d, const uint4 *defer, const uint32_t *defer_cnt, const uint8_t *eq, uint32_t *list,
+                            uint32_t *cnt) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= *defer_cnt) return;
+    if (i >= *defer_cnt || eq[i]) return;
+    atomicAdd(cnt + 1, 1u);                                        // decisions left to the checksums
     const uint4 e = defer[i];
     if (e.x & 0x80000000u) list[atomicAdd(cnt, 1u)] = d.NL + e.y;
     if ((e.w & 0x80000000u) && !(e.z & 0x80000000u) && e.z < d.dense_cap)                  // local pending
