@@ -166,6 +166,23 @@ def main():
     merge_gbps = (merge.get("alg_bytes", 0) / max(1, merge.get("launches", 1))) / (merge.get("avg_ms", 1) * 1e-3) / 1e9 \
         if merge.get("avg_ms", 0) > 0 else 0.0
 
+    def family_roofline(f):
+        # algorithmic bytes per launch / HIP-event time, and the PMC-measured HBM bytes per launch of the
+        # same kernels over the same time (the gathers' sector traffic: what actually bounds them)
+        k = kt.get(f, {})
+        if not k.get("avg_ms"):
+            return None
+        sec = k["avg_ms"] * 1e-3
+        alg = k["alg_bytes"] / max(1, k["launches"]) / sec / 1e9
+        p = pmc_family(f)
+        out = {"kernel": FAMILY_KERNELS[f][0], "avg_launch_ms": round(k["avg_ms"], 4), "launches": k["launches"],
+               "achieved_alg": round(alg, 2), "frac_alg": round(alg / HBM_PEAK_GBPS, 4), "unit": "GB/s"}
+        if p:
+            hbm = p["traffic"] / sec / 1e9
+            out.update({"traffic_per_launch": p["traffic"], "achieved_hbm": round(hbm, 2),
+                        "frac_hbm": round(hbm / HBM_PEAK_GBPS, 4)})
+        return out
+
     if rank == 0:
         value = n * args.steps / dt
         line = {
@@ -190,7 +207,8 @@ def main():
                          "traffic": pmc["traffic"] if pmc else None,
                          "traffic_unit": "bytes per launch (FETCH_SIZE + WRITE_SIZE, " + os.path.basename(PMC_SUMMARY) + ")",
                          "avg_launch_ms": round(info["avg_ms"], 5), "launches": info["launches"],
-                         "merge_kernel_GBps": round(merge_gbps, 2)},
+                         "merge_kernel_GBps": round(merge_gbps, 2),
+                         "merge": {f: family_roofline(f) for f in ("recv_merge", "resp_merge", "issue")}},
             "kernel_ms": {k: round(v["avg_ms"] * v["launches"], 3) for k, v in kt.items()},
             "counters": counters,
         }

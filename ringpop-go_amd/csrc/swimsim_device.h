@@ -35,7 +35,9 @@ enum Counter {
     C_SUSPECT_DECL, C_APPLIED, C_REFUTES, C_FULL_SYNCS, C_FULL_SYNCS_PINGREQ, C_RFS_DONE, C_RFS_OMITTED,
     C_TIMERS_FIRED, C_MSG_CHANGES, C_HEAL_ATTEMPTS, C_HEAL_FAILURES, C_NCOUNTERS,
     // measurement-only counters (not part of the parity record)
-    C_X_MERGED = C_NCOUNTERS, C_X_APPLIED, C_X_ISSUED, C_X_CS_ROWS, C_X_CS_DUP, C_NALL
+    // (merges and applies of k_recv and k_resp are counted apart: C_X_MERGED + 5 / C_X_APPLIED + 5)
+    C_X_MERGED = C_NCOUNTERS, C_X_APPLIED, C_X_ISSUED, C_X_CS_ROWS, C_X_CS_DUP,
+    C_X_MERGED_R, C_X_APPLIED_R, C_X_RISSUED, C_X_RCALLS, C_X_BUMPED, C_NALL
 };
 
 constexpr int CTR_SHARDS = 64, CTR_STRIDE = 32;   // d.ctr is [CTR_SHARDS][CTR_STRIDE] u64

@@ -37,10 +37,12 @@ struct Timed {
 // F_CHECKSUM times exactly the FarmHash kernel dispatches (k_checksum / k_checksum_n16), one per
 // launch, so its average matches the profiler's per-dispatch average; F_CSPREP is the work around
 // them (dirty lists, dedup, deferred-decision lists)
+// F_RECV times exactly the k_recv dispatches (phases D and Q2), so its launch count and average match
+// the profiler's; their deferred-decision epilogues are F_RECVFIN
 enum Fam { F_TIMERS, F_SELECT, F_ISSUE, F_SORT, F_RECV, F_RESP, F_PINGREQ, F_JOBS, F_CHECKSUM, F_CSPREP, F_EVENTS,
-           F_XCHG, F_NFAM };
+           F_XCHG, F_RECVFIN, F_NFAM };
 const char *kFamName[F_NFAM] = {"timers", "select", "issue", "sort", "recv_merge", "resp_merge", "pingreq",
-                                "rfs_jobs", "checksum", "checksum_prep", "events", "exchange"};
+                                "rfs_jobs", "checksum", "checksum_prep", "events", "exchange", "recv_finish"};
 
 // ---------------------------------------------------------------------------------------------
 // shard transports: how parcels move between the shards of one cluster
@@ -720,7 +722,7 @@ int resolve_deferred(swimsim *h, int phase, MsgDesc *rdesc, uint32_t maxn) {
                            h->csreqcnt, h->xitems, h->xcnt, h->xcap);
         if (int rc = xchg(h)) return rc;
     }
-    Scope sc(h, phase == 1 ? F_PINGREQ : F_RECV);
+    Scope sc(h, phase == 1 ? F_PINGREQ : F_RECVFIN);
     hipLaunchKernelGGL(k_recv_finish, dim3(blocks_for_threads(maxn)), dim3(256), 0, h->s, h->d, h->defer,
                        h->defer_cnt, rdesc, phase, h->fsflag, h->rcs, h->defer_eq);
     return 0;
@@ -742,13 +744,13 @@ int run_waves(swimsim *h, int phase, uint32_t nruns_valid, uint32_t maxcount) {
     a.r = h->round;
     hipMemsetAsync(h->defer_cnt, 0, 4, h->s);
     {
-        Scope sc(h, phase == 0 ? F_RECV : F_PINGREQ);
+        Scope sc(h, F_RECV);
         hipLaunchKernelGGL(k_recv, dim3(blocks_for_waves(nruns_valid)), dim3(256), 0, h->s, h->d, a);
     }
     const uint32_t maxdefer = std::min<uint64_t>((uint64_t)nruns_valid * maxcount, h->d.dense_cap);
     if (int rc = resolve_deferred(h, phase, a.rdesc, maxdefer)) return rc;
     if (phase == 0) {
-        Scope sc(h, F_RECV);
+        Scope sc(h, F_RECVFIN);
         hipLaunchKernelGGL(k_build_jobs, dim3(blocks_for_threads(nruns_valid)), dim3(256), 0, h->s, h->d, h->ukeys,
                            h->counts, h->offs, h->vals_out, nruns_valid, h->fsflag);
     }
@@ -967,9 +969,12 @@ int step_one(swimsim *h, const swimsim_event *ev, size_t nev) {
     uint32_t ninbox = h->NL;
     HIPCHK(h, hipMemsetAsync(h->d.dense_cur, 0, 4, h->s));         // dense snapshots live from here through R
     {
-        Scope sc(h, F_ISSUE);
-        hipLaunchKernelGGL(k_issue, dim3(blocks_for_waves(h->NL)), dim3(256), 0, h->s, h->d, 0, h->tgt, h->failed,
-                           h->sdesc, h->sI, h->sC, h->sS);
+        {
+            Scope sc(h, F_ISSUE);
+            hipLaunchKernelGGL(k_issue, dim3(blocks_for_waves(h->NL)), dim3(256), 0, h->s, h->d, 0, h->tgt, h->failed,
+                               h->sdesc, h->sI, h->sC, h->sS);
+        }
+        Scope sc(h, F_SORT);
         HIPCHK(h, hipMemsetAsync(h->info + 2, 0, 4, h->s));
         hipLaunchKernelGGL(k_pairs_direct, dim3(blocks_for_threads(h->NL)), dim3(256), 0, h->s, h->d, h->tgt, h->keys,
                            h->failed, h->info, h->xitems, h->xcnt, h->xcap);
@@ -1008,9 +1013,12 @@ int step_one(swimsim *h, const swimsim_event *ev, size_t nev) {
         }
         HIPCHK(h, hipMemsetAsync(h->d.dense_cur, 0, 4, h->s));     // dense snapshots live from here through Q3
         {
+            {
+                Scope sc(h, F_ISSUE);
+                hipLaunchKernelGGL(k_issue, dim3(blocks_for_waves(h->NL)), dim3(256), 0, h->s, h->d, 1, h->tgt, h->failed,
+                                   h->sdesc2, h->sI2, h->sC2, h->sS2);
+            }
             Scope sc(h, F_PINGREQ);
-            hipLaunchKernelGGL(k_issue, dim3(blocks_for_waves(h->NL)), dim3(256), 0, h->s, h->d, 1, h->tgt, h->failed,
-                               h->sdesc2, h->sI2, h->sC2, h->sS2);
             hipLaunchKernelGGL(k_pairs_helpers, dim3(blocks_for_threads(h->NL * h->K)), dim3(256), 0, h->s, h->d,
                                h->failed, h->H, h->nh, h->keys, h->xitems, h->xcnt, h->xcap);
         }
@@ -1688,10 +1696,16 @@ int swimsim_kernel_times(swimsim_t *h, const char **names, double *avg_ms, uint6
     const double issued = (double)(c[C_X_ISSUED] - h->fam_bytes_base[C_X_ISSUED]);
     const double csrows = (double)(c[C_X_CS_ROWS] - h->fam_bytes_base[C_X_CS_ROWS]);
     const double csdups = (double)(c[C_X_CS_DUP] - h->fam_bytes_base[C_X_CS_DUP]);
+    auto delta = [&](int k) { return (double)(c[k] - h->fam_bytes_base[k]); };
     // algorithmic bytes: merge = 16 B record + 4 B row word read per processed
     // change; + 4 B row word + 1 B counter + 16 B dissem/timer entry + 1 B timer state per applied change.
     // checksum = 4 B member word per member per dirty row. issue = 16 B per record written (+ 16 B read).
+    // recv_merge (k_recv): its merges + IssueAsReceiver: 16 B entry gather + 16 B record write + 4 B counter
+    // write-back per issued record, and the 4 B-per-32-members presence bitmap per call.
+    // resp_merge (k_resp): its merges + bumpPiggybackCounters: 16 B record read + 4 B counter read and write.
     const double merge_bytes = merged * 20.0 + applied * 22.0;
+    const double resp_bytes = delta(C_X_MERGED_R) * 20.0 + delta(C_X_APPLIED_R) * 22.0 + delta(C_X_BUMPED) * 24.0;
+    const double recv_issue_bytes = delta(C_X_RISSUED) * 36.0 + delta(C_X_RCALLS) * 4.0 * h->d.NBIT;
     for (int f = 0; f < F_NFAM && (size_t)f < cap; f++) {
         if (names) names[f] = kFamName[f];
         if (avg_ms) avg_ms[f] = h->fam_n[f] ? h->fam_ms[f] / (double)h->fam_n[f] : 0.0;
@@ -1701,7 +1715,8 @@ int swimsim_kernel_times(swimsim_t *h, const char **names, double *avg_ms, uint6
             if (f == F_CHECKSUM) b = csrows * 4.0 * h->N;      // member words of every hashed row
             if (f == F_CSPREP) b = csdups * 8.0 * h->N;        // duplicates verified word for word
             if (f == F_ISSUE) b = issued * 32.0;
-            if (f == F_RECV) b = merge_bytes;  // merge volume is attributed to the receive waves (the bulk)
+            if (f == F_RECV) b = merge_bytes + recv_issue_bytes;   // k_recv merges (and the few other
+            if (f == F_RESP) b = resp_bytes;                        // merges) + its issue; k_resp
             alg_bytes[f] = b;
         }
     }

@@ -145,7 +145,7 @@ __device__ __forceinline__ int wmax(int v) {
     return v;
 }
 
-__device__ __forceinline__ void wave_finalize(const DS &d, uint32_t ol, const MAcc &acc) {
+__device__ __forceinline__ void wave_finalize(const DS &d, uint32_t ol, const MAcc &acc, int cset = 0) {
     const int dping = wsum(acc.dping), ddc = wsum(acc.ddc), napp = wsum(acc.napp), nref = wsum(acc.nref);
     const int ev = wsum(acc.evict), np = wsum(acc.nproc), dl = wsum(acc.dlen), ml = wmax(acc.maxlast);
     const int inv = wmax(acc.inval);
@@ -154,8 +154,8 @@ __device__ __forceinline__ void wave_finalize(const DS &d, uint32_t ol, const MA
     for (int off = 32; off > 0; off >>= 1) dfp += __shfl_xor(dfp, off, 64);
     if (lane_id() == 0) {
         fold_row(d, ol, dping, ddc, napp, nref, ev, dl, ml, inv, dfp);
-        if (np) ctr_add(d, C_X_MERGED, (unsigned long long)np);
-        if (napp) ctr_add(d, C_X_APPLIED, (unsigned long long)napp);
+        if (np && cset < 2) ctr_add(d, cset ? C_X_MERGED_R : C_X_MERGED, (unsigned long long)np);
+        if (napp && cset < 2) ctr_add(d, cset ? C_X_APPLIED_R : C_X_APPLIED, (unsigned long long)napp);
     }
     __threadfence_block();
 }
@@ -165,7 +165,9 @@ __device__ __forceinline__ void wave_finalize(const DS &d, uint32_t ol, const MA
 constexpr int MB = 4;
 
 // merge a whole message into row ol (wave-wide; the changes of one message are distinct members)
-__device__ void wave_merge_msg(const DS &d, uint32_t ol, uint32_t o, const MsgDesc &md, uint32_t now_e, uint32_t sched_r) {
+// cset selects the measurement counters (0: k_recv's C_X_MERGED/C_X_APPLIED, 1: k_resp's pair, 2: none)
+__device__ void wave_merge_msg(const DS &d, uint32_t ol, uint32_t o, const MsgDesc &md, uint32_t now_e, uint32_t sched_r,
+                               int cset = 0) {
     MAcc acc;
     const uint32_t *rowp = d.mw + (size_t)ol * d.NP;
     if (md.kind == 0) {
@@ -207,7 +209,7 @@ __device__ void wave_merge_msg(const DS &d, uint32_t ol, uint32_t o, const MsgDe
         }
     }
     __threadfence_block();
-    wave_finalize(d, ol, acc);
+    wave_finalize(d, ol, acc, cset);
 }
 
 // bumpPiggybackCounters over a sparse list (disseminator.go:135-149)
@@ -830,6 +832,10 @@ __device__ void recv_one(const DS &d, const RecvArgs &a, uint32_t j, uint32_t se
     wave_merge_msg(d, ol, j, a.sdesc[sender_row], a.r, a.r);
     MsgDesc resp;
     const uint32_t kept = wave_issue_recv(d, ol, sender, a.sI[sender_row], resp);
+    if (lane_id() == 0) {
+        ctr_add(d, C_X_RISSUED, (unsigned long long)kept);
+        ctr_add(d, C_X_RCALLS, 1ull);
+    }
     if (kept == 0) {
         const uint32_t scs = a.sC[sender_row];
         const uint32_t sslot = a.sS ? a.sS[sender_row] : SRC_NONE;
@@ -989,8 +995,11 @@ __global__ void k_resp(DS d, const int32_t *tgt, const uint8_t *failed, const Ms
     if (tgt[ol] < 0 || failed[ol]) return;
     const uint32_t o = d.lo + ol;
     wave_bump(d, ol, sdesc[o]);
-    wave_merge_msg(d, ol, o, rdesc[o], r, r);
-    if (lane_id() == 0) ctr_add(d, C_PINGS_OK, 1ull);
+    wave_merge_msg(d, ol, o, rdesc[o], r, r, 1);
+    if (lane_id() == 0) {
+        ctr_add(d, C_PINGS_OK, 1ull);
+        if (sdesc[o].kind == 0) ctr_add(d, C_X_BUMPED, (unsigned long long)sdesc[o].len);
+    }
 }
 
 // Q3: resolve indirect pings (ping_request_sender.go:65-138, node.go:494-509)
@@ -1006,7 +1015,7 @@ __global__ void k_resolve(DS d, const int32_t *tgt, const uint8_t *failed, const
             errs++;
             wave_bump(d, ol, sdesc2[o]);                            // bump only on error (105-106)
         } else {
-            wave_merge_msg(d, ol, o, rdesc2[(size_t)o * K + q], r, r);
+            wave_merge_msg(d, ol, o, rdesc2[(size_t)o * K + q], r, r, 2);
         }
     }
     if (lane_id() == 0) {
@@ -1043,7 +1052,7 @@ __global__ void k_jobs_merge(DS d, uint32_t q, const MsgDesc *snapdesc, uint32_t
     const uint32_t ol = wave_gid();
     if (ol >= d.NL || d.njobs[ol] <= q) return;
     const uint32_t src = d.jobs[(size_t)ol * d.maxjobs + q];
-    wave_merge_msg(d, ol, d.lo + ol, snapdesc[src], r, r);
+    wave_merge_msg(d, ol, d.lo + ol, snapdesc[src], r, r, 2);
     if (lane_id() == 0) ctr_add(d, C_RFS_DONE, 1ull);
 }
 
@@ -1240,7 +1249,7 @@ __global__ void k_sender_info(DS d, uint32_t ol, uint32_t *out) {
 }
 
 __global__ void k_apply_msg(DS d, uint32_t ol, const MsgDesc *md, uint32_t r) {
-    wave_merge_msg(d, ol, d.lo + ol, *md, r, r);
+    wave_merge_msg(d, ol, d.lo + ol, *md, r, r, 2);
 }
 
 // sendPingWithChanges o → t whose response is discarded (heal_partition.go:97-124): target runs
@@ -1248,7 +1257,7 @@ __global__ void k_apply_msg(DS d, uint32_t ol, const MsgDesc *md, uint32_t r) {
 __global__ void k_ping_with(DS d, uint32_t tol, uint32_t sender, const MsgDesc *md, const uint32_t *sics,
                             MsgDesc *resp_out, uint4 *defer, uint32_t *defer_cnt, uint32_t r) {
     const uint32_t sinc = sics[0], scs = sics[1];
-    wave_merge_msg(d, tol, d.lo + tol, *md, r, r);
+    wave_merge_msg(d, tol, d.lo + tol, *md, r, r, 2);
     MsgDesc resp;
     const uint32_t kept = wave_issue_recv(d, tol, sender, sinc, resp);
     if (kept == 0) {
