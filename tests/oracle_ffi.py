@@ -106,6 +106,14 @@ def lib():
             "or_perm": (u32, [u64, u32, u32, u32, u32]),
             "or_perm_inv": (u32, [u64, u32, u32, u32, u32]),
             "or_checksum_string": (C.c_size_t, [P, u32, C.c_char_p, C.c_size_t]),
+            "or_ring_new": (P, [u32]),
+            "or_ring_free": (None, [P]),
+            "or_ring_add_remove": (i32, [P, P, C.c_size_t, P, C.c_size_t]),
+            "or_ring_checksum": (u32, [P]),
+            "or_ring_server_count": (u32, [P]),
+            "or_ring_lookup": (C.c_char_p, [P, C.c_char_p, C.c_size_t]),
+            "or_ring_lookup_n": (C.c_size_t, [P, C.c_char_p, C.c_size_t, u32, P]),
+            "or_ring_points": (C.c_size_t, [P, P, P, C.c_size_t]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -357,3 +365,49 @@ def perm(seed, o, epoch, n, idx):
 
 def perm_inv(seed, o, epoch, n, m):
     return lib().or_perm_inv(seed, o, epoch, n, m)
+
+
+def _cstrs(lst):
+    arr = (C.c_char_p * max(1, len(lst)))(*[x.encode() for x in lst])
+    return arr, len(lst)
+
+
+class OracleRing:
+    """CPU restatement of hashring.HashRing (oracle/ring_oracle.c); test infrastructure only."""
+
+    def __init__(self, replica_points=100):
+        self.h = lib().or_ring_new(replica_points)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().or_ring_free(self.h)
+            self.h = None
+
+    def add_remove_servers(self, add=(), remove=()):
+        a, na = _cstrs(list(add))
+        r, nr = _cstrs(list(remove))
+        return bool(lib().or_ring_add_remove(self.h, a, na, r, nr))
+
+    def checksum(self):
+        return lib().or_ring_checksum(self.h)
+
+    def server_count(self):
+        return lib().or_ring_server_count(self.h)
+
+    def lookup(self, key):
+        k = key.encode() if isinstance(key, str) else key
+        v = lib().or_ring_lookup(self.h, k, len(k))
+        return (v.decode(), True) if v is not None else ("", False)
+
+    def lookup_n(self, key, n):
+        k = key.encode() if isinstance(key, str) else key
+        out = (C.c_char_p * max(1, n + self.server_count()))()
+        got = lib().or_ring_lookup_n(self.h, k, len(k), n, out)
+        return [out[i].decode() for i in range(got)]
+
+    def points(self):
+        n = lib().or_ring_points(self.h, None, None, 0)
+        hs = (C.c_uint32 * max(1, n))()
+        own = (C.c_char_p * max(1, n))()
+        lib().or_ring_points(self.h, hs, own, n)
+        return [(hs[i], own[i].decode()) for i in range(n)]
