@@ -53,6 +53,29 @@ def pmc_family(family):
             "valu_insts": tot("sq_insts_valu_per_launch"), "lds_insts": tot("sq_insts_lds_per_launch")}
 
 
+def ring_bench(n, replicas=100, nkeys=1 << 20):
+    """SURVEY.md §8(f) rank 1, measured beside the headline (not part of `value`): the hash ring of a
+    converged n-member cluster (every member a server, `replicas` points each: hashring.go:148-155)
+    built on the device in one AddRemoveServers call, then `nkeys` Lookups in one batch. Device
+    times are HIP events around the kernels (swimring_last_times)."""
+    from swimsim import address_of
+    from swimsim.ring import HashRing
+
+    ring = HashRing(replicas, device=0)
+    ring.add_remove_servers([address_of(m) for m in range(n)])
+    build_ms, _ = ring.last_times()
+    keys = [f"key-{k}" for k in range(nkeys)]
+    ring.lookup_ids(keys[:1024])                       # warm-up
+    ring.lookup_ids(keys)
+    _, look_ms = ring.last_times()
+    pts = len(ring.points()[0])
+    ring.close()
+    return {"servers": n, "replica_points": replicas, "points": pts, "build_ms": round(build_ms, 3),
+            "build_points_per_s": round(n * replicas / (build_ms * 1e-3), 1) if build_ms > 0 else None,
+            "lookups": nkeys, "lookup_ms": round(look_ms, 3),
+            "lookups_per_s": round(nkeys / (look_ms * 1e-3), 1) if look_ms > 0 else None}
+
+
 def dist_env():
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -223,6 +246,8 @@ def main():
             line["exchange"] = {"bytes_rank0": shard["exchanged_bytes"], "exchanges_rank0": shard["exchanges"]}
         if ws == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline()
+        if ws == 1:
+            line["hashring"] = ring_bench(n)
         print(json.dumps(line), flush=True)
     if ws > 1:
         import torch.distributed as dist
