@@ -135,7 +135,17 @@ def main():
 
         # launcher plumbing only (RCCL id broadcast, barriers, max-over-ranks time); the data path is
         # libswimsim's own RCCL communicator
-        dist.init_process_group("gloo")
+        # gloo prints its connection banner on the C-level stdout; keep stdout for the one JSON line
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo")
+            dist.barrier()
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
 
     import swimsim
     from swimsim import workloads as W
