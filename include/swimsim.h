@@ -99,6 +99,10 @@ int swimsim_init_converged(swimsim_t *h);
 int swimsim_init_self_only(swimsim_t *h);
 /* raw row write, no side effects (scenario setup) */
 int swimsim_set_member(swimsim_t *h, uint32_t observer, uint32_t member, int32_t status, int64_t inc_ms);
+/* raw write of a whole row (status[N], inc_ms[N]; SWIMSIM_UNKNOWN = not a member), no side effects:
+ * seeds an observer from a received membership, e.g. a joinResponse's (join_handler.go:27-32,
+ * memberlist.go:325-334 takes unseen members wholesale). Incarnations must be t0 + e*period. */
+int swimsim_set_row(swimsim_t *h, uint32_t observer, const uint8_t *status, const int64_t *inc_ms);
 /* memberlist.MakeChange (memberlist.go:282-307): returns #applied (0/1) or an error */
 int swimsim_make_change(swimsim_t *h, uint32_t observer, uint32_t member, int64_t inc_ms, int32_t status);
 /* disseminator.ClearChanges (disseminator.go:217-221) */

@@ -1397,6 +1397,24 @@ int swimsim_set_member(swimsim_t *h, uint32_t o, uint32_t m, int32_t status, int
     return SWIMSIM_OK;
 }
 
+int swimsim_set_row(swimsim_t *h, uint32_t o, const uint8_t *status, const int64_t *inc_ms) {
+    if (!h || !own(h, o) || !status || !inc_ms) return SWIMSIM_EINVAL;
+    std::vector<uint32_t> row(h->NP, (uint32_t)SWIMSIM_UNKNOWN);
+    for (uint32_t m = 0; m < h->N; m++) {
+        const int32_t s = status[m];
+        if (s == SWIMSIM_UNKNOWN) continue;
+        if (s > 4) return h->fail(SWIMSIM_EINVAL, "member %u: status %d", m, s);
+        uint32_t e;
+        if (int rc = to_e(h, inc_ms[m], &e)) return rc;
+        row[m] = (e << 3) | (uint32_t)s;
+    }
+    HIPCHK(h, hipMemcpyAsync(h->d.mw + (size_t)(o - h->lo) * h->NP, row.data(), (size_t)h->N * 4,
+                             hipMemcpyHostToDevice, h->s));
+    hipLaunchKernelGGL(k_recount, dim3(1), dim3(64), 0, h->s, h->d, o - h->lo);
+    HIPCHK(h, hipStreamSynchronize(h->s));
+    return SWIMSIM_OK;
+}
+
 int swimsim_make_change(swimsim_t *h, uint32_t o, uint32_t m, int64_t inc_ms, int32_t status) {
     if (!h || !own(h, o) || m >= h->N || status < 0 || status > 4) return SWIMSIM_EINVAL;
     uint32_t e;

@@ -87,6 +87,7 @@ def load_library(path: str = LIB_PATH):
         "swimsim_init_converged": (C.c_int, [P]),
         "swimsim_init_self_only": (C.c_int, [P]),
         "swimsim_set_member": (C.c_int, [P, u32, u32, i32, i64]),
+        "swimsim_set_row": (C.c_int, [P, u32, P, P]),
         "swimsim_make_change": (C.c_int, [P, u32, u32, i64, i32]),
         "swimsim_clear_changes": (C.c_int, [P, u32]),
         "swimsim_set_live": (C.c_int, [P, u32, i32]),
@@ -252,6 +253,14 @@ class Cluster:
     # ---- setup -----------------------------------------------------------------------------
     def set_member(self, o, m, status, inc):
         self._chk(load_library().swimsim_set_member(self.h, o, m, status, inc))
+
+    def set_row(self, o, status, inc):
+        """raw write of observer o's whole row (swimsim_set_row); UNKNOWN marks a non-member"""
+        st = np.ascontiguousarray(status, dtype=np.uint8)
+        ic = np.ascontiguousarray(inc, dtype=np.int64)
+        if st.shape != (self.n,) or ic.shape != (self.n,):
+            raise ValueError(f"set_row needs two length-{self.n} columns")
+        self._chk(load_library().swimsim_set_row(self.h, o, st.ctypes.data, ic.ctypes.data))
 
     def make_change(self, o, m, inc, status):
         return self._chk(load_library().swimsim_make_change(self.h, o, m, inc, status))
@@ -482,6 +491,9 @@ class ShardedCluster:
     # setup calls act on the owning shard (row writes) or on every shard (topology)
     def set_member(self, o, m, status, inc):
         self.owner(o).set_member(o, m, status, inc)
+
+    def set_row(self, o, status, inc):
+        self.owner(o).set_row(o, status, inc)
 
     def make_change(self, o, m, inc, status):
         return self.owner(o).make_change(o, m, inc, status)
