@@ -1,0 +1,96 @@
+"""Join and bootstrap (swimsim.join).
+
+A cluster bootstraps from one seed member: every other member starts stopped and knowing only itself,
+then joins through up to joinSize = 3 members already in (join_sender.go:51), taking their
+joinResponse membership (join_handler.go:52-77, memberlist.go:398-406). CPU: the oracle alone
+converges to a full alive membership. GPU: the engine and the oracle run the same joins and rounds
+and match bit for bit each round (checksums, row/dissemination/timer digests, counters).
+"""
+import numpy as np
+import pytest
+
+import swimsim
+from swimsim import join as J
+from oracle_ffi import OracleSim
+
+
+def _plan(n, every):
+    """(round, joiner, coordinators): one member joins every `every` rounds through the first 3 joined"""
+    out, joined = [], [0]
+    for k, j in enumerate(J.bootstrap_order(n)):
+        out.append((1 + k * every, j, joined[:3]))
+        joined.append(j)
+    return out
+
+
+def _stop_all_but_seed(c, n):
+    for m in range(1, n):
+        c.set_live(m, 0)
+
+
+def _run(clusters, n, rounds, every, check=None):
+    plan = {r: (j, co) for r, j, co in _plan(n, every)}
+    for _ in range(rounds):
+        r = clusters[0].round
+        if r in plan:
+            j, co = plan[r]
+            res = [J.join(c, j, co) for c in clusters]
+            assert all(x == res[0] for x in res), f"join of {j}: {res}"
+        for c in clusters:
+            c.step(1) if isinstance(c, swimsim.Cluster) else c.step(())
+        if check:
+            check(r)
+
+
+def test_join_errors():
+    ora = OracleSim(4, init="self")
+    with pytest.raises(ValueError):
+        J.join(ora, 1, [])
+    with pytest.raises(ValueError):
+        J.join(ora, 1, [1])
+
+
+def test_bootstrap_converges_on_oracle():
+    n, every = 12, 2
+    ora = OracleSim(n, init="self")
+    _stop_all_but_seed(ora, n)
+    _run([ora], n, 1 + n * every + 60, every)
+    st, inc = ora.rows()
+    assert (st == swimsim.ALIVE).all(), "every member knows every other alive"
+    assert len(set(ora.checksums().tolist())) == 1
+    # each member's incarnation is its join round's clock (Reincarnate at join, memberlist.go:234-236)
+    for r, j, _ in _plan(n, every):
+        assert (inc[:, j] == ora.t0_ms + r * ora.period_ms).all()
+
+
+def test_joiner_takes_coordinator_membership_without_gossiping_it():
+    n = 8
+    ora = OracleSim(n, init="self")
+    _stop_all_but_seed(ora, n)
+    J.join(ora, 1, [0])
+    for _ in range(20):
+        ora.step(())
+    res = J.join(ora, 2, [0, 1])
+    st, _ = ora.row(2)
+    assert st[0] == st[1] == st[2] == swimsim.ALIVE and (st[3:] == swimsim.UNKNOWN).all()
+    assert res["applied"] == 2                     # 0 and 1 from coordinator 0; coordinator 1 adds nothing new
+    assert list(ora.dis_entries(2)) == [2]         # only its own Reincarnate change is disseminated
+
+
+@pytest.mark.gpu
+def test_gpu_bootstrap_parity_with_oracle():
+    n, every = 48, 2
+    eng = swimsim.Cluster(n, device=0, init="self")
+    ora = OracleSim(n, init="self")
+    _stop_all_but_seed(eng, n)
+    _stop_all_but_seed(ora, n)
+
+    def check(r):
+        ec, oc = eng.checksums(), ora.checksums()
+        assert (ec == oc).all(), f"round {r}: checksums differ at {np.nonzero(ec != oc)[0][:5]}"
+        assert eng.digest() == ora.digest(), f"round {r}: state digests differ"
+        assert eng.counters() == ora.counters(), f"round {r}: counters differ"
+
+    _run([eng, ora], n, 1 + n * every + 40, every, check)
+    st, _ = eng.rows()
+    assert (st == swimsim.ALIVE).all()
