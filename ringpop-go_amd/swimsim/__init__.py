@@ -444,6 +444,20 @@ class ShardedCluster:
     def round(self):
         return self.shards[0].round
 
+    @property
+    def t0_ms(self):
+        return self.shards[0].t0_ms
+
+    @property
+    def period_ms(self):
+        return self.shards[0].period_ms
+
+    def checksum(self, o):
+        return self.owner(o).checksum(o)
+
+    def member(self, o, m):
+        return self.owner(o).member(o, m)
+
     def checksums(self):
         return np.concatenate([c.checksums() for c in self.shards])
 

@@ -37,7 +37,7 @@ def _run(clusters, n, rounds, every, check=None):
             res = [J.join(c, j, co) for c in clusters]
             assert all(x == res[0] for x in res), f"join of {j}: {res}"
         for c in clusters:
-            c.step(1) if isinstance(c, swimsim.Cluster) else c.step(())
+            c.step(()) if isinstance(c, OracleSim) else c.step(1)
         if check:
             check(r)
 
@@ -94,3 +94,20 @@ def test_gpu_bootstrap_parity_with_oracle():
     _run([eng, ora], n, 1 + n * every + 40, every, check)
     st, _ = eng.rows()
     assert (st == swimsim.ALIVE).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nshards", [2, 3])
+def test_gpu_sharded_bootstrap_matches_single(nshards):
+    """joins on observer-row shards (ShardedCluster routes each call to the joiner's owner shard)"""
+    n, every = 40, 2
+    one = swimsim.Cluster(n, device=0, init="self")
+    sh = swimsim.ShardedCluster(n, nshards, init="self")
+    _stop_all_but_seed(one, n)
+    _stop_all_but_seed(sh, n)
+
+    def check(r):
+        assert (one.checksums() == sh.checksums()).all(), f"round {r}: checksums differ"
+        assert one.digest() == sh.digest(), f"round {r}: state digests differ"
+
+    _run([one, sh], n, 1 + n * every + 30, every, check)
