@@ -205,3 +205,18 @@ def test_gpu_seed_rows_from_join_response():
         assert (s1 == s2).all() and (i1 == i2).all()
         assert dst.checksum(o) == src.checksum(o) == jr.checksum
         assert dst.count_reachable(o) == src.count_reachable(o)
+
+
+@pytest.mark.gpu
+def test_gpu_seed_refuses_foreign_incarnations():
+    """the engine keeps incarnations as t0 + e*period: another value is refused, never rounded"""
+    eng = swimsim.Cluster(16, device=0)
+    before = eng.row(3)
+    bad = [W.Change(address=swimsim.address_of(m), incarnation=swimsim.T0_MS + 1, status="alive") for m in range(16)]
+    with pytest.raises(swimsim.SwimsimError):
+        W.seed_from_membership(eng, 3, bad)
+    st = np.full(16, 9, np.uint8)
+    with pytest.raises(swimsim.SwimsimError):
+        eng.set_row(3, st, np.full(16, swimsim.T0_MS, np.int64))
+    after = eng.row(3)
+    assert (before[0] == after[0]).all() and (before[1] == after[1]).all(), "a refused row write changed the row"
