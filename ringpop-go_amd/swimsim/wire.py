@@ -401,6 +401,34 @@ def ping_of(cluster, o: int, timestamp: int = GO_ZERO_TIME_UNIX) -> Ping:
                 cluster.member(o, o)[1])
 
 
+def issue_as_receiver(cluster, o: int, sender: str, sender_incarnation: int, sender_checksum: int,
+                      timestamp: int = GO_ZERO_TIME_UNIX):
+    """disseminator.IssueAsReceiver (disseminator.go:155-181) of observer o, read-only: the buffered
+    changes minus those that came from the sender at its incarnation (filterChangesFromSender,
+    185-199); if none are left and the checksums differ, the full membership and full_sync = True.
+    The device's piggyback counters are not bumped (the engine bumps them inside swimsim_step)."""
+    changes = [c for c in issue_as_sender(cluster, o, timestamp)
+               if not (c.source == sender and c.source_incarnation == sender_incarnation)]
+    if changes or cluster.checksum(o) == sender_checksum:
+        return changes, False
+    return membership_as_changes(cluster, o, timestamp), True
+
+
+def ping_request_of(cluster, o: int, target: int, timestamp: int = GO_ZERO_TIME_UNIX) -> PingRequest:
+    """the pingRequest body o sends to each helper about `target` (ping_request_sender.go:95-101)"""
+    return PingRequest(address_of(o), cluster.member(o, o)[1], address_of(target), cluster.checksum(o),
+                       issue_as_sender(cluster, o, timestamp))
+
+
+def ping_response_of(cluster, helper: int, req: PingRequest, ok: bool,
+                     timestamp: int = GO_ZERO_TIME_UNIX) -> PingResponse:
+    """the helper's answer to a pingRequest (handlePingRequest, ping_request_handler.go:32-76): the
+    relayed ping's outcome and IssueAsReceiver's changes, the full membership included when it falls
+    back to a full sync (whose flag the handler ignores, line 69)."""
+    changes, _full = issue_as_receiver(cluster, helper, req.source, req.source_incarnation, req.checksum, timestamp)
+    return PingResponse(bool(ok), req.target, changes)
+
+
 def membership_as_changes(cluster, o: int, timestamp: int = GO_ZERO_TIME_UNIX) -> List[Change]:
     """disseminator.MembershipAsChanges (disseminator.go:107-123): every known member, source = self"""
     st, inc = cluster.row(o)
@@ -429,6 +457,7 @@ def seed_from_membership(cluster, o: int, changes: List[Change]) -> int:
 
 
 __all__ = ["Change", "Ping", "PingRequest", "PingResponse", "JoinRequest", "JoinResponse", "WireError",
-           "go_string", "index_of", "changes_to_arrays", "issue_as_sender", "ping_of", "membership_as_changes",
+           "go_string", "index_of", "changes_to_arrays", "issue_as_sender", "issue_as_receiver", "ping_of",
+           "ping_request_of", "ping_response_of", "membership_as_changes",
            "join_response", "seed_from_membership", "GO_ZERO_TIME_UNIX", "STATUS_CODES",
            "ALIVE", "SUSPECT", "FAULTY", "LEAVE", "TOMBSTONE"]

@@ -165,6 +165,30 @@ def test_bridge_bodies_from_oracle_state():
     assert all(c.source == swimsim.address_of(o) for c in jr.membership)
 
 
+def test_ping_request_and_response_bodies_on_oracle():
+    wl = WL.config1()
+    ora = _oracle_after(wl, 4)            # six observers hold buffered suspect changes
+    v = OracleView(ora)
+    o = next(o for o in range(wl.n) if ora.dis_entries(o))
+    req = W.ping_request_of(v, o, 5)
+    assert (req.source, req.target) == (swimsim.address_of(o), swimsim.address_of(5))
+    assert req.changes == W.issue_as_sender(v, o) and req.checksum == ora.checksum(o)
+    assert W.PingRequest.from_json(req.to_json()) == req
+    # filterChangesFromSender: a helper drops what came from the requester at its incarnation
+    h = next(h for h in range(wl.n) if h != o and ora.dis_entries(h))
+    mine = W.issue_as_sender(v, h)
+    fake = W.PingRequest(mine[0].source, mine[0].source_incarnation, swimsim.address_of(5), ora.checksum(h), [])
+    res = W.ping_response_of(v, h, fake, True)
+    assert res.ok and res.target == swimsim.address_of(5)
+    assert res.changes == [c for c in mine if (c.source, c.source_incarnation) != (fake.source, fake.source_incarnation)]
+    # nothing left and checksums differ: IssueAsReceiver falls back to the full membership
+    quiet = next(q for q in range(wl.n) if q != 5 and not ora.dis_entries(q))
+    ch, full = W.issue_as_receiver(v, quiet, "x", 0, ora.checksum(quiet) ^ 1)
+    assert full and len(ch) == wl.n and all(c.source == swimsim.address_of(quiet) for c in ch)
+    ch, full = W.issue_as_receiver(v, quiet, "x", 0, ora.checksum(quiet))
+    assert (ch, full) == ([], False)
+
+
 def test_seed_from_join_response_reproduces_checksum_on_oracle():
     wl = WL.config1()
     ora = _oracle_after(wl, 40)           # member 5 faulty in every live row by now
@@ -189,6 +213,9 @@ def test_gpu_ping_and_join_bodies_match_oracle():
     for o in range(0, wl.n, 17):
         assert W.ping_of(eng, o).to_json() == W.ping_of(v, o).to_json(), f"ping body of {o}"
         assert W.join_response(eng, o, "ringpop").to_json() == W.join_response(v, o, "ringpop").to_json()
+        assert W.ping_request_of(eng, o, (o + 1) % wl.n).to_json() == W.ping_request_of(v, o, (o + 1) % wl.n).to_json()
+        req = W.ping_request_of(v, (o + 3) % wl.n, o)
+        assert W.ping_response_of(eng, o, req, True).to_json() == W.ping_response_of(v, o, req, True).to_json()
 
 
 @pytest.mark.gpu
