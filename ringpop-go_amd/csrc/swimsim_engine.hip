@@ -370,7 +370,12 @@ void drain_timing(swimsim *h) {
     h->pending.clear();
 }
 
-inline uint32_t blocks_for_waves(uint32_t waves) { return waves ? (waves + 3) / 4 : 1; }  // 4 waves per 256-thread block
+// wave-per-observer kernels (no LDS, no block barriers): SWIM_WAVE_BLOCK threads per workgroup
+#ifndef SWIM_WAVE_BLOCK
+#define SWIM_WAVE_BLOCK 256
+#endif
+constexpr uint32_t kWavesPerBlock = SWIM_WAVE_BLOCK / 64;
+inline uint32_t blocks_for_waves(uint32_t waves) { return waves ? (waves + kWavesPerBlock - 1) / kWavesPerBlock : 1; }
 inline uint32_t blocks_for_threads(uint32_t n) { return n ? (n + 255) / 256 : 1; }
 
 int build_tail_table(swimsim *h, uint32_t ecap) {
@@ -550,7 +555,7 @@ int xchg(swimsim *h) {
     }
     HIPCHK(h, hipMemcpyAsync(h->xseg, cur.data(), 3 * G * 8, hipMemcpyHostToDevice, h->s));
     if (nitems)
-        hipLaunchKernelGGL(k_x_pack, dim3(blocks_for_waves(nitems)), dim3(256), 0, h->s, h->d, x, h->xitems, h->xcnt,
+        hipLaunchKernelGGL(k_x_pack, dim3(blocks_for_waves(nitems)), dim3(SWIM_WAVE_BLOCK), 0, h->s, h->d, x, h->xitems, h->xcnt,
                            h->xcap, h->sbuf, h->xseg, h->xtcur, h->xdcur);
     HIPCHK(h, hipStreamSynchronize(h->s));
     if (int rc = h->xp->sizes(sendsz.data(), recvsz.data(), 2)) return h->fail(rc, "shard size exchange failed (%s)", h->xp->name());
@@ -573,7 +578,7 @@ int xchg(swimsim *h) {
         return h->fail(rc, "shard data exchange failed (%s)", h->xp->name());
     if (nparc) {
         HIPCHK(h, hipMemcpyAsync(h->xsrcs, srcs.data(), G * sizeof(ulonglong2), hipMemcpyHostToDevice, h->s));
-        hipLaunchKernelGGL(k_x_unpack, dim3(blocks_for_waves((uint32_t)nparc)), dim3(256), 0, h->s, h->d, x, h->rbuf,
+        hipLaunchKernelGGL(k_x_unpack, dim3(blocks_for_waves((uint32_t)nparc)), dim3(SWIM_WAVE_BLOCK), 0, h->s, h->d, x, h->rbuf,
                            h->xsrcs, G, (uint32_t)nparc);
     }
     HIPCHK(h, hipMemsetAsync(h->xcnt, 0, 4, h->s));
@@ -636,7 +641,7 @@ int checksum_dirty(swimsim *h, int mode, bool async = false) {
     auto go_side = [&](const uint32_t *rows, uint32_t n2, const uint32_t *vals, const uint32_t *dups) -> int {
         {
             Scope sc(h, F_CSPREP);
-            hipLaunchKernelGGL(k_snap_rows, dim3(blocks_for_waves(std::max(n2, 1u))), dim3(256), 0, h->s, h->d, rows, n2,
+            hipLaunchKernelGGL(k_snap_rows, dim3(blocks_for_waves(std::max(n2, 1u))), dim3(SWIM_WAVE_BLOCK), 0, h->s, h->d, rows, n2,
                                h->side_ids, h->side_cnt);
             hipLaunchKernelGGL(k_snap_dups, dim3(blocks_for_threads(n)), dim3(256), 0, h->s, h->d, vals, n, dups,
                                h->side_map);
@@ -665,7 +670,7 @@ int checksum_dirty(swimsim *h, int mode, bool async = false) {
         bytes = h->cub_bytes;
         HIPCHK(h, hipcub::DeviceScan::InclusiveScan(h->cub_tmp, bytes, h->fph, h->fph_s, hipcub::Max(), (int)n, h->s));
         HIPCHK(h, hipMemsetAsync(h->fpcnt, 0, 4, h->s));
-        hipLaunchKernelGGL(k_fp_verify, dim3(blocks_for_waves(n)), dim3(256), 0, h->s, h->d, h->fpv_s, h->fph_s, n, h->hflag,
+        hipLaunchKernelGGL(k_fp_verify, dim3(blocks_for_waves(n)), dim3(SWIM_WAVE_BLOCK), 0, h->s, h->d, h->fpv_s, h->fph_s, n, h->hflag,
                            h->dup_of);
         hipLaunchKernelGGL(k_list_flagged, dim3(blocks_for_threads(h->NL)), dim3(256), 0, h->s, h->NL, h->hflag, h->fplist,
                            h->fpcnt);
@@ -694,7 +699,7 @@ int resolve_deferred(swimsim *h, int phase, MsgDesc *rdesc, uint32_t maxn) {
     {
         Scope sc(h, F_CSPREP);
         HIPCHK(h, hipMemsetAsync(h->cnt, 0, 8, h->s));
-        hipLaunchKernelGGL(k_defer_eq, dim3(blocks_for_waves(maxn)), dim3(256), 0, h->s, h->d, h->defer, h->defer_cnt,
+        hipLaunchKernelGGL(k_defer_eq, dim3(blocks_for_waves(maxn)), dim3(SWIM_WAVE_BLOCK), 0, h->s, h->d, h->defer, h->defer_cnt,
                            phase, h->defer_eq);
         hipLaunchKernelGGL(k_defer_ids, dim3(blocks_for_threads(maxn)), dim3(256), 0, h->s, h->d, h->defer,
                            h->defer_cnt, h->defer_eq, h->list, h->cnt);
@@ -745,7 +750,7 @@ int run_waves(swimsim *h, int phase, uint32_t nruns_valid, uint32_t maxcount) {
     hipMemsetAsync(h->defer_cnt, 0, 4, h->s);
     {
         Scope sc(h, F_RECV);
-        hipLaunchKernelGGL(k_recv, dim3(blocks_for_waves(nruns_valid)), dim3(256), 0, h->s, h->d, a);
+        hipLaunchKernelGGL(k_recv, dim3(blocks_for_waves(nruns_valid)), dim3(SWIM_WAVE_BLOCK), 0, h->s, h->d, a);
     }
     const uint32_t maxdefer = std::min<uint64_t>((uint64_t)nruns_valid * maxcount, h->d.dense_cap);
     if (int rc = resolve_deferred(h, phase, a.rdesc, maxdefer)) return rc;
@@ -953,7 +958,7 @@ int step_one(swimsim *h, const swimsim_event *ev, size_t nev) {
     // ---- T: timers ----
     {
         Scope sc(h, F_TIMERS);
-        hipLaunchKernelGGL(k_timers, dim3(blocks_for_waves(h->NL)), dim3(256), 0, h->s, h->d, r);
+        hipLaunchKernelGGL(k_timers, dim3(blocks_for_waves(h->NL)), dim3(SWIM_WAVE_BLOCK), 0, h->s, h->d, r);
     }
     // ---- S: target selection ----
     {
@@ -971,7 +976,7 @@ int step_one(swimsim *h, const swimsim_event *ev, size_t nev) {
     {
         {
             Scope sc(h, F_ISSUE);
-            hipLaunchKernelGGL(k_issue, dim3(blocks_for_waves(h->NL)), dim3(256), 0, h->s, h->d, 0, h->tgt, h->failed,
+            hipLaunchKernelGGL(k_issue, dim3(blocks_for_waves(h->NL)), dim3(SWIM_WAVE_BLOCK), 0, h->s, h->d, 0, h->tgt, h->failed,
                                h->sdesc, h->sI, h->sC, h->sS);
         }
         Scope sc(h, F_SORT);
@@ -999,7 +1004,7 @@ int step_one(swimsim *h, const swimsim_event *ev, size_t nev) {
     // ---- R: responses ----
     {
         Scope sc(h, F_RESP);
-        hipLaunchKernelGGL(k_resp, dim3(blocks_for_waves(h->NL)), dim3(256), 0, h->s, h->d, h->tgt, h->failed, h->sdesc,
+        hipLaunchKernelGGL(k_resp, dim3(blocks_for_waves(h->NL)), dim3(SWIM_WAVE_BLOCK), 0, h->s, h->d, h->tgt, h->failed, h->sdesc,
                            h->rdesc, r);
     }
     // ---- Q: indirect pings (collective if any shard has a failed ping) ----
@@ -1015,7 +1020,7 @@ int step_one(swimsim *h, const swimsim_event *ev, size_t nev) {
         {
             {
                 Scope sc(h, F_ISSUE);
-                hipLaunchKernelGGL(k_issue, dim3(blocks_for_waves(h->NL)), dim3(256), 0, h->s, h->d, 1, h->tgt, h->failed,
+                hipLaunchKernelGGL(k_issue, dim3(blocks_for_waves(h->NL)), dim3(SWIM_WAVE_BLOCK), 0, h->s, h->d, 1, h->tgt, h->failed,
                                    h->sdesc2, h->sI2, h->sC2, h->sS2);
             }
             Scope sc(h, F_PINGREQ);
@@ -1039,7 +1044,7 @@ int step_one(swimsim *h, const swimsim_event *ev, size_t nev) {
         }
         {
             Scope sc(h, F_PINGREQ);
-            hipLaunchKernelGGL(k_resolve, dim3(blocks_for_waves(h->NL)), dim3(256), 0, h->s, h->d, h->tgt, h->failed,
+            hipLaunchKernelGGL(k_resolve, dim3(blocks_for_waves(h->NL)), dim3(SWIM_WAVE_BLOCK), 0, h->s, h->d, h->tgt, h->failed,
                                h->H, h->nh, h->sdesc2, h->rdesc2, r);
         }
     }
@@ -1057,7 +1062,7 @@ int step_one(swimsim *h, const swimsim_event *ev, size_t nev) {
     }
     {
         Scope sc(h, F_JOBS);
-        hipLaunchKernelGGL(k_jobs_snap, dim3(blocks_for_waves(h->NL)), dim3(256), 0, h->s, h->d, h->need, h->snapdesc);
+        hipLaunchKernelGGL(k_jobs_snap, dim3(blocks_for_waves(h->NL)), dim3(SWIM_WAVE_BLOCK), 0, h->s, h->d, h->need, h->snapdesc);
     }
     if (sharded) {
         hipLaunchKernelGGL(k_x_snap, dim3(blocks_for_threads(h->needcap)), dim3(256), 0, h->s, h->d, h->needlist,
@@ -1067,7 +1072,7 @@ int step_one(swimsim *h, const swimsim_event *ev, size_t nev) {
     {
         Scope sc(h, F_JOBS);
         for (uint32_t q = 0; q < h->maxjobs; q++)
-            hipLaunchKernelGGL(k_jobs_merge, dim3(blocks_for_waves(h->NL)), dim3(256), 0, h->s, h->d, q, h->snapdesc, r);
+            hipLaunchKernelGGL(k_jobs_merge, dim3(blocks_for_waves(h->NL)), dim3(SWIM_WAVE_BLOCK), 0, h->s, h->d, q, h->snapdesc, r);
         hipLaunchKernelGGL(k_jobs_reset, dim3(blocks_for_threads(std::max(h->NL, h->N))), dim3(256), 0, h->s, h->d,
                            h->need);
     }
@@ -1375,7 +1380,7 @@ int swimsim_destroy(swimsim_t *h) {
 }
 
 static int init_rows(swimsim_t *h, int mode) {
-    hipLaunchKernelGGL(k_init_rows, dim3(blocks_for_waves(h->NL)), dim3(256), 0, h->s, h->d, mode, 0u);
+    hipLaunchKernelGGL(k_init_rows, dim3(blocks_for_waves(h->NL)), dim3(SWIM_WAVE_BLOCK), 0, h->s, h->d, mode, 0u);
     checksum_dirty(h, 0);
     return check_err(h);
 }
@@ -1622,7 +1627,7 @@ int swimsim_counters(swimsim_t *h, uint64_t *out) {
 int swimsim_digest(swimsim_t *h, uint64_t *rows, uint64_t *dis, uint64_t *tim) {
     if (!h) return SWIMSIM_EINVAL;
     HIPCHK(h, hipMemsetAsync(h->digest_buf, 0, 32, h->s));
-    hipLaunchKernelGGL(k_digest, dim3(blocks_for_waves(h->NL)), dim3(256), 0, h->s, h->d, h->digest_buf, 0u);
+    hipLaunchKernelGGL(k_digest, dim3(blocks_for_waves(h->NL)), dim3(SWIM_WAVE_BLOCK), 0, h->s, h->d, h->digest_buf, 0u);
     unsigned long long v[3];
     HIPCHK(h, hipMemcpyAsync(v, h->digest_buf, 24, hipMemcpyDeviceToHost, h->s));
     HIPCHK(h, hipStreamSynchronize(h->s));
