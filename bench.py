@@ -100,11 +100,18 @@ def cpu_baseline(seconds_budget=25.0):
         if time.perf_counter() - t0 > seconds_budget:
             break
     dt = time.perf_counter() - t0
+    host = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            host = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), host)
+    except OSError:
+        pass
     return {
         "value": round(n * done / dt, 1),
         "unit": "member-rounds/s",
         "cores": 1,
         "kind": "port",
+        "host_cpu": host,
         "sample": f"C oracle (oracle/swim_oracle.c, -O2, 1 thread) on the config-3 protocol at N={n} "
                   f"(1% killed at r=10), rounds 0-{done - 1}, {dt:.1f} s; per-member-round cost grows ~linearly in N",
     }
