@@ -247,3 +247,29 @@ def test_gpu_seed_refuses_foreign_incarnations():
         eng.set_row(3, st, np.full(16, swimsim.T0_MS, np.int64))
     after = eng.row(3)
     assert (before[0] == after[0]).all() and (before[1] == after[1]).all(), "a refused row write changed the row"
+
+
+def test_round_trip_properties():
+    """random bodies: the encoding is valid JSON carrying the same values, and decodes to the body"""
+    import json
+    from hypothesis import given, settings, strategies as st
+
+    text = st.text(st.characters(blacklist_categories=("Cs",)), max_size=12)
+    i64 = st.integers(-(1 << 63), (1 << 63) - 1)
+    change = st.builds(W.Change, text, i64, text, i64, st.sampled_from(["alive", "suspect", "faulty", "leave"]),
+                       st.booleans(), i64)
+
+    @settings(max_examples=200, deadline=None)
+    @given(st.lists(change, max_size=5) | st.none(), st.integers(0, (1 << 32) - 1), text, i64)
+    def check(changes, checksum, source, sinc):
+        p = W.Ping(changes, checksum, source, sinc)
+        j = p.to_json()
+        plain = json.loads(j)
+        assert (plain["checksum"], plain["source"], plain["sourceIncarnationNumber"]) == (checksum, source, sinc)
+        assert list(plain) == ["changes", "checksum", "source", "sourceIncarnationNumber"]
+        if changes:
+            assert [c["address"] for c in plain["changes"]] == [c.address for c in changes]
+            assert all(("tombstone" in c) == x.tombstone for c, x in zip(plain["changes"], changes))
+        assert W.Ping.from_json(j) == p
+
+    check()
