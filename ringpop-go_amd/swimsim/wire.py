@@ -61,8 +61,8 @@ def go_string(s: str) -> str:
             out.append("\\u00" + _HEX[o >> 4] + _HEX[o & 15])
         elif o in (0x2028, 0x2029):
             out.append("\\u202" + _HEX[o & 15])
-        elif 0xD800 <= o <= 0xDFFF:          # lone surrogate: invalid UTF-8 becomes U+FFFD
-            out.append("�")
+        elif 0xD800 <= o <= 0xDFFF:          # invalid UTF-8 (a lone surrogate here): Go writes \ufffd
+            out.append("\\ufffd")
         else:
             out.append(ch)
     out.append('"')

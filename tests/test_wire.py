@@ -72,6 +72,7 @@ def test_go_string_escapes():
     assert W.go_string('q"\\\n\r\t\x01') == '"q\\"\\\\\\n\\r\\t\\u0001"'
     assert W.go_string(" x ") == '"\\u2028x\\u2029"'
     assert W.go_string("é") == '"é"'
+    assert W.go_string("a\udc80b") == '"a\\ufffdb"'        # invalid UTF-8 (surrogateescape) -> \ufffd
 
 
 def test_unmarshal_rules():
