@@ -1,25 +1,36 @@
 """bench.py — member-rounds/sec of the MI355X SWIM engine on BASELINE.json's 65,536-member config.
 
 Workload (BASELINE.json configs[2], the metric's "64k members"): 65,536 members, converged start,
-1 % (655) killed at round 10, then the suspect wave and the faulty wave ~25 rounds later.
-One "step" is one synchronous protocol round of every member (docs/ROUND_SEMANTICS.md §4).
---warmup W rounds (default 10: rounds 0-9, steady state) run untimed. --steps K rounds (default
-90: rounds 10-99, the kill and both cascades) are timed between barrier+synchronize brackets.
+1 % (655) killed at round 10 (fixed, whatever --warmup is), then the suspect wave and, 25 rounds
+after each suspect declaration, the faulty wave. One "step" is one synchronous protocol round of
+every live member (docs/ROUND_SEMANTICS.md §4). --warmup W rounds (0..W-1) run untimed; --steps K
+rounds (W..W+K-1) are timed between barrier + synchronize brackets. The JSON line names the window.
 
---gpus N > 1 (one process per GPU, launched by torch.distributed.run): the same 65,536-member
-cluster's observer rows are sharded over the N GPUs (rank r holds rows [N*r/G, N*(r+1)/G)) and every
-cross-shard message moves over RCCL point-to-point on xGMI inside libswimsim. Total work is fixed, so
-"scaling" is "strong". value = members x K / max-over-ranks time.
+value = live member-rounds in the timed window / max-over-ranks time. A member killed at round r
+executes no protocol period from round r on (SURVEY.md §8(d) counts live members only).
+
+--gpus N > 1: without WORLD_SIZE in the environment, bench.py starts N ranks itself
+(`python -m torch.distributed.run --nproc-per-node N bench.py ...` as a child process, before this
+process touches the GPU) and exits with its status; the child's rank 0 prints the line. Each rank
+holds observer rows [N*r/G, N*(r+1)/G) of the same 65,536-member cluster on GPU LOCAL_RANK, and every
+cross-shard message moves over RCCL point-to-point (xGMI) inside libswimsim. Total work is fixed, so
+"scaling" is "strong".
 
 The JSON line carries:
-  roofline     : for the kernel family with the most device time (rank 0), its algorithmic bytes per
-                 launch / HIP-event-measured average launch time (events on the engine's stream) vs the
-                 8 TB/s HBM peak; merge_kernel_GBps is the same figure for the receive-merge family.
-  cpu_baseline : the C oracle (single thread) on a bounded sample of the same protocol, rank 0, N=1 only.
+  roofline     : the kernel with the most device time (rank 0): its algorithmic bytes per launch
+                 (DESIGN.md §8 per-unit figures x the units the launch processed, counted on the device
+                 during the timed rounds) / its average launch time (HIP events on the engine's own
+                 stream), against the 8 TB/s HBM peak. `traffic` is FETCH_SIZE + WRITE_SIZE per launch from
+                 the rocprofv3 PMC passes of THIS command (profiles/r02_pmc_summary.json; null when that
+                 summary was taken on another workload). `merge` gives the same figures for the merge
+                 kernels (k_recv, k_resp, k_issue); `merge_kernel` repeats k_recv, the north-star kernel.
+  cpu_baseline : the C oracle on the GPU box's host cores (rank 0, N=1 only), bounded sample.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -28,21 +39,26 @@ sys.path.insert(0, os.path.join(REPO, "ringpop-go_amd"))
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 VALU_PEAK_GINST = 256 * 4 * 2.4 / 2  # wave-instructions/ns: 1024 SIMDs, one wave64 VALU op per 2 cycles at 2.4 GHz
+KILL_ROUND = 10
 # kernel family (swimsim_kernel_times) -> kernel symbols in the rocprofv3 PMC summary
 FAMILY_KERNELS = {"checksum": ["swimdev::k_checksum<19, 11, 9, 0>", "swimdev::k_checksum_n16<19, 11, 9, 0>"],
                   "recv_merge": ["swimdev::k_recv"], "issue": ["swimdev::k_issue"], "resp_merge": ["swimdev::k_resp"],
                   "timers": ["swimdev::k_timers"]}
-PMC_SUMMARY = os.path.join(REPO, "profiles", "r01_pmc_summary.json")
+FAMILY_SYMBOL = {"checksum": "k_checksum", "recv_merge": "k_recv", "resp_merge": "k_resp", "issue": "k_issue",
+                 "timers": "k_timers"}
+PMC_SUMMARY = os.path.join(REPO, "profiles", "r02_pmc_summary.json")
 
 
-def pmc_family(family):
-    """Per-launch PMC figures of the family's kernels (launch-weighted over the committed PMC passes of this
-    bench: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / SQ_INSTS_VALU..., separate runs; tools/pmc_summary.py),
-    or None."""
+def pmc_family(family, workload):
+    """Per-launch PMC figures of the family's kernels, launch-weighted over the committed rocprofv3 --pmc
+    passes (FETCH_SIZE / WRITE_SIZE / SQ_INSTS_VALU..., separate runs; tools/pmc_summary.py), or None when the
+    summary is missing or was collected on a different workload than this run's."""
     try:
         with open(PMC_SUMMARY) as f:
             t = json.load(f)
-        ks = [t[k] for k in FAMILY_KERNELS[family] if k in t]
+        if t.get("_workload") != workload:
+            return None
+        ks = [t[k] for k in FAMILY_KERNELS.get(family, []) if k in t]
     except (OSError, KeyError, ValueError):
         return None
     n = sum(k["launches"] for k in ks)
@@ -83,38 +99,54 @@ def dist_env():
     return ws, rank, local
 
 
-def cpu_baseline(seconds_budget=25.0):
-    """Oracle (tests/oracle_ffi.py, CPU restatement) on a bounded sample of the config-3 protocol."""
-    sys.path.insert(0, os.path.join(REPO, "tests"))
-    from oracle_ffi import OracleSim
+def live_member_rounds(wl, first, last):
+    """sum over rounds first..last of the members alive in that round (events apply in phase E)"""
     from swimsim import workloads as W
 
-    n, rounds = 4096, 40
-    wl = W.config3(n=n, rounds=rounds)
-    sim = OracleSim(n)
-    t0 = time.perf_counter()
-    done = 0
-    for r in range(rounds):
-        sim.step(wl.events_for(r))
-        done += 1
-        if time.perf_counter() - t0 > seconds_budget:
-            break
-    dt = time.perf_counter() - t0
-    host = "unknown"
-    try:
-        with open("/proc/cpuinfo") as f:
-            host = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), host)
-    except OSError:
-        pass
-    return {
-        "value": round(n * done / dt, 1),
-        "unit": "member-rounds/s",
-        "cores": 1,
-        "kind": "port",
-        "host_cpu": host,
-        "sample": f"C oracle (oracle/swim_oracle.c, -O2, 1 thread) on the config-3 protocol at N={n} "
-                  f"(1% killed at r=10), rounds 0-{done - 1}, {dt:.1f} s; per-member-round cost grows ~linearly in N",
-    }
+    live = [True] * wl.n
+    nlive, total = wl.n, 0
+    for r in range(0, last + 1):
+        for (_, k, a, _b) in wl.events_for(r):
+            if k == W.EV_KILL and live[a]:
+                live[a] = False
+                nlive -= 1
+            elif k == W.EV_REVIVE and not live[a]:
+                live[a] = True
+                nlive += 1
+        if r >= first:
+            total += nlive
+    return total
+
+
+def cpu_baseline(gpu_window, seconds_budget=25.0):
+    """The CPU oracle on a bounded sample of the same protocol (tools/cpu_baseline.py does the timing in a
+    child process so that OpenMP threads do not share this process with the HIP runtime)."""
+    out = subprocess.run([sys.executable, os.path.join(REPO, "tools", "cpu_baseline.py"), "--budget",
+                          str(seconds_budget), "--window", gpu_window], capture_output=True, text=True, timeout=600)
+    if out.returncode != 0:
+        return {"error": out.stderr[-400:]}
+    return json.loads(out.stdout.strip().splitlines()[-1])
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args):
+    """--gpus N without a launcher: start N ranks as a child torch.distributed.run, relay its status."""
+    if not args.launch_check:
+        import torch  # device_count() does not initialise the GPU on this image
+
+        have = torch.cuda.device_count()
+        if have < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but only {have} GPU(s) visible", file=sys.stderr)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.run(cmd, env=env).returncode
 
 
 def main():
@@ -124,12 +156,23 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--members", type=int, default=65536)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-ring", action="store_true")
     # diagnostics: every rank on cuda:0, shards exchanging through the gloo host transport instead of
     # RCCL (lets the multi-process path run on a one-GPU machine); never used for reported numbers
     ap.add_argument("--host-transport", action="store_true")
+    # test hook: the ranks report (rank, world size) and exit before any GPU call
+    ap.add_argument("--launch-check", action="store_true")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     ws, rank, local = dist_env()
+    if ws != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws}")
+    if args.launch_check:
+        print(json.dumps({"rank": rank, "world_size": ws, "local_rank": local}), flush=True)
+        return
+
     import torch
 
     if not torch.cuda.is_available():
@@ -141,8 +184,8 @@ def main():
         import torch.distributed as dist
 
         # launcher plumbing only (RCCL id broadcast, barriers, max-over-ranks time); the data path is
-        # libswimsim's own RCCL communicator
-        # gloo prints its connection banner on the C-level stdout; keep stdout for the one JSON line
+        # libswimsim's own RCCL communicator. gloo prints its banner on the C-level stdout: keep stdout
+        # for the one JSON line
         sys.stdout.flush()
         saved = os.dup(1)
         os.dup2(2, 1)
@@ -159,7 +202,8 @@ def main():
 
     n = args.members
     total_rounds = args.warmup + args.steps
-    wl = W.config3(n=n, rounds=total_rounds)
+    wl = W.config3(n=n, rounds=max(total_rounds, KILL_ROUND + 1), kill_round=KILL_ROUND)
+    nkilled = sum(1 for e in wl.events if e[1] == W.EV_KILL)
     if ws > 1:
         from swimsim import dist as sd
 
@@ -197,36 +241,34 @@ def main():
     eng.enable_timing(False)
     if ws > 1:
         counters = sd.reduce_counters(counters)
-    dominant = max(kt.items(), key=lambda kv: kv[1]["avg_ms"] * kv[1]["launches"])
-    fam, info = dominant
-    per_launch_bytes = info["alg_bytes"] / max(1, info["launches"])
-    achieved = per_launch_bytes / (info["avg_ms"] * 1e-3) / 1e9 if info["avg_ms"] > 0 else 0.0
-    pmc = pmc_family(fam)
-    merge = kt.get("recv_merge", {})
-    merge_gbps = (merge.get("alg_bytes", 0) / max(1, merge.get("launches", 1))) / (merge.get("avg_ms", 1) * 1e-3) / 1e9 \
-        if merge.get("avg_ms", 0) > 0 else 0.0
+    workload = {"members": n, "steps": args.steps, "warmup": args.warmup, "gpus": ws}
 
     def family_roofline(f):
-        # algorithmic bytes per launch / HIP-event time, and the PMC-measured HBM bytes per launch of the
-        # same kernels over the same time (the gathers' sector traffic: what actually bounds them)
+        # algorithmic bytes per launch / HIP-event time of the same launches; PMC traffic of this command
         k = kt.get(f, {})
         if not k.get("avg_ms"):
             return None
         sec = k["avg_ms"] * 1e-3
-        alg = k["alg_bytes"] / max(1, k["launches"]) / sec / 1e9
-        p = pmc_family(f)
-        out = {"kernel": FAMILY_KERNELS[f][0], "avg_launch_ms": round(k["avg_ms"], 4), "launches": k["launches"],
-               "achieved_alg": round(alg, 2), "frac_alg": round(alg / HBM_PEAK_GBPS, 4), "unit": "GB/s"}
-        if p:
-            hbm = p["traffic"] / sec / 1e9
-            out.update({"traffic_per_launch": p["traffic"], "achieved_hbm": round(hbm, 2),
-                        "frac_hbm": round(hbm / HBM_PEAK_GBPS, 4)})
+        per_launch = k["alg_bytes"] / max(1, k["launches"])
+        alg = per_launch / sec / 1e9
+        p = pmc_family(f, workload)
+        out = {"kernel": FAMILY_SYMBOL.get(f, f), "avg_launch_ms": round(k["avg_ms"], 4), "launches": k["launches"],
+               "alg_bytes_per_launch": round(per_launch, 1), "achieved": round(alg, 2),
+               "frac": round(alg / HBM_PEAK_GBPS, 4), "unit": "GB/s",
+               "traffic": p["traffic"] if p else None,
+               "traffic_over_alg": round(p["traffic"] / per_launch, 2) if p and per_launch > 0 else None}
         return out
 
     if rank == 0:
-        value = n * args.steps / dt
+        timed_first, timed_last = args.warmup, total_rounds - 1
+        live_mr = live_member_rounds(wl, timed_first, timed_last)
+        value = live_mr / dt
+        dominant = max(kt.items(), key=lambda kv: kv[1]["avg_ms"] * kv[1]["launches"])[0]
+        dom = family_roofline(dominant)
+        in_window = timed_first <= KILL_ROUND <= timed_last
+        faulty_from = KILL_ROUND + 26       # suspect declared at KILL_ROUND, timer fires 25 rounds later at the earliest
         line = {
-            "metric": "simulated member-rounds/sec at 64k members",
+            "metric": "simulated member-rounds/sec at 64k members" if n == 65536 else f"simulated member-rounds/sec at {n} members",
             "value": round(value, 1),
             "unit": "member-rounds/s",
             "n_gpus": ws,
@@ -237,33 +279,36 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "u32",
-            "data": f"synthetic (converged {n}-member cluster; {max(1, n // 100)} members killed at round 10; Philox seed 11)",
-            "config": {"workload": f"config3_cascade: {n} members, 1% killed at r={args.warmup}, rounds {args.warmup}-{total_rounds - 1} timed",
-                       "members": n, "rounds_timed": args.steps,
+            "data": f"synthetic (converged {n}-member cluster; {nkilled} members killed at round {KILL_ROUND}; Philox seed 11)",
+            "config": {"workload": f"config3_cascade: {n} members, {nkilled} killed at r={KILL_ROUND}; rounds "
+                                   f"{timed_first}-{timed_last} timed (" +
+                                   ("steady state, kill, suspect wave" if in_window else "no kill in window") +
+                                   ("; faulty wave from r>=%d in window" % faulty_from if timed_last >= faulty_from
+                                    else "; faulty wave (r>=%d) outside the window" % faulty_from) + ")",
+                       "members": n, "rounds_timed": args.steps, "live_member_rounds": live_mr,
                        "parallelism": (f"observer-row shards x{ws} over " + ("host transport (diagnostic)" if args.host_transport
                                                                               else "RCCL")) if ws > 1 else "1 GPU"},
-            "roofline": {"bound": "hbm", "kernel": fam, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5),
-                         "traffic": pmc["traffic"] if pmc else None,
+            "roofline": {"bound": "hbm", **(dom or {}), "peak": HBM_PEAK_GBPS,
                          "traffic_unit": "bytes per launch (FETCH_SIZE + WRITE_SIZE, " + os.path.basename(PMC_SUMMARY) + ")",
-                         "avg_launch_ms": round(info["avg_ms"], 5), "launches": info["launches"],
-                         "merge_kernel_GBps": round(merge_gbps, 2),
+                         "merge_kernel": family_roofline("recv_merge"),
                          "merge": {f: family_roofline(f) for f in ("recv_merge", "resp_merge", "issue")}},
             "kernel_ms": {k: round(v["avg_ms"] * v["launches"], 3) for k, v in kt.items()},
             "counters": counters,
         }
-        if pmc and pmc["valu_insts"] and info["avg_ms"] > 0:
+        pmc = pmc_family(dominant, workload)
+        if dominant == "checksum" and pmc and pmc["valu_insts"] and kt[dominant]["avg_ms"] > 0:
             # the checksum is integer-VALU work: its instruction rate against the chip's VALU issue peak
-            rate = pmc["valu_insts"] / (info["avg_ms"] * 1e6)
+            rate = pmc["valu_insts"] / (kt[dominant]["avg_ms"] * 1e6)
             line["roofline"]["valu"] = {"achieved": round(rate, 2), "peak": VALU_PEAK_GINST, "unit": "G wave-instr/s",
                                         "frac": round(rate / VALU_PEAK_GINST, 4),
                                         "valu_insts_per_launch": round(pmc["valu_insts"]),
                                         "lds_insts_per_launch": round(pmc["lds_insts"])}
         if ws > 1:
-            line["exchange"] = {"bytes_rank0": shard["exchanged_bytes"], "exchanges_rank0": shard["exchanges"]}
+            line["exchange"] = {"bytes_rank0": shard["exchanged_bytes"], "exchanges_rank0": shard["exchanges"],
+                                "bytes_per_round_rank0": round(shard["exchanged_bytes"] / max(1, total_rounds), 1)}
         if ws == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline()
-        if ws == 1:
+            line["cpu_baseline"] = cpu_baseline(f"{n}:{args.warmup}:{args.steps}")
+        if ws == 1 and not args.no_ring:
             line["hashring"] = ring_bench(n)
         print(json.dumps(line), flush=True)
     if ws > 1:

@@ -101,6 +101,13 @@ static void omap_clear(omap *m) {
 /* ------------------------------------------------------------------------------------------ */
 typedef struct obs {
     omap dis;             /* disseminator.changes (disseminator.go:44-45) */
+    int32_t nmem;         /* len(memberlist.members.list) (memberlist.go:174-179), kept incrementally */
+    /* applied-change log of a watched observer (MemberlistChangesAppliedEvent, events.go:56-61):
+     * the last applied change of every member since the last drain */
+    int32_t watched;
+    uint32_t wcs_prev;    /* checksum at the last drain (the event's OldChecksum) */
+    uint8_t *wdirty;      /* [n] */
+    or_change *wlast;     /* [n] */
     omap tim;             /* stateTransitions.timers (state_transitions.go:49) */
     int64_t clock_off;
     uint32_t cs;          /* memberlist.members.checksum (memberlist.go:46) */
@@ -127,17 +134,21 @@ struct or_sim {
     uint32_t addr_cap;
     uint64_t counters[OR_NCOUNTERS];
     int32_t *last_target;
-    /* scratch */
-    char *csbuf;
-    size_t csbuf_cap;
-    int64_t now_override;  /* >= 0 inside a timer callback: Mock.Add sets now = timer deadline */
 };
+
+/* Per-thread scratch: the OpenMP build (libswim_oracle_omp.so, CPU baseline only) runs the per-observer
+ * loops of a phase in parallel. Observers of one phase touch only their own row, maps and timers, so the
+ * results equal the single-threaded oracle's; counters are atomic. */
+static __thread char *tl_csbuf;
+static __thread size_t tl_csbuf_cap;
+static __thread int64_t tl_now_override = -1;  /* >= 0 inside a timer callback: Mock.Add sets now = deadline */
+#define CTR_ADD(s, c, v) __atomic_fetch_add(&(s)->counters[(c)], (uint64_t)(v), __ATOMIC_RELAXED)
 
 #define ST(s, o, m) ((s)->st[(size_t)(o) * (s)->n + (m)])
 #define INC(s, o, m) ((s)->inc[(size_t)(o) * (s)->n + (m)])
 
 static int64_t now_ms(const or_sim *s, uint32_t o) {
-    if (s->now_override >= 0) return s->now_override;
+    if (tl_now_override >= 0) return tl_now_override;
     return s->cfg.t0_ms + (int64_t)s->round * s->cfg.period_ms + s->o[o].clock_off;
 }
 
@@ -190,7 +201,6 @@ or_sim *or_create(const or_config *cfg) {
             s->addr_len[i] = (uint32_t)strlen(a);
         }
     }
-    s->now_override = -1;
     s->last_target = (int32_t *)malloc(sizeof(int32_t) * s->n);
     for (uint32_t i = 0; i < s->n; i++) s->last_target[i] = -1;
     return s;
@@ -202,9 +212,11 @@ void or_destroy(or_sim *s) {
         omap_free(&s->o[i].dis);
         omap_free(&s->o[i].tim);
         free(s->o[i].jobs);
+        free(s->o[i].wdirty);
+        free(s->o[i].wlast);
     }
     free(s->o); free(s->st); free(s->inc); free(s->addr); free(s->addr_len);
-    free(s->last_target); free(s->csbuf);
+    free(s->last_target);
     free(s);
 }
 
@@ -216,11 +228,13 @@ void or_recompute_pingable(or_sim *s, uint32_t o) {
 }
 
 void or_init_converged(or_sim *s) {
+#pragma omp parallel for schedule(static)
     for (uint32_t o = 0; o < s->n; o++) {
         for (uint32_t m = 0; m < s->n; m++) {
             ST(s, o, m) = OR_ALIVE;
             INC(s, o, m) = s->cfg.t0_ms;
         }
+        s->o[o].nmem = (int32_t)s->n;
         or_recompute_pingable(s, o);
         s->o[o].maxp = s->o[o].pfactor * digits10(s->o[o].pingable);
         s->o[o].cs_dirty = 1;
@@ -231,6 +245,7 @@ void or_init_self_only(or_sim *s) {
     for (uint32_t o = 0; o < s->n; o++) {
         ST(s, o, o) = OR_ALIVE;
         INC(s, o, o) = s->cfg.t0_ms;
+        s->o[o].nmem = 1;
         or_recompute_pingable(s, o);
         s->o[o].maxp = s->o[o].pfactor;  /* newDisseminator: maxP = defaultPFactor (disseminator.go:62) */
         s->o[o].cs_dirty = 1;
@@ -241,6 +256,7 @@ void or_set_member(or_sim *s, uint32_t o, uint32_t m, int32_t status, int64_t in
     ST(s, o, m) = (uint8_t)status;
     INC(s, o, m) = inc;
     or_recompute_pingable(s, o);
+    s->o[o].nmem = or_num_members(s, o);
     s->o[o].cs_dirty = 1;
 }
 
@@ -335,17 +351,17 @@ static const char *STATUS_STR[5] = {"alive", "suspect", "faulty", "leave", "tomb
 
 static int cmp_cstr(const void *a, const void *b) { return strcmp(*(const char *const *)a, *(const char *const *)b); }
 
-static void csbuf_reserve(or_sim *s, size_t need) {
-    if (s->csbuf_cap >= need) return;
-    s->csbuf_cap = need * 2;
-    s->csbuf = (char *)realloc(s->csbuf, s->csbuf_cap);
+static void csbuf_reserve(size_t need) {
+    if (tl_csbuf_cap >= need) return;
+    tl_csbuf_cap = need * 2;
+    tl_csbuf = (char *)realloc(tl_csbuf, tl_csbuf_cap);
 }
 
 /* GenChecksumString: fmt.Sprintf("%s%s%v", addr, status, inc) per non-tombstone member, sorted,
- * each followed by ";" (memberlist.go:106-128). Returns length; writes into s->csbuf. */
+ * each followed by ";" (memberlist.go:106-128). Returns length; writes into tl_csbuf. */
 static size_t gen_checksum_string(or_sim *s, uint32_t o) {
     size_t per = s->addr_cap + 32;
-    csbuf_reserve(s, (size_t)s->n * per + 1);
+    csbuf_reserve((size_t)s->n * per + 1);
     size_t len = 0;
     if (s->cfg.faithful_checksum) {
         char *pool = (char *)malloc((size_t)s->n * per);
@@ -361,9 +377,9 @@ static size_t gen_checksum_string(or_sim *s, uint32_t o) {
         qsort(v, k, sizeof(char *), cmp_cstr);
         for (uint32_t i = 0; i < k; i++) {
             size_t l = strlen(v[i]);
-            memcpy(s->csbuf + len, v[i], l);
+            memcpy(tl_csbuf + len, v[i], l);
             len += l;
-            s->csbuf[len++] = ';';
+            tl_csbuf[len++] = ';';
         }
         free(pool);
         free(v);
@@ -372,13 +388,13 @@ static size_t gen_checksum_string(or_sim *s, uint32_t o) {
         for (uint32_t m = 0; m < s->n; m++) {
             int32_t st = ST(s, o, m);
             if (st == OR_UNKNOWN || st == OR_TOMBSTONE) continue;
-            memcpy(s->csbuf + len, s->addr + (size_t)m * (s->addr_cap + 1), s->addr_len[m]);
+            memcpy(tl_csbuf + len, s->addr + (size_t)m * (s->addr_cap + 1), s->addr_len[m]);
             len += s->addr_len[m];
             size_t sl = strlen(STATUS_STR[st]);
-            memcpy(s->csbuf + len, STATUS_STR[st], sl);
+            memcpy(tl_csbuf + len, STATUS_STR[st], sl);
             len += sl;
-            len += (size_t)snprintf(s->csbuf + len, 24, "%lld", (long long)INC(s, o, m));
-            s->csbuf[len++] = ';';
+            len += (size_t)snprintf(tl_csbuf + len, 24, "%lld", (long long)INC(s, o, m));
+            tl_csbuf[len++] = ';';
         }
     }
     return len;
@@ -388,7 +404,7 @@ size_t or_checksum_string(or_sim *s, uint32_t o, char *out, size_t cap) {
     size_t len = gen_checksum_string(s, o);
     if (out && cap) {
         size_t c = len < cap ? len : cap;
-        memcpy(out, s->csbuf, c);
+        memcpy(out, tl_csbuf, c);
     }
     return len;
 }
@@ -397,7 +413,7 @@ uint32_t or_checksum(or_sim *s, uint32_t o) {
     obs *ob = &s->o[o];
     if (ob->cs_dirty) {
         size_t len = gen_checksum_string(s, o);
-        ob->cs = or_fingerprint32((const uint8_t *)s->csbuf, len);
+        ob->cs = or_fingerprint32((const uint8_t *)tl_csbuf, len);
         ob->cs_dirty = 0;
     }
     return ob->cs;
@@ -519,6 +535,7 @@ static void apply_row(or_sim *s, uint32_t j, const or_change *c) {
     if ((uint32_t)c->member != j) {
         s->o[j].pingable += (is_pingable_status(c->status) ? 1 : 0) - (is_pingable_status(old) ? 1 : 0);
     }
+    if (old == OR_UNKNOWN) s->o[j].nmem++;
     ST(s, j, c->member) = (uint8_t)c->status;
     INC(s, j, c->member) = c->inc;
 }
@@ -560,7 +577,7 @@ int32_t or_update(or_sim *s, uint32_t j, const or_change *ch, int32_t n, or_chan
             or_change ov = {c.member, OR_ALIVE, (int32_t)j, 0, t, t};
             apply_row(s, j, &ov);
             applied[na++] = ov;
-            s->counters[OR_C_REFUTES]++;
+            CTR_ADD(s, OR_C_REFUTES, 1);
             continue;
         }
         if (or_non_local_override(INC(s, j, c.member), cur, c.inc, c.status)) { /* 357-361 */
@@ -569,9 +586,22 @@ int32_t or_update(or_sim *s, uint32_t j, const or_change *ch, int32_t n, or_chan
         }
     }
     if (na > 0) {
-        s->o[j].cs_dirty = 1;                             /* ComputeChecksum (memberlist.go:367-368) */
+        obs *ob = &s->o[j];
+        ob->cs_dirty = 1;                                 /* ComputeChecksum (memberlist.go:367-368) */
+        if (s->cfg.reference_cost) {
+            /* the reference's cost model: checksum string rebuilt (and sorted when faithful_checksum) and
+             * hashed at every Update that applied something; NumPingableMembers rescans the list in
+             * AdjustMaxPropagations (disseminator.go:78, memberlist.go:188-198). Same results. */
+            or_checksum(s, j);
+            or_recompute_pingable(s, j);
+        }
+        if (ob->watched)                                  /* MemberlistChangesAppliedEvent (memberlist.go:378-383) */
+            for (int32_t i = 0; i < na; i++) {
+                ob->wdirty[applied[i].member] = 1;
+                ob->wlast[applied[i].member] = applied[i];
+            }
         handle_changes(s, j, applied, na);                /* memberlist.go:384 */
-        s->counters[OR_C_APPLIED] += (uint64_t)na;
+        CTR_ADD(s, OR_C_APPLIED, (uint64_t)na);
     }
     if (applied_out) memcpy(applied_out, applied, sizeof(or_change) * (size_t)(na < cap ? na : cap));
     free(applied);
@@ -589,7 +619,9 @@ static void evict(or_sim *s, uint32_t o, uint32_t m) {
     if (ST(s, o, m) == OR_UNKNOWN) return;
     if (is_pingable_status(ST(s, o, m))) s->o[o].pingable--;
     ST(s, o, m) = OR_UNKNOWN;   /* incarnation kept: the buffered change still reads (tombstone, inc) */
+    s->o[o].nmem--;
     s->o[o].cs_dirty = 1;
+    if (s->cfg.reference_cost) or_checksum(s, o);         /* RemoveMember → ComputeChecksum (memberlist.go:156-159) */
 }
 
 /* ------------------------------------------------------------------------------------------ */
@@ -693,9 +725,10 @@ int32_t or_issue_as_receiver(or_sim *s, uint32_t j, int32_t sender, int64_t send
 int32_t or_next(or_sim *s, uint32_t o) {
     obs *ob = &s->o[o];
     uint32_t n = s->n;
-    int32_t max_to_visit = 0;                             /* NumMembers */
-    for (uint32_t m = 0; m < n; m++) if (ST(s, o, m) != OR_UNKNOWN) max_to_visit++;
-    uint8_t *visited = (uint8_t *)calloc(n, 1);
+    int32_t max_to_visit = ob->nmem;                      /* NumMembers: len(list) (memberlist_iter.go:51) */
+    /* visited set: a short list while the walk is short (the common case), a bitmap beyond */
+    uint32_t few[64];
+    uint8_t *visited = NULL;
     int32_t nvisited = 0, result = -1;
     while (nvisited < max_to_visit) {
         ob->it_idx++;
@@ -705,7 +738,21 @@ int32_t or_next(or_sim *s, uint32_t o) {
         }
         uint32_t m = or_perm(s->cfg.seed, o, ob->it_epoch, n, (uint32_t)ob->it_idx);
         if (ST(s, o, m) == OR_UNKNOWN) continue;          /* not a list entry */
-        if (!visited[m]) { visited[m] = 1; nvisited++; }
+        int seen = 0;
+        if (visited) {
+            seen = visited[m];
+        } else {
+            for (int32_t i = 0; i < nvisited && !seen; i++) seen = few[i] == m;
+        }
+        if (!seen) {
+            if (!visited && nvisited == 64) {
+                visited = (uint8_t *)calloc(n, 1);
+                for (int32_t i = 0; i < 64; i++) visited[few[i]] = 1;
+            }
+            if (visited) visited[m] = 1;
+            else few[nvisited] = m;
+            nvisited++;
+        }
         if (m != o && is_pingable_status(ST(s, o, m))) { result = (int32_t)m; break; } /* Pingable 181-185 */
     }
     free(visited);
@@ -765,12 +812,12 @@ void or_fire_timers(or_sim *s, uint32_t o) {
         slot *e = omap_find(&ob->tim, v[i].member);
         if (!e) continue;
         e->b = 1;                                         /* fired; the entry stays in s.timers */
-        s->counters[OR_C_TIMERS_FIRED]++;
-        s->now_override = v[i].deadline;                  /* clock.Mock.runNextTimer: now = t.next */
+        CTR_ADD(s, OR_C_TIMERS_FIRED, 1);
+        tl_now_override = v[i].deadline;                  /* clock.Mock.runNextTimer: now = t.next */
         if (v[i].state == OR_SUSPECT) or_make_change(s, o, (uint32_t)v[i].member, v[i].subj, OR_FAULTY);  /* 90-97 */
         else if (v[i].state == OR_FAULTY) or_make_change(s, o, (uint32_t)v[i].member, v[i].subj, OR_TOMBSTONE); /* 100-107 */
         else evict(s, o, (uint32_t)v[i].member);          /* 110-117 */
-        s->now_override = -1;
+        tl_now_override = -1;
     }
     free(v);
 }
@@ -781,7 +828,7 @@ void or_fire_timers(or_sim *s, uint32_t o) {
 static void queue_rfs(or_sim *s, uint32_t j, int32_t src) {   /* tryStartReverseFullSync 257-278 */
     obs *ob = &s->o[j];
     if ((uint32_t)ob->njobs < s->cfg.max_rfs_jobs) ob->jobs[ob->njobs++] = src;
-    else s->counters[OR_C_RFS_OMITTED]++;
+    else CTR_ADD(s, OR_C_RFS_OMITTED, 1);
 }
 
 /* sendPingWithChanges o → t, response discarded (heal_partition.go:97-124) */
@@ -791,7 +838,7 @@ static void ping_with_changes(or_sim *s, uint32_t o, uint32_t t, const or_change
     or_update(s, t, ch, n, NULL, 0);                       /* handlePing: ping_handler.go:40 */
     int32_t k, fs;
     or_change *r = issue_as_receiver(s, t, (int32_t)o, inc, cs, &k, &fs);
-    if (fs) { s->counters[OR_C_FULL_SYNCS]++; queue_rfs(s, t, (int32_t)o); }
+    if (fs) { CTR_ADD(s, OR_C_FULL_SYNCS, 1); queue_rfs(s, t, (int32_t)o); }
     free(r);
 }
 
@@ -828,10 +875,10 @@ int32_t or_heal(or_sim *s, uint32_t o, int32_t *ret_out, int32_t cap) {
     while (nt != 0 && failures < 10) {
         int32_t target = targets[0];
         nt = del_target(targets, nt, target);
-        s->counters[OR_C_HEAL_ATTEMPTS]++;
+        CTR_ADD(s, OR_C_HEAL_ATTEMPTS, 1);
         if (!reach(s, o, (uint32_t)target)) {              /* sendJoinRequest fails */
             failures++;
-            s->counters[OR_C_HEAL_FAILURES]++;
+            CTR_ADD(s, OR_C_HEAL_FAILURES, 1);
             continue;
         }
         int32_t na, nb;
@@ -911,22 +958,25 @@ void or_step(or_sim *s, const or_event *ev, size_t nev) {
     for (size_t i = 0; i < nev; i++)
         if (ev[i].round == s->round) apply_event(s, &ev[i]);
     /* T */
+#pragma omp parallel for schedule(dynamic, 64)
     for (uint32_t o = 0; o < n; o++)
         if (s->o[o].live) or_fire_timers(s, o);
     /* S */
     int32_t *t = s->last_target;
+#pragma omp parallel for schedule(dynamic, 64)
     for (uint32_t o = 0; o < n; o++) t[o] = s->o[o].live ? or_next(s, o) : -1;
     /* I */
     msg *S = (msg *)calloc(n, sizeof(msg));
     uint32_t *C = (uint32_t *)calloc(n, sizeof(uint32_t));
     int64_t *I = (int64_t *)calloc(n, sizeof(int64_t));
+#pragma omp parallel for schedule(dynamic, 64)
     for (uint32_t o = 0; o < n; o++) {
         if (t[o] < 0) continue;
         S[o].v = issue_changes(s, o, &S[o].n);
         C[o] = or_checksum(s, o);
         I[o] = INC(s, o, o);
-        s->counters[OR_C_PINGS]++;
-        s->counters[OR_C_MSG_CHANGES] += (uint64_t)S[o].n;
+        CTR_ADD(s, OR_C_PINGS, 1);
+        CTR_ADD(s, OR_C_MSG_CHANGES, (uint64_t)S[o].n);
     }
     /* D: receiver j processes its inbox in ascending sender order (receivers are independent) */
     int32_t *cnt = (int32_t *)calloc(n + 1, sizeof(int32_t));
@@ -938,20 +988,22 @@ void or_step(or_sim *s, const or_event *ev, size_t nev) {
     for (uint32_t o = 0; o < n; o++)
         if (t[o] >= 0 && reach(s, o, (uint32_t)t[o])) inbox[cnt[t[o]] + fill[t[o]]++] = (int32_t)o;
     msg *R = (msg *)calloc(n, sizeof(msg));
+#pragma omp parallel for schedule(dynamic, 16)
     for (uint32_t j = 0; j < n; j++) {
         for (int32_t q = cnt[j]; q < cnt[j + 1]; q++) {
             uint32_t o = (uint32_t)inbox[q];
             or_update(s, j, S[o].v, S[o].n, NULL, 0);                   /* ping_handler.go:40 */
             int32_t fs;
             R[o].v = issue_as_receiver(s, j, (int32_t)o, I[o], C[o], &R[o].n, &fs);
-            s->counters[OR_C_MSG_CHANGES] += (uint64_t)R[o].n;
-            if (fs) { s->counters[OR_C_FULL_SYNCS]++; queue_rfs(s, j, (int32_t)o); }
+            CTR_ADD(s, OR_C_MSG_CHANGES, (uint64_t)R[o].n);
+            if (fs) { CTR_ADD(s, OR_C_FULL_SYNCS, 1); queue_rfs(s, j, (int32_t)o); }
         }
     }
     /* R */
+#pragma omp parallel for schedule(dynamic, 16)
     for (uint32_t o = 0; o < n; o++) {
         if (t[o] < 0 || !reach(s, o, (uint32_t)t[o])) continue;
-        s->counters[OR_C_PINGS_OK]++;
+        CTR_ADD(s, OR_C_PINGS_OK, 1);
         or_bump(s, o, S[o].v, S[o].n);                                 /* ping_sender.go:52 */
         or_update(s, o, R[o].v, R[o].n, NULL, 0);                      /* node.go:488 */
     }
@@ -962,10 +1014,11 @@ void or_step(or_sim *s, const or_event *ev, size_t nev) {
     uint32_t *C2 = (uint32_t *)calloc(n, sizeof(uint32_t));
     int64_t *I2 = (int64_t *)calloc(n, sizeof(int64_t));
     uint8_t *failed = (uint8_t *)calloc(n, 1);
+#pragma omp parallel for schedule(dynamic, 16)
     for (uint32_t o = 0; o < n; o++) {
         if (t[o] < 0 || reach(s, o, (uint32_t)t[o])) continue;
         failed[o] = 1;
-        s->counters[OR_C_PINGREQS]++;
+        CTR_ADD(s, OR_C_PINGREQS, 1);
         nh[o] = or_random_pingable(s, o, (int32_t)k, t[o], H + (size_t)o * k);
         S2[o].v = issue_changes(s, o, &S2[o].n);
         C2[o] = or_checksum(s, o);
@@ -987,21 +1040,23 @@ void or_step(or_sim *s, const or_event *ev, size_t nev) {
             int32_t h = H[(size_t)o * k + q];
             if (reach(s, o, (uint32_t)h)) hin[hcnt[h] + fill[h]++] = (int32_t)(o * k + (uint32_t)q);
         }
+#pragma omp parallel for schedule(dynamic, 16)
     for (uint32_t h = 0; h < n; h++) {
         for (int32_t q = hcnt[h]; q < hcnt[h + 1]; q++) {
             uint32_t o = (uint32_t)hin[q] / k;
-            s->counters[OR_C_HELPER_CALLS]++;
-            s->counters[OR_C_MSG_CHANGES] += (uint64_t)S2[o].n;
+            CTR_ADD(s, OR_C_HELPER_CALLS, 1);
+            CTR_ADD(s, OR_C_MSG_CHANGES, (uint64_t)S2[o].n);
             or_update(s, h, S2[o].v, S2[o].n, NULL, 0);                /* ping_request_handler.go:48 */
             /* helper's ping to t_o fails (reachability is an equivalence; ROUND_SEMANTICS §2) */
             int32_t fs;
             msg *r = &R2[hin[q]];
             r->v = issue_as_receiver(s, h, (int32_t)o, I2[o], C2[o], &r->n, &fs); /* 66-69 */
-            s->counters[OR_C_MSG_CHANGES] += (uint64_t)r->n;
-            if (fs) s->counters[OR_C_FULL_SYNCS_PINGREQ]++;
+            CTR_ADD(s, OR_C_MSG_CHANGES, (uint64_t)r->n);
+            if (fs) CTR_ADD(s, OR_C_FULL_SYNCS_PINGREQ, 1);
         }
     }
     /* Q3 */
+#pragma omp parallel for schedule(dynamic, 16)
     for (uint32_t o = 0; o < n; o++) {
         if (!failed[o]) continue;
         uint32_t errs = 0;
@@ -1009,35 +1064,39 @@ void or_step(or_sim *s, const or_event *ev, size_t nev) {
             int32_t h = H[(size_t)o * k + q];
             if (!reach(s, o, (uint32_t)h)) {
                 errs++;
-                s->counters[OR_C_HELPER_ERRORS]++;
+                CTR_ADD(s, OR_C_HELPER_ERRORS, 1);
                 or_bump(s, o, S2[o].v, S2[o].n);                       /* ping_request_sender.go:105-106 */
             } else {
                 msg *r = &R2[(size_t)o * k + q];
                 or_update(s, o, r->v, r->n, NULL, 0);                  /* ping_request_sender.go:77-79 */
             }
         }
-        if (errs == k) { s->counters[OR_C_INCONCLUSIVE]++; continue; } /* node.go:497-504 */
-        s->counters[OR_C_SUSPECT_DECL]++;
+        if (errs == k) { CTR_ADD(s, OR_C_INCONCLUSIVE, 1); continue; } /* node.go:497-504 */
+        CTR_ADD(s, OR_C_SUSPECT_DECL, 1);
         or_make_change(s, o, (uint32_t)t[o], INC(s, o, t[o]), OR_SUSPECT);  /* node.go:506-509 */
     }
     /* F: reverse full syncs; sources snapshotted at phase start */
     msg *snap = (msg *)calloc(n, sizeof(msg));
+    uint8_t *need = (uint8_t *)calloc(n, 1);
     for (uint32_t j = 0; j < n; j++)
-        for (int32_t q = 0; q < s->o[j].njobs; q++) {
-            int32_t src = s->o[j].jobs[q];
-            if (!snap[src].v) snap[src].v = membership_as_changes(s, (uint32_t)src, &snap[src].n);
-        }
+        for (int32_t q = 0; q < s->o[j].njobs; q++) need[s->o[j].jobs[q]] = 1;
+#pragma omp parallel for schedule(dynamic, 16)
+    for (uint32_t src = 0; src < n; src++)
+        if (need[src]) snap[src].v = membership_as_changes(s, src, &snap[src].n);
+    free(need);
+#pragma omp parallel for schedule(dynamic, 16)
     for (uint32_t j = 0; j < n; j++) {
         for (int32_t q = 0; q < s->o[j].njobs; q++) {
             int32_t src = s->o[j].jobs[q];
-            s->counters[OR_C_RFS_DONE]++;
+            CTR_ADD(s, OR_C_RFS_DONE, 1);
             or_update(s, j, snap[src].v, snap[src].n, NULL, 0);        /* disseminator.go:300 */
         }
         s->o[j].njobs = 0;
     }
     /* C */
+#pragma omp parallel for schedule(dynamic, 16)
     for (uint32_t o = 0; o < n; o++) or_checksum(s, o);
-    s->counters[OR_C_ROUNDS]++;
+    CTR_ADD(s, OR_C_ROUNDS, 1);
     s->round++;
 
     for (uint32_t o = 0; o < n; o++) {
@@ -1046,6 +1105,43 @@ void or_step(or_sim *s, const or_event *ev, size_t nev) {
     for (size_t i = 0; i < (size_t)n * (k ? k : 1); i++) free(R2[i].v);
     free(S); free(C); free(I); free(cnt); free(inbox); free(fill); free(R);
     free(H); free(nh); free(S2); free(C2); free(I2); free(failed); free(R2); free(hcnt); free(hin); free(snap);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* applied-change stream of watched observers (MemberlistChangesAppliedEvent, events.go:56-61)  */
+/* ------------------------------------------------------------------------------------------ */
+void or_watch(or_sim *s, uint32_t o, int32_t on) {
+    obs *ob = &s->o[o];
+    if (on && !ob->watched) {
+        ob->wdirty = (uint8_t *)calloc(s->n, 1);
+        ob->wlast = (or_change *)calloc(s->n, sizeof(or_change));
+        ob->wcs_prev = or_checksum(s, o);
+    } else if (!on && ob->watched) {
+        free(ob->wdirty); free(ob->wlast);
+        ob->wdirty = NULL; ob->wlast = NULL;
+    }
+    ob->watched = on ? 1 : 0;
+}
+
+/* every member with an applied change since the last drain (its last applied change), in member order,
+ * the checksum at the last drain (OldChecksum), the current one (NewChecksum) and NumMembers */
+int32_t or_drain_applied(or_sim *s, uint32_t o, or_change *out, int32_t cap, uint32_t *old_cs, uint32_t *new_cs,
+                         int32_t *num_members) {
+    obs *ob = &s->o[o];
+    if (!ob->watched) return -1;
+    int32_t k = 0;
+    for (uint32_t m = 0; m < s->n; m++) {
+        if (!ob->wdirty[m]) continue;
+        ob->wdirty[m] = 0;
+        if (k < cap) out[k] = ob->wlast[m];
+        k++;
+    }
+    const uint32_t cs = or_checksum(s, o);
+    if (old_cs) *old_cs = ob->wcs_prev;
+    if (new_cs) *new_cs = cs;
+    if (num_members) *num_members = ob->nmem;
+    ob->wcs_prev = cs;
+    return k;
 }
 
 /* ------------------------------------------------------------------------------------------ */

@@ -49,6 +49,8 @@ typedef struct or_config {
     uint64_t seed;                    /* Philox key */
     const char *addresses;            /* NULL: synthetic 10.%03u.%03u.%03u:7000; else n strings */
     uint32_t addr_stride;             /* bytes per address slot when addresses != NULL */
+    uint32_t reference_cost;          /* 1: checksum + pingable rescan at every applying Update (the
+                                         reference's cost model, CPU baseline); results unchanged */
 } or_config;
 
 enum {
@@ -104,6 +106,11 @@ int32_t or_last_targets(const or_sim *s, int32_t *out);  /* phase-S targets of t
 int32_t or_live(const or_sim *s, uint32_t o);
 /* canonical digests (docs/ROUND_SEMANTICS.md; inc mapped to e = (inc - t0)/period) */
 void or_digest(or_sim *s, uint64_t *rows, uint64_t *dis, uint64_t *tim);
+
+/* --- applied-change stream (MemberlistChangesAppliedEvent, swim/events.go:56-61) --- */
+void or_watch(or_sim *s, uint32_t o, int32_t on);
+int32_t or_drain_applied(or_sim *s, uint32_t o, or_change *out, int32_t cap, uint32_t *old_cs, uint32_t *new_cs,
+                         int32_t *num_members);
 
 /* --- unit-level primitives (for the reference KATs) --- */
 int32_t or_non_local_override(int64_t cur_inc, int32_t cur_st, int64_t ch_inc, int32_t ch_st);

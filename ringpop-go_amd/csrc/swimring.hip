@@ -158,19 +158,25 @@ __global__ void k_ring_lookup(const uint8_t *bytes, const uint64_t *off, uint32_
     out[k] = (int32_t)(uint32_t)ring[p];
 }
 
-// LookupN: distinct owners walking up from the key's hash, then from 0 (rbtree.go:262-286)
+// LookupN: distinct owners walking up from the key's hash, then from 0 (rbtree.go:262-286). One workgroup:
+// its threads clear a seen-bitmap over server ids, then one lane walks the ring (O(P) at worst, one bit test
+// per point; the order of first occurrences decides which n owners are taken)
 __global__ void k_ring_lookup_n(const uint8_t *key, uint32_t len, const unsigned long long *ring, uint32_t P, uint32_t n,
-                                int32_t *out, uint32_t *nout) {
-    if (threadIdx.x || blockIdx.x) return;
+                                int32_t *out, uint32_t *nout, uint32_t *seen, uint32_t seen_words) {
+    if (blockIdx.x) return;
+    for (uint32_t i = threadIdx.x; i < seen_words; i += blockDim.x) seen[i] = 0;
+    __syncthreads();
+    if (threadIdx.x) return;
     uint32_t got = 0;
     const uint32_t h = fp32_dev(key, len);
     const uint32_t start = lower_bound_u64(ring, P, (unsigned long long)h << 32);
     for (int pass = 0; pass < 2 && got < n; pass++) {
         for (uint32_t p = pass ? 0 : start; p < P && got < n; p++) {
-            const int32_t o = (int32_t)(uint32_t)ring[p];
-            bool seen = false;
-            for (uint32_t q = 0; q < got && !seen; q++) seen = out[q] == o;
-            if (!seen) out[got++] = o;
+            const uint32_t o = (uint32_t)ring[p];
+            const uint32_t bit = 1u << (o & 31);
+            if (seen[o >> 5] & bit) continue;
+            seen[o >> 5] |= bit;
+            out[got++] = (int32_t)o;
         }
     }
     *nout = got;
@@ -198,6 +204,8 @@ struct swimring {
     std::vector<uint32_t> hnlen;
     // ring
     unsigned long long *ring = nullptr, *ring2 = nullptr;
+    uint32_t *seen = nullptr;                                     // LookupN's seen-bitmap over server ids
+    size_t seen_cap = 0;
     uint32_t P = 0;
     size_t ring_cap = 0;
     uint32_t checksum = 0;
@@ -390,7 +398,7 @@ int swimring_destroy(swimring_t *r) {
     if (!r) return SWIMSIM_OK;
     if (r->s) hipStreamSynchronize(r->s);
     void *bufs[] = {r->dnames, r->dnoff, r->dnlen, r->ring, r->ring2, r->k0, r->k1, r->kept, r->v0, r->v1, r->nsel,
-                    r->flag, r->bid, r->cub, r->bytes, r->boff, r->iout, r->uout};
+                    r->flag, r->bid, r->cub, r->bytes, r->boff, r->iout, r->uout, r->seen};
     for (void *p : bufs)
         if (p) hipFree(p);
     if (r->e0) hipEventDestroy(r->e0);
@@ -402,31 +410,9 @@ int swimring_destroy(swimring_t *r) {
 
 const char *swimring_last_error(swimring_t *r) { return r ? r->err.c_str() : "null handle"; }
 
-int swimring_add_remove(swimring_t *r, const char *const *add, size_t nadd, const char *const *remove, size_t nremove,
-                        int32_t *changed) {
-    if (!r || (nadd && !add) || (nremove && !remove)) return SWIMSIM_EINVAL;
-    if (changed) *changed = 0;
-    std::vector<int32_t> A, D;
-    for (size_t i = 0; i < nadd; i++) {                          // addServerNoLock: skip servers in the set
-        int32_t id;
-        if (!add[i]) return SWIMSIM_EINVAL;
-        if (int rc = intern(r, add[i], &id)) return rc;
-        if (r->in_set[id]) continue;
-        r->in_set[id] = 1;
-        r->nset++;
-        A.push_back(id);
-    }
-    for (size_t i = 0; i < nremove; i++) {                       // removeServerNoLock: skip unknown ones
-        if (!remove[i]) return SWIMSIM_EINVAL;
-        auto it = r->ids.find(remove[i]);
-        if (it == r->ids.end() || !r->in_set[it->second]) continue;
-        r->in_set[it->second] = 0;
-        r->nset--;
-        D.push_back(it->second);
-    }
-    if (A.empty() && D.empty()) return SWIMSIM_OK;
-    if (changed) *changed = 1;
-    if (int rc = sync_names(r)) return rc;
+// the device half of AddRemoveServers: hash and insert the added servers' points, then drop the removed
+// servers' points. *adds_done tells a failing caller whether the adds reached the ring
+static int ring_apply(swimring *r, const std::vector<int32_t> &A, const std::vector<int32_t> &D, bool *adds_done) {
     RCHK(r, hipEventRecord(r->e0, r->s));
     size_t c;
     if (!A.empty()) {
@@ -456,6 +442,7 @@ int swimring_add_remove(swimring_t *r, const char *const *add, size_t nadd, cons
         std::swap(r->ring, r->ring2);
         r->P = P2;
     }
+    *adds_done = true;
     if (!D.empty() && r->P) {
         const uint32_t nd = (uint32_t)(D.size() * r->R);
         if (int rc = ensure_scratch(r, std::max<size_t>(r->P, nd))) return rc;   // before k1 is filled
@@ -477,6 +464,49 @@ int swimring_add_remove(swimring_t *r, const char *const *add, size_t nadd, cons
     float ms = 0;
     hipEventElapsedTime(&ms, r->e0, r->e1);
     r->t_add = ms;
+    return 0;
+}
+
+int swimring_add_remove(swimring_t *r, const char *const *add, size_t nadd, const char *const *remove, size_t nremove,
+                        int32_t *changed) {
+    if (!r || (nadd && !add) || (nremove && !remove)) return SWIMSIM_EINVAL;
+    if (changed) *changed = 0;
+    // every name is checked and interned before the server set changes, so a bad name leaves the ring as
+    // it was; a HIP failure further down rolls the set back to the servers the device ring holds
+    for (size_t i = 0; i < nadd; i++)
+        if (!add[i] || strlen(add[i]) > RING_NAME_MAX) return r->fail(SWIMSIM_EINVAL, "bad server name in the add list");
+    for (size_t i = 0; i < nremove; i++)
+        if (!remove[i]) return SWIMSIM_EINVAL;
+    std::vector<int32_t> aid(nadd);
+    for (size_t i = 0; i < nadd; i++)
+        if (int rc = intern(r, add[i], &aid[i])) return rc;
+    std::vector<int32_t> A, D;
+    for (size_t i = 0; i < nadd; i++) {                          // addServerNoLock: skip servers in the set
+        const int32_t id = aid[i];
+        if (r->in_set[id]) continue;
+        r->in_set[id] = 1;
+        r->nset++;
+        A.push_back(id);
+    }
+    for (size_t i = 0; i < nremove; i++) {                       // removeServerNoLock: skip unknown ones
+        auto it = r->ids.find(remove[i]);
+        if (it == r->ids.end() || !r->in_set[it->second]) continue;
+        r->in_set[it->second] = 0;
+        r->nset--;
+        D.push_back(it->second);
+    }
+    if (A.empty() && D.empty()) return SWIMSIM_OK;
+    if (changed) *changed = 1;
+    auto undo = [&](bool adds, int rc) {
+        if (adds)
+            for (int32_t id : A) { r->in_set[id] = 0; r->nset--; }
+        for (int32_t id : D) { r->in_set[id] = 1; r->nset++; }
+        if (changed) *changed = 0;
+        return rc;
+    };
+    if (int rc = sync_names(r)) return undo(true, rc);
+    bool adds_done = false;
+    if (int rc = ring_apply(r, A, D, &adds_done)) return undo(!adds_done, rc);
     return compute_checksum(r);
 }
 
@@ -530,8 +560,16 @@ int swimring_lookup_n(swimring_t *r, const uint8_t *key, size_t len, uint32_t n,
     if (int rc = grow(r, &r->iout, &c, n)) return rc;
     if (int rc = grow(r, &r->uout, &c2, n)) return rc;
     r->out_cap = std::min(c, c2);
-    hipLaunchKernelGGL(k_ring_lookup_n, dim3(1), dim3(64), 0, r->s, r->bytes, (uint32_t)len, r->ring, r->P, n, r->iout,
-                       r->uout);
+    const size_t words = (r->names.size() + 31) / 32;
+    if (words > r->seen_cap) {
+        if (r->seen) hipFree(r->seen);
+        r->seen = nullptr;
+        r->seen_cap = 0;
+        RCHK(r, hipMalloc(&r->seen, std::max<size_t>(words, 64) * 4));
+        r->seen_cap = std::max<size_t>(words, 64);
+    }
+    hipLaunchKernelGGL(k_ring_lookup_n, dim3(1), dim3(256), 0, r->s, r->bytes, (uint32_t)len, r->ring, r->P, n, r->iout,
+                       r->uout, r->seen, (uint32_t)words);
     uint32_t got = 0;
     RCHK(r, hipMemcpyAsync(&got, r->uout, 4, hipMemcpyDeviceToHost, r->s));
     RCHK(r, hipStreamSynchronize(r->s));

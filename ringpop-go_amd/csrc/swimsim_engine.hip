@@ -1381,7 +1381,7 @@ int swimsim_destroy(swimsim_t *h) {
 
 static int init_rows(swimsim_t *h, int mode) {
     hipLaunchKernelGGL(k_init_rows, dim3(blocks_for_waves(h->NL)), dim3(SWIM_WAVE_BLOCK), 0, h->s, h->d, mode, 0u);
-    checksum_dirty(h, 0);
+    if (int rc = checksum_dirty(h, 0)) return rc;
     return check_err(h);
 }
 
@@ -1487,7 +1487,7 @@ uint32_t swimsim_round(swimsim_t *h) { return h ? h->round : 0; }
 
 int swimsim_checksums(swimsim_t *h, uint32_t *out) {
     if (!h || !out) return SWIMSIM_EINVAL;
-    checksum_dirty(h, 0);
+    if (int rc = checksum_dirty(h, 0)) return rc;
     HIPCHK(h, hipMemcpyAsync(out, h->d.cs, h->NL * 4, hipMemcpyDeviceToHost, h->s));
     return check_err(h);
 }

@@ -390,8 +390,13 @@ def issue_as_sender(cluster, o: int, timestamp: int = GO_ZERO_TIME_UNIX) -> List
     st, inc = cluster.row(o)
     out = []
     for m, (_p, s, sinc) in sorted(cluster.changes(o).items()):
+        # an entry can outlive its member's eviction (Evict leaves the disseminator alone,
+        # memberlist.go:271-279): the change then reads (tombstone, inc), as issueChanges builds it from
+        # the last applied change
+        code = int(st[m])
+        name = STATUS_NAMES[TOMBSTONE if code == UNKNOWN else code]
         out.append(Change(address_of(s) if s >= 0 else "", sinc, address_of(m), int(inc[m]),
-                          STATUS_NAMES[int(st[m])], False, timestamp).validate_outgoing())
+                          name, False, timestamp).validate_outgoing())
     return out
 
 
@@ -444,14 +449,21 @@ def join_response(cluster, o: int, app: str, timestamp: int = GO_ZERO_TIME_UNIX)
 
 def seed_from_membership(cluster, o: int, changes: List[Change]) -> int:
     """Write a received membership (a joinResponse's, or a real node's) into observer o's row as its
-    bootstrap state: each change taken wholesale, as memberlist.Update does for members it has not seen
-    (memberlist.go:325-334), tombstones included (validateIncoming); members absent from the list are
-    unknown. One swimsim_set_row call. Returns the number of members written."""
+    bootstrap state: the list applied in order by memberlist.Update's rules to an empty memberlist
+    (memberlist.go:310-390). An unseen member is taken wholesale (325-334) unless the change is a
+    tombstone, which Apply refuses to create (424-426); a later duplicate applies only if it overrides
+    (nonLocalOverride, member.go:79-93). Members absent from the list stay unknown. No side effects (no
+    dissemination entries or timers): one swimsim_set_row call. Returns the number of members written."""
     cols = changes_to_arrays(changes, cluster.n)
     status = np.full(cluster.n, UNKNOWN, np.uint8)
     inc = np.zeros(cluster.n, np.int64)
-    status[cols["member"]] = cols["status"]         # duplicates: the later change wins, as in Update
-    inc[cols["member"]] = cols["incarnation"]
+    for m, st, ic in zip(cols["member"].tolist(), cols["status"].tolist(), cols["incarnation"].tolist()):
+        if status[m] == UNKNOWN:
+            if st == TOMBSTONE:
+                continue
+        elif not (ic > inc[m] or (ic == inc[m] and st > status[m])):
+            continue
+        status[m], inc[m] = st, ic
     cluster.set_row(o, status, inc)
     return int(np.count_nonzero(status != UNKNOWN))
 

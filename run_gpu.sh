@@ -1,14 +1,19 @@
 #!/bin/bash
 # GPU session script: each step under its own time limit; stop at the first failing step.
-# usage: run_gpu.sh [tests|bench|prof|pmc|all ...]   (several modes run in the order given)
+# usage: run_gpu.sh [tests|smoke|bench|prof|pmc|all ...]   (several modes run in the order given)
+# BENCH_ARGS defaults to the driver's round-end command (--steps 20 --warmup 5); prof and pmc profile
+# exactly that command, so profiles/ figures and the bench line describe the same workload.
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+BENCH_ARGS=${BENCH_ARGS:---steps 20 --warmup 5}
+PROF_ARGS="$BENCH_ARGS --no-cpu-baseline --no-ring"
+WL=${WL:-65536:20:5:1}
 [ $# -eq 0 ] && set -- all
 for mode in "$@"; do
   case $mode in
   tests|all)
-    timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+    timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} \
       > gpurun_out/gpu_tests.log 2>&1
     rc=$?; echo "pytest rc=$rc" >> gpurun_out/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
     ;;&
@@ -22,8 +27,20 @@ for mode in "$@"; do
     ;;&
   prof|all)
     timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv \
-      -- python3 bench.py --no-cpu-baseline > gpurun_out/prof.log 2>&1
+      -- python3 bench.py $PROF_ARGS > gpurun_out/prof.log 2>&1
     rc=$?; echo "rocprof rc=$rc" >> gpurun_out/prof.log; [ $rc -eq 0 ] || exit $rc
+    ;;&
+  pmc|all)
+    timeout -k 10 -s KILL 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run \
+      --output-format csv -- python3 bench.py $PROF_ARGS > gpurun_out/pmc_fetch.log 2>&1
+    rc=$?; echo "pmc fetch rc=$rc" >> gpurun_out/pmc_fetch.log; [ $rc -eq 0 ] || exit $rc
+    timeout -k 10 -s KILL 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run \
+      --output-format csv -- python3 bench.py $PROF_ARGS > gpurun_out/pmc_write.log 2>&1
+    rc=$?; echo "pmc write rc=$rc" >> gpurun_out/pmc_write.log; [ $rc -eq 0 ] || exit $rc
+    timeout -k 10 -s KILL 400 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVES GRBM_GUI_ACTIVE --kernel-trace \
+      -d gpurun_out/pmc_valu -o run --output-format csv -- python3 bench.py $PROF_ARGS > gpurun_out/pmc_valu.log 2>&1
+    rc=$?; echo "pmc valu rc=$rc" >> gpurun_out/pmc_valu.log; [ $rc -eq 0 ] || exit $rc
+    python3 tools/pmc_summary.py --workload $WL gpurun_out/pmc_summary.json gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc_valu
     ;;
   bench2)
     timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
@@ -32,20 +49,8 @@ for mode in "$@"; do
     rc=$?; echo "bench2 rc=$rc" >> gpurun_out/bench2.err; [ $rc -eq 0 ] || exit $rc
     ;;
   csbench)
-    timeout -k 10 300 python -u tools_cs_bench.py 65536 64,1024,16384,65536 2 ${CS_MODES:-0,1,2} > gpurun_out/csbench.json 2> gpurun_out/csbench.err
+    timeout -k 10 300 python -u tools/cs_bench.py 65536 64,1024,16384,65536 2 ${CS_MODES:-0,1,2} > gpurun_out/csbench.json 2> gpurun_out/csbench.err
     rc=$?; echo "csbench rc=$rc" >> gpurun_out/csbench.err; [ $rc -eq 0 ] || exit $rc
-    ;;
-  pmc)
-    timeout -k 10 -s KILL 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run \
-      --output-format csv -- python3 bench.py --no-cpu-baseline > gpurun_out/pmc_fetch.log 2>&1
-    rc=$?; echo "pmc fetch rc=$rc" >> gpurun_out/pmc_fetch.log; [ $rc -eq 0 ] || exit $rc
-    timeout -k 10 -s KILL 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run \
-      --output-format csv -- python3 bench.py --no-cpu-baseline > gpurun_out/pmc_write.log 2>&1
-    rc=$?; echo "pmc write rc=$rc" >> gpurun_out/pmc_write.log; [ $rc -eq 0 ] || exit $rc
-    timeout -k 10 -s KILL 400 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVES GRBM_GUI_ACTIVE --kernel-trace \
-      -d gpurun_out/pmc_valu -o run --output-format csv -- python3 bench.py --no-cpu-baseline > gpurun_out/pmc_valu.log 2>&1
-    rc=$?; echo "pmc valu rc=$rc" >> gpurun_out/pmc_valu.log; [ $rc -eq 0 ] || exit $rc
-    python3 tools/pmc_summary.py gpurun_out/pmc_summary.json gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc_valu
     ;;
   esac
 done

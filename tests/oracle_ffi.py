@@ -13,6 +13,8 @@ import numpy as np
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(REPO, "oracle")
 LIB_PATH = os.path.join(ORACLE_DIR, "build", "libswim_oracle.so")
+# OpenMP build of the same source: bench.py's cpu_baseline leg only (ORACLE_LIB selects it)
+OMP_LIB_PATH = os.path.join(ORACLE_DIR, "build", "libswim_oracle_omp.so")
 
 ALIVE, SUSPECT, FAULTY, LEAVE, TOMBSTONE, UNKNOWN = 0, 1, 2, 3, 4, 7
 SOURCE_NONE = -1
@@ -36,7 +38,7 @@ class OrConfig(C.Structure):
                 ("suspect_ms", C.c_int64), ("faulty_ms", C.c_int64), ("tombstone_ms", C.c_int64),
                 ("ping_request_size", C.c_uint32), ("max_rfs_jobs", C.c_uint32), ("p_factor", C.c_uint32),
                 ("faithful_checksum", C.c_uint32), ("seed", C.c_uint64), ("addresses", C.c_char_p),
-                ("addr_stride", C.c_uint32)]
+                ("addr_stride", C.c_uint32), ("reference_cost", C.c_uint32)]
 
 
 class OrEvent(C.Structure):
@@ -54,9 +56,10 @@ def build() -> str:
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
+        path = os.environ.get("ORACLE_LIB", LIB_PATH)
+        if not os.path.exists(path):
             build()
-        L = C.CDLL(LIB_PATH)
+        L = C.CDLL(path)
         P = C.c_void_p
         u32, i32, i64, u64 = C.c_uint32, C.c_int32, C.c_int64, C.c_uint64
         sig = {
@@ -88,6 +91,9 @@ def lib():
             "or_last_targets": (i32, [P, P]),
             "or_live": (i32, [P, u32]),
             "or_digest": (None, [P, C.POINTER(u64), C.POINTER(u64), C.POINTER(u64)]),
+            "or_watch": (None, [P, u32, i32]),
+            "or_drain_applied": (i32, [P, u32, C.POINTER(OrChange), i32, C.POINTER(u32), C.POINTER(u32),
+                                       C.POINTER(i32)]),
             "or_non_local_override": (i32, [i64, i32, i64, i32]),
             "or_local_override": (i32, [i32, i64, i64, i32]),
             "or_update": (i32, [P, u32, C.POINTER(OrChange), i32, C.POINTER(OrChange), i32]),
@@ -153,12 +159,12 @@ class OracleSim:
 
     def __init__(self, n, *, t0_ms=T0_MS, period_ms=PERIOD_MS, suspect_ms=5000, faulty_ms=24 * 3600 * 1000,
                  tombstone_ms=60_000, ping_request_size=3, max_rfs_jobs=5, p_factor=15, seed=1,
-                 faithful_checksum=False, addresses=None, init="converged"):
+                 faithful_checksum=False, reference_cost=False, addresses=None, init="converged"):
         L = lib()
         self.n = n
         self.t0_ms, self.period_ms = t0_ms, period_ms
         cfg = OrConfig(n, t0_ms, period_ms, suspect_ms, faulty_ms, tombstone_ms, ping_request_size, max_rfs_jobs,
-                       p_factor, int(bool(faithful_checksum)), seed, None, 0)
+                       p_factor, int(bool(faithful_checksum)), seed, None, 0, int(bool(reference_cost)))
         self._addr_buf = None
         if addresses is not None:
             stride = max(len(a) for a in addresses) + 1
@@ -301,6 +307,20 @@ class OracleSim:
         buf = C.create_string_buffer(n + 1)
         lib().or_checksum_string(self.h, o, buf, n)
         return buf.raw[:n]
+
+    # --- applied-change stream (MemberlistChangesAppliedEvent, swim/events.go:56-61) ---
+    def watch(self, o, on=True):
+        lib().or_watch(self.h, o, int(on))
+
+    def drain_applied(self, o):
+        """(changes, old checksum, new checksum, NumMembers) since the last drain of watched observer o;
+        changes = [(member, status, inc, source, source_inc)] in member order"""
+        out = (OrChange * self.n)()
+        a, b, c = C.c_uint32(), C.c_uint32(), C.c_int32()
+        k = lib().or_drain_applied(self.h, o, out, self.n, C.byref(a), C.byref(b), C.byref(c))
+        if k < 0:
+            raise ValueError(f"observer {o} is not watched")
+        return _unpack(out, k), a.value, b.value, c.value
 
     # --- unit-level primitives (reference KATs) ---
     def update(self, j, changes):

@@ -1,0 +1,28 @@
+"""bench.py's launch contract on CPU (no GPU call): `--gpus N` without a launcher starts N ranks itself
+through a child torch.distributed.run, and the workload accounting counts live members only."""
+import json
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_gpus2_spawns_two_ranks():
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--launch-check"],
+                         capture_output=True, text=True, timeout=300, env=env, cwd=REPO)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [json.loads(l) for l in out.stdout.splitlines() if l.startswith("{")]
+    assert sorted(l["rank"] for l in lines) == [0, 1]
+    assert all(l["world_size"] == 2 for l in lines)
+
+
+def test_live_member_rounds_counts_live_members_only():
+    sys.path.insert(0, REPO)
+    import bench
+    from swimsim import workloads as W
+
+    wl = W.config3(n=1000, rounds=30, kill_round=10)
+    # rounds 5-24: 5 rounds of 1000 live members, then 15 rounds of 990
+    assert bench.live_member_rounds(wl, 5, 24) == 5 * 1000 + 15 * 990

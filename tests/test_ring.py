@@ -265,3 +265,34 @@ def test_gpu_ring_from_engine_rows():
     o.add_remove_servers([], [addr(m) for m in np.nonzero(~want)[0]])
     _same(g, o)
     assert g.server_count() == int(want.sum()) < wl.n
+
+
+@pytest.mark.gpu
+def test_gpu_lookup_n_near_server_count_on_a_large_ring():
+    """LookupN with n = server count - 1 walks nearly the whole ring: one bit test per point (a seen-bitmap over
+    server ids), not a scan of the owners found so far"""
+    import time
+    servers = gen_addresses(5, 1, 8192)
+    g, o = _gpu_ring(100), OracleRing(100)
+    assert g.add_remove_servers(servers) == o.add_remove_servers(servers)
+    t0 = time.perf_counter()
+    got = g.lookup_n("a random key", len(servers) - 1)
+    dt = time.perf_counter() - t0
+    assert len(got) == len(set(got)) == len(servers) - 1
+    assert set(got) == set(o.lookup_n("a random key", len(servers) - 1))
+    assert dt < 5.0
+
+
+@pytest.mark.gpu
+def test_gpu_add_remove_bad_name_leaves_the_ring_unchanged():
+    """a batch with an over-long name fails before the server set changes (no half-applied batch)"""
+    g, o = _gpu_ring(10), OracleRing(10)
+    g.add_remove_servers(["server1", "server2"])
+    o.add_remove_servers(["server1", "server2"])
+    cs = g.checksum()
+    with pytest.raises(Exception):
+        g.add_remove_servers(["server3", "x" * 300, "server4"])
+    assert g.checksum() == cs and g.server_count() == 2
+    assert not g.has_server("server3")
+    assert g.add_remove_servers(["server3"]) and o.add_remove_servers(["server3"])
+    _same(g, o)

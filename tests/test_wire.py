@@ -17,6 +17,7 @@ import swimsim
 from swimsim import wire as W
 from swimsim import workloads as WL
 from oracle_ffi import OracleSim
+from swimsim import TOMBSTONE, UNKNOWN
 
 ZERO = W.GO_ZERO_TIME_UNIX
 
@@ -198,6 +199,45 @@ def test_seed_from_join_response_reproduces_checksum_on_oracle():
     assert W.seed_from_membership(OracleView(fresh), 3, W.JoinResponse.from_json(body).membership) == wl.n
     assert (fresh.row(3)[0] == ora.row(0)[0]).all() and (fresh.row(3)[1] == ora.row(0)[1]).all()
     assert fresh.checksum(3) == ora.checksum(0) == W.JoinResponse.from_json(body).checksum
+
+
+def test_seed_skips_tombstones_of_unseen_members():
+    """Apply refuses to create a member whose first state is tombstone (memberlist.go:424-426)"""
+    wl = WL.config1()
+    ora = _oracle_after(wl, 3)
+    inc9 = ora.member(0, 9)[1]
+    assert ora.make_change(0, 9, inc9, TOMBSTONE) == 1
+    jr = W.join_response(OracleView(ora), 0, "ringpop")
+    assert any(c.validate_incoming().status == "tombstone" for c in jr.membership)
+    fresh = OracleSim(wl.n, init="self")
+    assert W.seed_from_membership(OracleView(fresh), 3, jr.membership) == wl.n - 1
+    assert fresh.member(3, 9)[0] == UNKNOWN and fresh.num_members(3) == wl.n - 1
+    assert fresh.checksum(3) == ora.checksum(0)       # tombstones are not in the checksum string
+
+
+def test_ping_of_after_eviction_keeps_buffered_tombstone():
+    """An entry can outlive its member's eviction (Evict leaves the disseminator alone,
+    memberlist.go:271-279): the ping then carries it as faulty + tombstone flag (issueChanges builds it
+    from the last applied change; validateOutgoing, member.go:161-167)"""
+    n = 8
+    ora = OracleSim(n, suspect_ms=400, faulty_ms=400, tombstone_ms=400)
+    v = OracleView(ora)
+    ev = [(0, WL.EV_PARTITION, 0, 1)]
+    found = None
+    for r in range(40):
+        ora.step([e for e in ev if e[0] == r])
+        for o in range(1, n):
+            ents = ora.dis_entries(o)
+            if 0 in ents and ora.member(o, 0)[0] == UNKNOWN:
+                found = o
+                break
+        if found is not None:
+            break
+    assert found is not None, "no observer held a buffered change of an evicted member"
+    ping = W.ping_of(v, found)
+    c0 = next(c for c in ping.changes if W.index_of(c.address) == 0)
+    assert c0.status == "faulty" and c0.tombstone
+    assert W.Ping.from_json(ping.to_json()) == ping
 
 
 # ---- GPU: bodies from device state, byte for byte against the oracle's -------------------------------

@@ -4,9 +4,10 @@ first `rows` observer rows of a converged N-member cluster, mode 0 = full kernel
 and 5 leave garbage checksums), 6 = the 16-row narrow kernel. With a 5th argument "verify", rows are
 perturbed first (one suspect each) and the checksums of mode 6 are compared with mode 0's."""
 import json
+import os
 import sys
 
-sys.path.insert(0, "ringpop-go_amd")
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ringpop-go_amd"))
 import swimsim  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536

@@ -1,6 +1,7 @@
 """Per-kernel, per-launch PMC figures from rocprofv3 --pmc passes of bench.py (one directory per pass).
 
-usage: python tools/pmc_summary.py <out.json> <pass_dir> [<pass_dir> ...]
+usage: python tools/pmc_summary.py [--workload MEMBERS:STEPS:WARMUP:GPUS] <out.json> <pass_dir> [<pass_dir> ...]
+--workload records the bench.py command the passes profiled (bench.py uses the summary only for that workload).
 Every counter of every pass is averaged per launch of each kernel. FETCH_SIZE and WRITE_SIZE are in
 KiB (TCC_EA0_RDREQ/WRREQ-derived) and are reported as bytes. MI355X_MICROARCH.md §HBM: on gfx950
 FETCH_SIZE reports half the bytes of a wide coalesced 16-B/lane streaming read (doubled here as
@@ -22,10 +23,16 @@ def load(path, agg):
 
 
 def main():
+    argv = sys.argv[1:]
+    workload = None
+    if argv and argv[0] == "--workload":
+        m, st, w, g = (int(x) for x in argv[1].split(":"))
+        workload = {"members": m, "steps": st, "warmup": w, "gpus": g}
+        argv = argv[2:]
     agg = collections.defaultdict(lambda: collections.defaultdict(lambda: [set(), 0.0]))
-    for p in sys.argv[2:]:
+    for p in argv[1:]:
         load(p, agg)
-    out = {}
+    out = {"_workload": workload}
     for k in sorted(agg):
         e = {}
         for c, (ids, v) in agg[k].items():
@@ -39,7 +46,7 @@ def main():
             else:
                 e[c.lower() + "_per_launch"] = v / n
         out[k] = e
-    json.dump(out, open(sys.argv[1], "w"), indent=1)
+    json.dump(out, open(argv[0], "w"), indent=1)
 
 
 if __name__ == "__main__":

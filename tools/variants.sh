@@ -10,7 +10,7 @@ for v in variants/*.so; do
     SWIMSIM_LIB=$PWD/$v timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/var_$n.json 2> gpurun_out/var_$n.err || exit $?
     echo "$n $(python3 -c "import json; d=json.load(open('gpurun_out/var_$n.json')); print(d['value'], d['kernel_ms'])")"
   else
-    SWIMSIM_LIB=$PWD/$v timeout -k 10 200 python -u tools_cs_bench.py 65536 64,65536 2 ${CS_MODES:-0,2} \
+    SWIMSIM_LIB=$PWD/$v timeout -k 10 200 python -u tools/cs_bench.py 65536 64,65536 2 ${CS_MODES:-0,2} \
       > gpurun_out/var_$n.json 2> gpurun_out/var_$n.err || exit $?
     echo "$n $(cat gpurun_out/var_$n.json)"
   fi
