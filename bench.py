@@ -266,7 +266,7 @@ def main():
         dominant = max(kt.items(), key=lambda kv: kv[1]["avg_ms"] * kv[1]["launches"])[0]
         dom = family_roofline(dominant)
         in_window = timed_first <= KILL_ROUND <= timed_last
-        faulty_from = KILL_ROUND + 26       # suspect declared at KILL_ROUND, timer fires 25 rounds later at the earliest
+        faulty_from = KILL_ROUND + 25       # first suspicions at KILL_ROUND; their timers fire 25 rounds later
         line = {
             "metric": "simulated member-rounds/sec at 64k members" if n == 65536 else f"simulated member-rounds/sec at {n} members",
             "value": round(value, 1),

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SWIMSIM_ABI_VERSION 2
+#define SWIMSIM_ABI_VERSION 3
 
 enum {
     SWIMSIM_OK = 0,
@@ -147,6 +147,34 @@ int swimsim_counters(swimsim_t *h, uint64_t *out);
 int swimsim_digest(swimsim_t *h, uint64_t *rows, uint64_t *dissemination, uint64_t *timers);
 /* converged (test_utils.go:188-198): no live node has changes and all live checksums equal */
 int swimsim_converged(swimsim_t *h, int32_t *out);
+
+/* ---- upward coupling: NodeInterface.RegisterListener (node.go:146) ----
+ * MemberlistChangesAppliedEvent{Changes, OldChecksum, NewChecksum, NumMembers} (swim/events.go:56-61) is
+ * emitted by memberlist.Update whenever it applied something (memberlist.go:366-384); Ringpop feeds its
+ * hash ring from it (ringpop.go:398-400,550-563). Watch an observer to record its applied changes (off by
+ * default: unwatched rows pay one predicated branch per applied change); a drain returns, in member order,
+ * the last applied change of every member since the previous drain (the per-Update events of the rounds in
+ * between, coalesced per member: the ring's final membership depends only on each member's last change),
+ * the checksum at the previous drain (OldChecksum), the current one (NewChecksum) and NumMembers. n = 0:
+ * nothing applied, no event. Evictions are not events (RemoveMember emits none, memberlist.go:141-162).
+ * At most 64 watched observers per handle. */
+int swimsim_watch(swimsim_t *h, uint32_t observer, int32_t on);
+int swimsim_applied_changes(swimsim_t *h, uint32_t observer, int32_t *member, int32_t *status, int64_t *inc_ms,
+                            int32_t *source, int64_t *source_inc_ms, size_t cap, size_t *n, uint32_t *old_checksum,
+                            uint32_t *new_checksum, int32_t *num_members);
+
+/* NodeInterface.ProtocolStats (node.go:137-147, stats.go:81-104). Each round is one ProtocolPeriod of every
+ * live node (gossip.go:178-188), so the Timing histogram is over rounds: the device wall time of each round
+ * (HIP events on the engine's stream), in ns. ProtocolRate = max(2 x median, MinProtocolPeriod)
+ * (AdjustProtocolRate, gossip.go:110-115). ServerRate = pings and ping-reqs handled per node per simulated
+ * second (ping_handler.go:37, ping_request_handler.go:45); ClientRate is never marked by the reference (0). */
+typedef struct swimsim_protocol_stats {
+    int64_t count;
+    double min_ns, max_ns, sum_ns, mean_ns, variance, stddev_ns, median_ns, p75_ns, p95_ns, p99_ns, p999_ns;
+    int64_t protocol_rate_ns;
+    double client_rate, server_rate, total_rate;
+} swimsim_protocol_stats_t;
+int swimsim_protocol_stats(swimsim_t *h, swimsim_protocol_stats_t *out);
 
 /* ---- measurement ---- */
 /* average device time (ms) of each kernel family since the last reset, for roofline reporting */

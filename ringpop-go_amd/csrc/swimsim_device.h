@@ -102,6 +102,10 @@ struct DS {
     uint32_t G, rank;         // observer-row shards of the cluster and this handle's shard
     const uint32_t *shard_lo; // [G+1] first observer of each shard (ascending, shard_lo[G] = N)
     uint32_t dig_thr[8];      // e at which t0 + e*period gains a digit (0xFFFFFFFF = never)
+    // applied-change stream of watched rows (MemberlistChangesAppliedEvent, swim/events.go:56-61)
+    uint32_t *wslot;          // [NL] watched row -> slot of wlog, SRC_NONE if unwatched; nullptr: no row watched
+    uint4 *wlog;              // [slots][NP] per member, the last change applied since the last drain:
+                              // {member word, source, source e, 1}; .w = 0: none
 };
 
 __host__ __device__ inline bool is_pingable(uint32_t st) { return st <= ST_SUSPECT; }

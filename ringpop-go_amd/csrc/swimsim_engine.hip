@@ -11,6 +11,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cmath>
 #include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
@@ -28,6 +29,7 @@ using namespace swimdev;
 namespace {
 
 const char *kStatus[4] = {"alive", "suspect", "faulty", "leave"};
+constexpr uint32_t kWatchCap = 64;       // watched rows per handle (1 MB of log per row at N = 65,536)
 
 struct Timed {
     int fam;
@@ -293,6 +295,16 @@ struct swimsim {
     double fam_ms[F_NFAM] = {0};
     uint64_t fam_n[F_NFAM] = {0};
     uint64_t fam_bytes_base[C_NALL] = {0};
+    // ProtocolStats (swim/stats.go:81-104): device wall time of every round, from consecutive round-start
+    // events on the main stream (the last round ends at the step's closing event)
+    std::vector<hipEvent_t> round_ev;
+    std::vector<float> round_ms;
+    // applied-change stream of watched rows (swimsim_watch / swimsim_applied_changes)
+    std::vector<uint32_t> wslot_h;                // [NL] slot or SRC_NONE
+    std::vector<uint8_t> wused;                   // [kWatchCap]
+    std::vector<uint32_t> wcs;                    // checksum at the last drain (OldChecksum), per slot
+    uint4 *wout = nullptr;
+    uint32_t *winfo = nullptr;
     std::string err;
 
     int fail(int code, const char *fmt, ...) {
@@ -923,6 +935,11 @@ int do_heal(swimsim *h, uint32_t o, std::vector<int32_t> *ret) {
 int step_one(swimsim *h, const swimsim_event *ev, size_t nev) {
     const uint32_t r = h->round;
     const bool sharded = h->G > 1;
+    {
+        hipEvent_t e = take_event(h);
+        HIPCHK(h, hipEventRecord(e, h->s));
+        h->round_ev.push_back(e);
+    }
     HIPCHK(h, hipMemsetAsync(h->d.pool_cur, 0, 8, h->s));
     // ---- E: events (the event list is the same on every shard; row events act on owned rows) ----
     std::vector<uint4> batch;
@@ -1365,6 +1382,7 @@ int swimsim_destroy(swimsim_t *h) {
     if (h->side) hipStreamSynchronize(h->side);
     if (h->s) hipStreamSynchronize(h->s);
     for (auto &t : h->pending) { hipEventDestroy(t.a); hipEventDestroy(t.b); }
+    for (auto e : h->round_ev) hipEventDestroy(e);
     for (auto e : h->evpool) hipEventDestroy(e);
     for (void *p : h->allocs) hipFree(p);
     if (h->sbuf) hipFree(h->sbuf);
@@ -1465,7 +1483,19 @@ int swimsim_step(swimsim_t *h, uint32_t nrounds, const swimsim_event *events, si
         if (int rc = step_one(h, events, nevents)) return rc;
     }
     if (int rc = sync_side(h)) return rc;    // a step call returns with every checksum current
+    if (!h->round_ev.empty()) {
+        hipEvent_t e = take_event(h);
+        HIPCHK(h, hipEventRecord(e, h->s));
+        h->round_ev.push_back(e);
+    }
     if (int rc = check_err(h)) return rc;
+    for (size_t i = 0; i + 1 < h->round_ev.size(); i++) {
+        float ms = 0;
+        hipEventElapsedTime(&ms, h->round_ev[i], h->round_ev[i + 1]);
+        if (h->round_ms.size() < (1u << 20)) h->round_ms.push_back(ms);
+    }
+    for (hipEvent_t e : h->round_ev) h->evpool.push_back(e);
+    h->round_ev.clear();
     drain_timing(h);
     return SWIMSIM_OK;
 }
@@ -1695,6 +1725,129 @@ int swimsim_debug_cs_stream(swimsim_t *h, uint32_t ol, uint32_t *out, size_t cap
     HIPCHK(h, hipStreamSynchronize(h->s));
     hipFree(dev);
     return check_err(h);
+}
+
+// ---- applied-change stream: MemberlistChangesAppliedEvent (swim/events.go:56-61) ----
+int swimsim_watch(swimsim_t *h, uint32_t o, int32_t on) {
+    if (!h || !own(h, o)) return SWIMSIM_EINVAL;
+    const uint32_t ol = o - h->lo;
+    if (!h->d.wslot) {
+        if (!on) return SWIMSIM_OK;
+        int rc = 0;
+        if ((rc = dalloc(h, &h->d.wslot, h->NL, "watch slots")) ||
+            (rc = dalloc(h, &h->d.wlog, (size_t)kWatchCap * h->NP, "applied-change log")) ||
+            (rc = dalloc(h, &h->wout, h->NP, "applied-change drain")) || (rc = dalloc(h, &h->winfo, 2, "drain info"))) {
+            h->d.wslot = nullptr;
+            h->d.wlog = nullptr;
+            return rc;
+        }
+        HIPCHK(h, hipMemsetAsync(h->d.wslot, 0xFF, (size_t)h->NL * 4, h->s));
+        h->wslot_h.assign(h->NL, SRC_NONE);
+        h->wused.assign(kWatchCap, 0);
+        h->wcs.assign(kWatchCap, 0);
+    }
+    uint32_t slot = h->wslot_h[ol];
+    if (on && slot == SRC_NONE) {
+        for (slot = 0; slot < kWatchCap && h->wused[slot]; slot++) {}
+        if (slot == kWatchCap) return h->fail(SWIMSIM_ECAPACITY, "at most %u watched observers per handle", kWatchCap);
+        if (int rc = checksum_dirty(h, 0)) return rc;
+        HIPCHK(h, hipMemsetAsync(h->d.wlog + (size_t)slot * h->NP, 0, (size_t)h->NP * 16, h->s));
+        HIPCHK(h, hipMemcpyAsync(h->d.wslot + ol, &slot, 4, hipMemcpyHostToDevice, h->s));
+        HIPCHK(h, hipMemcpyAsync(&h->wcs[slot], h->d.cs + ol, 4, hipMemcpyDeviceToHost, h->s));
+        HIPCHK(h, hipStreamSynchronize(h->s));
+        h->wused[slot] = 1;
+        h->wslot_h[ol] = slot;
+    } else if (!on && slot != SRC_NONE) {
+        const uint32_t none = SRC_NONE;
+        HIPCHK(h, hipMemcpyAsync(h->d.wslot + ol, &none, 4, hipMemcpyHostToDevice, h->s));
+        HIPCHK(h, hipStreamSynchronize(h->s));
+        h->wused[slot] = 0;
+        h->wslot_h[ol] = SRC_NONE;
+    }
+    return SWIMSIM_OK;
+}
+
+int swimsim_applied_changes(swimsim_t *h, uint32_t o, int32_t *member, int32_t *status, int64_t *inc_ms, int32_t *source,
+                            int64_t *source_inc_ms, size_t cap, size_t *n, uint32_t *old_checksum,
+                            uint32_t *new_checksum, int32_t *num_members) {
+    if (!h || !own(h, o)) return SWIMSIM_EINVAL;
+    const uint32_t ol = o - h->lo;
+    if (!h->d.wslot || h->wslot_h[ol] == SRC_NONE) return h->fail(SWIMSIM_EINVAL, "observer %u is not watched", o);
+    const uint32_t slot = h->wslot_h[ol];
+    if (int rc = checksum_dirty(h, 0)) return rc;
+    HIPCHK(h, hipMemsetAsync(h->winfo, 0, 8, h->s));
+    hipLaunchKernelGGL(k_drain_applied, dim3(1), dim3(1024), 0, h->s, h->d, ol, slot, h->wout, h->winfo);
+    uint32_t info[2] = {0, 0}, cs = 0;
+    HIPCHK(h, hipMemcpyAsync(info, h->winfo, 8, hipMemcpyDeviceToHost, h->s));
+    HIPCHK(h, hipMemcpyAsync(&cs, h->d.cs + ol, 4, hipMemcpyDeviceToHost, h->s));
+    HIPCHK(h, hipStreamSynchronize(h->s));
+    std::vector<uint4> rec(info[0]);
+    if (info[0]) {
+        HIPCHK(h, hipMemcpyAsync(rec.data(), h->wout, (size_t)info[0] * 16, hipMemcpyDeviceToHost, h->s));
+        HIPCHK(h, hipStreamSynchronize(h->s));
+    }
+    for (size_t i = 0; i < rec.size() && i < cap; i++) {
+        const uint4 v = rec[i];
+        if (member) member[i] = (int32_t)v.x;
+        if (status) status[i] = (int32_t)(v.y & 7u);
+        if (inc_ms) inc_ms[i] = from_e(h, v.y >> 3);
+        if (source) source[i] = v.z == SRC_NONE ? -1 : (int32_t)v.z;
+        if (source_inc_ms) source_inc_ms[i] = v.z == SRC_NONE ? 0 : from_e(h, v.w);
+    }
+    if (n) *n = rec.size();
+    if (old_checksum) *old_checksum = h->wcs[slot];
+    if (new_checksum) *new_checksum = cs;
+    if (num_members) *num_members = (int32_t)info[1];
+    h->wcs[slot] = cs;
+    return SWIMSIM_OK;
+}
+
+// ---- ProtocolStats (swim/stats.go:81-104) ----
+int swimsim_protocol_stats(swimsim_t *h, swimsim_protocol_stats_t *out) {
+    if (!h || !out) return SWIMSIM_EINVAL;
+    memset(out, 0, sizeof *out);
+    std::vector<double> v(h->round_ms.begin(), h->round_ms.end());
+    for (double &x : v) x *= 1e6;                                 // ns, as go-metrics times durations
+    const size_t n = v.size();
+    out->count = (int64_t)n;
+    out->protocol_rate_ns = (int64_t)h->period * 1000000;         // AdjustProtocolRate (gossip.go:110-115):
+    if (n) {                                                      // max(2 x median, MinProtocolPeriod)
+        std::sort(v.begin(), v.end());
+        double sum = 0, sq = 0;
+        for (double x : v) sum += x;
+        const double mean = sum / (double)n;
+        for (double x : v) sq += (x - mean) * (x - mean);
+        // go-metrics SampleVariance / SamplePercentile (pos = p * (n + 1), linear interpolation)
+        auto pct = [&](double p) {
+            const double pos = p * (double)(n + 1);
+            if (pos < 1.0) return v[0];
+            if (pos >= (double)n) return v[n - 1];
+            const double lo = v[(size_t)pos - 1], hi = v[(size_t)pos];
+            return lo + (pos - std::floor(pos)) * (hi - lo);
+        };
+        out->min_ns = v[0];
+        out->max_ns = v[n - 1];
+        out->sum_ns = sum;
+        out->mean_ns = mean;
+        out->variance = sq / (double)n;
+        out->stddev_ns = std::sqrt(out->variance);
+        out->median_ns = pct(0.5);
+        out->p75_ns = pct(0.75);
+        out->p95_ns = pct(0.95);
+        out->p99_ns = pct(0.99);
+        out->p999_ns = pct(0.999);
+        out->protocol_rate_ns = std::max<int64_t>(out->protocol_rate_ns, (int64_t)(2.0 * out->median_ns));
+    }
+    // Meter rates per node and simulated second: served = pings handled + ping-reqs handled
+    // (ping_handler.go:37-38, ping_request_handler.go:45-46); clientRate is never marked in the reference
+    uint64_t c[CTR_STRIDE];
+    if (int rc = read_counters(h, c)) return rc;
+    const double secs = (double)h->round * h->period * 1e-3;
+    if (secs > 0) {
+        out->server_rate = (double)(c[C_PINGS_OK] + c[C_HELPER_CALLS]) / ((double)h->N * secs);
+        out->total_rate = out->server_rate;
+    }
+    return SWIMSIM_OK;
 }
 
 int swimsim_enable_timing(swimsim_t *h, int32_t enable) {

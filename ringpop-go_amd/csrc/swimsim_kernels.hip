@@ -102,6 +102,10 @@ __device__ __forceinline__ void merge_change_w(const DS &d, uint32_t ol, uint32_
         atomicOr(&d.dbit[(size_t)ol * d.NBIT + (m >> 5)], 1u << (m & 31));
     }
     d.dent[idx] = make_uint4(de_x(nsrc, 0), nsinc, nw_, 0);
+    if (d.wslot) {                                                 // watched row: MemberlistChangesAppliedEvent
+        const uint32_t ws = d.wslot[ol];                           // (memberlist.go:378-383)
+        if (ws != SRC_NONE) d.wlog[(size_t)ws * d.NP + m] = make_uint4(nw_, nsrc, nsinc, 1u);
+    }
     if (m != o) {                                                  // no timers for the local member
         const uint8_t ts = d.tst[idx];
         const uint32_t tstate = ts & 7u;
@@ -1280,6 +1284,44 @@ __global__ void k_ping_with(DS d, uint32_t tol, uint32_t sender, const MsgDesc *
 // ---------------------------------------------------------------------------------------------
 // readback helpers
 // ---------------------------------------------------------------------------------------------
+// drain the applied-change log of watched row ol (slot): out[i] = {member, member word, source, source e}
+// in member order, the flags cleared; info = {count, NumMembers}. One 1024-thread workgroup: each thread
+// takes a contiguous run of members, a block scan of the run counts places the records.
+__global__ void __launch_bounds__(1024) k_drain_applied(DS d, uint32_t ol, uint32_t slot, uint4 *out, uint32_t *info) {
+    __shared__ uint32_t part[1024];
+    __shared__ uint32_t memb[1024];
+    const uint32_t t = threadIdx.x, C = (d.NP + 1023) / 1024;
+    const uint32_t b = min(t * C, d.N), e = min(b + C, d.N);
+    uint4 *lg = d.wlog + (size_t)slot * d.NP;
+    const uint32_t *row = d.mw + (size_t)ol * d.NP;
+    uint32_t cnt = 0, mem = 0;
+    for (uint32_t m = b; m < e; m++) {
+        cnt += lg[m].w != 0u;
+        mem += (row[m] & 7u) != ST_UNKNOWN;
+    }
+    part[t] = cnt;
+    memb[t] = mem;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024; off <<= 1) {               // inclusive scans (Hillis-Steele)
+        const uint32_t v = t >= off ? part[t - off] : 0u, w = t >= off ? memb[t - off] : 0u;
+        __syncthreads();
+        part[t] += v;
+        memb[t] += w;
+        __syncthreads();
+    }
+    uint32_t pos = part[t] - cnt;
+    for (uint32_t m = b; m < e; m++) {
+        const uint4 v = lg[m];
+        if (!v.w) continue;
+        out[pos++] = make_uint4(m, v.x, v.y, v.z);
+        lg[m] = make_uint4(0, 0, 0, 0);
+    }
+    if (t == 1023) {
+        info[0] = part[1023];
+        info[1] = memb[1023];
+    }
+}
+
 __global__ void k_digest(DS d, unsigned long long *out, uint32_t period_div) {
     const uint32_t ol = wave_gid();
     if (ol >= d.NL) return;

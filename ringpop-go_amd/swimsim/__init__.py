@@ -62,6 +62,23 @@ ALLTOALLV = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, _U64P, _U64P, C.c_void_
 BCAST = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32)
 
 
+class ProtocolStatsC(C.Structure):
+    """swimsim_protocol_stats_t (include/swimsim.h)"""
+    _fields_ = [("count", C.c_int64)] + [(f, C.c_double) for f in (
+        "min_ns", "max_ns", "sum_ns", "mean_ns", "variance", "stddev_ns", "median_ns", "p75_ns", "p95_ns", "p99_ns",
+        "p999_ns")] + [("protocol_rate_ns", C.c_int64), ("client_rate", C.c_double), ("server_rate", C.c_double),
+                       ("total_rate", C.c_double)]
+
+
+@dataclass
+class MemberlistChangesAppliedEvent:
+    """swim.MemberlistChangesAppliedEvent (swim/events.go:56-61): changes are swimsim.wire.Change values"""
+    changes: list
+    old_checksum: int
+    new_checksum: int
+    num_members: int
+
+
 class HostTransport(C.Structure):
     """swimsim_host_transport (include/swimsim.h): host collectives for one-process-per-shard runs"""
     _fields_ = [("ctx", C.c_void_p), ("alltoall_u64", ALLTOALL_U64), ("alltoallv", ALLTOALLV), ("bcast", BCAST)]
@@ -119,6 +136,10 @@ def load_library(path: str = LIB_PATH):
         "swimsim_shard_info": (C.c_int, [P, C.POINTER(u32), C.POINTER(u32), C.POINTER(u32), C.POINTER(u32),
                                          C.POINTER(u64), C.POINTER(u64)]),
         "swimsim_comm_attach_host": (C.c_int, [P, u32, u32, C.POINTER(HostTransport)]),
+        "swimsim_watch": (C.c_int, [P, u32, i32]),
+        "swimsim_applied_changes": (C.c_int, [P, u32, P, P, P, P, P, sz, C.POINTER(sz), C.POINTER(u32),
+                                              C.POINTER(u32), C.POINTER(i32)]),
+        "swimsim_protocol_stats": (C.c_int, [P, C.POINTER(ProtocolStatsC)]),
     }
     for name, (res, args) in sigs.items():
         f = getattr(L, name)
@@ -171,6 +192,7 @@ class Cluster:
         self.h, self.n, self.lo, self.nl = h, n, lo, nl
         self.t0_ms, self.period_ms = t0_ms, period_ms
         self._addr_buf = None
+        self._listeners = {}
         return self
 
     def __init__(self, n, *, t0_ms=T0_MS, period_ms=200, suspect_ms=5000, faulty_ms=24 * 3600 * 1000,
@@ -182,6 +204,7 @@ class Cluster:
         L = load_library()
         self.n = n
         self.t0_ms, self.period_ms = t0_ms, period_ms
+        self._listeners = {}                     # observer -> [listener] (Node.RegisterListener)
         if comm is not None and observer_range is None:
             observer_range = shard_range(n, comm[0], comm[1])
         cfg = Config()
@@ -236,6 +259,61 @@ class Cluster:
     def step(self, rounds=1, events=()):
         ev = _events(events)
         self._chk(load_library().swimsim_step(self.h, rounds, ev, len(events)))
+        self._emit()
+
+    def _emit(self):
+        """deliver MemberlistChangesAppliedEvent to the listeners of watched observers (node.emit, node.go:266-270):
+        one event per observer with changes applied since the previous delivery"""
+        for o, ls in self._listeners.items():
+            if not ls:
+                continue
+            changes, old, new, nm = self.applied_changes(o)
+            if not changes:
+                continue
+            evt = MemberlistChangesAppliedEvent(self._wire_changes(changes), old, new, nm)
+            for l in ls:
+                (l.HandleEvent if hasattr(l, "HandleEvent") else l)(evt)
+
+    @staticmethod
+    def _wire_changes(changes):
+        from .wire import Change
+        return [Change(address_of(s) if s >= 0 else "", si, address_of(m), inc, STATUS_NAMES[st], False)
+                for (m, st, inc, s, si) in changes]
+
+    # ---- applied-change stream (MemberlistChangesAppliedEvent, swim/events.go:56-61) ----------
+    def watch(self, o, on=True):
+        self._chk(load_library().swimsim_watch(self.h, o, int(on)))
+
+    def applied_changes(self, o):
+        """drain watched observer o: ([(member, status, inc, source, source_inc)] in member order, old checksum,
+        new checksum, NumMembers) since the previous drain"""
+        cap = self.n
+        m = np.empty(cap, np.int32); st = np.empty(cap, np.int32); inc = np.empty(cap, np.int64)
+        s = np.empty(cap, np.int32); si = np.empty(cap, np.int64)
+        n, old, new, nm = C.c_size_t(), C.c_uint32(), C.c_uint32(), C.c_int32()
+        self._chk(load_library().swimsim_applied_changes(self.h, o, m.ctypes.data, st.ctypes.data, inc.ctypes.data,
+                                                         s.ctypes.data, si.ctypes.data, cap, C.byref(n), C.byref(old),
+                                                         C.byref(new), C.byref(nm)))
+        k = n.value
+        return ([(int(m[i]), int(st[i]), int(inc[i]), int(s[i]), int(si[i])) for i in range(k)], old.value, new.value,
+                nm.value)
+
+    def register_listener(self, o, listener):
+        """NodeInterface.RegisterListener (node.go:146) for simulated node o"""
+        if o not in self._listeners:
+            self.watch(o)
+            self._listeners[o] = []
+        self._listeners[o].append(listener)
+
+    def protocol_stats(self):
+        """NodeInterface.ProtocolStats (stats.go:81-104): Timing over protocol rounds (ns), ProtocolRate (ns),
+        ClientRate / ServerRate / TotalRate per node per simulated second"""
+        p = ProtocolStatsC()
+        self._chk(load_library().swimsim_protocol_stats(self.h, C.byref(p)))
+        timing = {k: getattr(p, k) for k in ("count", "min_ns", "max_ns", "sum_ns", "mean_ns", "variance", "stddev_ns",
+                                             "median_ns", "p75_ns", "p95_ns", "p99_ns", "p999_ns")}
+        return {"timing": timing, "protocol_rate_ns": p.protocol_rate_ns, "client_rate": p.client_rate,
+                "server_rate": p.server_rate, "total_rate": p.total_rate}
 
     def run(self, rounds, events=()):
         self.step(rounds, events)
@@ -439,6 +517,20 @@ class ShardedCluster:
         if rc < 0:
             msgs = "; ".join(load_library().swimsim_last_error(c.h).decode() for c in self.shards)
             raise SwimsimError(f"{ERRORS.get(rc, rc)}: {msgs}")
+        for c in self.shards:
+            c._emit()
+
+    def watch(self, o, on=True):
+        self.owner(o).watch(o, on)
+
+    def applied_changes(self, o):
+        return self.owner(o).applied_changes(o)
+
+    def register_listener(self, o, listener):
+        self.owner(o).register_listener(o, listener)
+
+    def protocol_stats(self):
+        return self.shards[0].protocol_stats()
 
     @property
     def round(self):
@@ -636,3 +728,9 @@ class Node:
 
     def HasChanges(self):
         return self.disseminator.HasChanges()
+
+    def RegisterListener(self, listener):                 # node.go:146; events.EventListener.HandleEvent
+        self.c.register_listener(self.o, listener)
+
+    def ProtocolStats(self):                              # stats.go:81-104
+        return self.c.protocol_stats()
