@@ -176,6 +176,17 @@ typedef struct swimsim_protocol_stats {
 } swimsim_protocol_stats_t;
 int swimsim_protocol_stats(swimsim_t *h, swimsim_protocol_stats_t *out);
 
+/* device memory of the handle (DESIGN.md §2 budget): bytes of the row words, dissemination entries (+ presence
+ * bits), timers (+ block bounds), message pool and dense snapshots, total bytes held; the dense-snapshot slots
+ * (main, side stream) and how many phases hashed their dirty senders before issue because the lazy C_o
+ * snapshots would not have fit in the slots (exact either way) */
+typedef struct swimsim_memory_t {
+    uint64_t row_words, dissemination, timers, message_pool, dense_snapshots, total;
+    uint32_t dense_cap, side_cap;
+    uint64_t lazy_fallbacks;
+} swimsim_memory_t;
+int swimsim_memory(swimsim_t *h, swimsim_memory_t *out);
+
 /* ---- measurement ---- */
 /* average device time (ms) of each kernel family since the last reset, for roofline reporting */
 int swimsim_kernel_times(swimsim_t *h, const char **names, double *avg_ms, uint64_t *launches,

@@ -260,6 +260,8 @@ struct swimsim {
     unsigned long long *keys = nullptr, *keys_sorted = nullptr;
     uint32_t keycap = 0;
     uint64_t x_bytes = 0, x_calls = 0;        // exchanged bytes / exchanges (measurement)
+    uint64_t lazy_fallbacks = 0;              // phases whose dirty senders were hashed before issue
+    uint64_t alloc_bytes = 0;                 // device bytes held by the handle (dalloc)
     // work buffers
     int32_t *tgt = nullptr;
     uint8_t *failed = nullptr;
@@ -333,6 +335,7 @@ int dalloc(swimsim *h, T **p, size_t count, const char *what) {
     hipError_t e = hipMalloc(&q, bytes);
     if (e != hipSuccess) return h->fail(SWIMSIM_ENOMEM, "hipMalloc(%s, %zu bytes): %s", what, bytes, hipGetErrorString(e));
     h->allocs.push_back(q);
+    h->alloc_bytes += bytes;
     *p = (T *)q;
     return 0;
 }
@@ -696,6 +699,25 @@ int checksum_dirty(swimsim *h, int mode, bool async = false) {
     return 0;
 }
 
+// Lazy C_o (k_issue) takes one dense snapshot per dirty sender. When the snapshot pool could not hold them
+// beside the phase's other snapshots (deferred decisions, reverse-full-sync sources), the dirty senders are
+// hashed now instead: ComputeChecksum at Update time, as the reference does (memberlist.go:367). The checksum
+// values are the same either way; only where the work happens changes. mode: k_list's 1 (phase I senders) or
+// 2 (phase Q1 senders).
+int bound_lazy_snapshots(swimsim *h, int mode) {
+    HIPCHK(h, hipMemsetAsync(h->cnt, 0, 4, h->s));
+    hipLaunchKernelGGL(k_list, dim3(blocks_for_threads(h->NL)), dim3(256), 0, h->s, h->d, mode, h->tgt, h->failed,
+                       h->list, h->cnt);
+    uint32_t *hc = h->hinfo + 12;
+    HIPCHK(h, hipMemcpyAsync(hc, h->cnt, 4, hipMemcpyDeviceToHost, h->s));
+    HIPCHK(h, hipStreamSynchronize(h->s));
+    if (*hc <= h->d.dense_cap / 2) return 0;
+    if (int rc = sync_side(h)) return rc;
+    hash_rows(h, h->list, h->cnt, h->NL, *hc);
+    h->lazy_fallbacks++;
+    return 0;
+}
+
 // run the receive waves over a sorted inbox (phase D when phase==0, phase Q2 when phase==1), then
 // resolve the deferred full-sync decisions with one batched checksum of the receivers' snapshots
 // resolve the deferred full-sync decisions: one batched checksum of the snapshots they wait on (dirty
@@ -989,6 +1011,7 @@ int step_one(swimsim *h, const swimsim_event *ev, size_t nev) {
     //      hashed only if a receiver, on any shard, compares it) ----
     uint32_t *hi = h->hinfo;
     uint32_t ninbox = h->NL;
+    if (int rc = bound_lazy_snapshots(h, 1)) return rc;
     HIPCHK(h, hipMemsetAsync(h->d.dense_cur, 0, 4, h->s));         // dense snapshots live from here through R
     {
         {
@@ -1033,6 +1056,7 @@ int step_one(swimsim *h, const swimsim_event *ev, size_t nev) {
             hipLaunchKernelGGL(k_helpers, dim3(blocks_for_threads(h->NL)), dim3(256), 0, h->s, h->d, h->tgt, h->failed,
                                h->H, h->nh, r);
         }
+        if (int rc = bound_lazy_snapshots(h, 2)) return rc;
         HIPCHK(h, hipMemsetAsync(h->d.dense_cur, 0, 4, h->s));     // dense snapshots live from here through Q3
         {
             {
@@ -1237,6 +1261,8 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
         return bail(SWIMSIM_EHIP);
     }
     if (const char *v = getenv("SWIMSIM_CS_ASYNC")) h->cs_async = atoi(v) != 0;
+    if (const char *v = getenv("SWIMSIM_CS_KERNEL")) g_cs_kernel = atoi(v);
+    if (const char *v = getenv("SWIMSIM_CS_NARROW_ROWS")) g_cs_narrow_rows = (uint32_t)strtoul(v, nullptr, 10);
     DS &d = h->d;
     d.N = h->N; d.NP = h->NP; d.NL = h->NL; d.lo = h->lo;
     d.NB = h->NP / 64;
@@ -1292,6 +1318,8 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
         hipMemGetInfo(&freeb, &totalb);
         const uint64_t by_mem = (uint64_t)(freeb / 3) / (4ull * h->NP);
         d.dense_cap = (uint32_t)std::max<uint64_t>(64, std::min<uint64_t>(2ull * h->NL + 64, by_mem));
+        if (const char *v = getenv("SWIMSIM_DENSE_CAP"))               // tests: a small pool exercises the fallbacks
+            d.dense_cap = (uint32_t)std::max<unsigned long>(64, std::min<unsigned long>(d.dense_cap, strtoul(v, nullptr, 10)));
         // side-stream checksum snapshots (latency-bound phase C launches only), up to 1/8 of the free HBM
         const uint64_t snap_mem = (uint64_t)(freeb / 8) / (4ull * h->NP);
         uint64_t async_rows = CS_NARROW_ROWS;
@@ -1847,6 +1875,21 @@ int swimsim_protocol_stats(swimsim_t *h, swimsim_protocol_stats_t *out) {
         out->server_rate = (double)(c[C_PINGS_OK] + c[C_HELPER_CALLS]) / ((double)h->N * secs);
         out->total_rate = out->server_rate;
     }
+    return SWIMSIM_OK;
+}
+
+int swimsim_memory(swimsim_t *h, swimsim_memory_t *out) {
+    if (!h || !out) return SWIMSIM_EINVAL;
+    const uint64_t rows = (uint64_t)h->NL * h->NP;
+    out->row_words = rows * 4;
+    out->dissemination = rows * 16 + (uint64_t)h->NL * h->d.NBIT * 4;
+    out->timers = rows * 9 + (uint64_t)h->NL * h->d.NB * 4;
+    out->message_pool = h->d.pool_cap * 16;
+    out->dense_snapshots = ((uint64_t)h->d.dense_cap + h->snap_cap) * h->NP * 4;
+    out->total = h->alloc_bytes + h->sbuf_cap + h->rbuf_cap;
+    out->dense_cap = h->d.dense_cap;
+    out->side_cap = h->snap_cap;
+    out->lazy_fallbacks = h->lazy_fallbacks;
     return SWIMSIM_OK;
 }
 

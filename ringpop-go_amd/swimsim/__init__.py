@@ -79,6 +79,13 @@ class MemberlistChangesAppliedEvent:
     num_members: int
 
 
+class MemoryC(C.Structure):
+    """swimsim_memory_t (include/swimsim.h)"""
+    _fields_ = [(f, C.c_uint64) for f in ("row_words", "dissemination", "timers", "message_pool", "dense_snapshots",
+                                          "total")] + [("dense_cap", C.c_uint32), ("side_cap", C.c_uint32),
+                                                       ("lazy_fallbacks", C.c_uint64)]
+
+
 class HostTransport(C.Structure):
     """swimsim_host_transport (include/swimsim.h): host collectives for one-process-per-shard runs"""
     _fields_ = [("ctx", C.c_void_p), ("alltoall_u64", ALLTOALL_U64), ("alltoallv", ALLTOALLV), ("bcast", BCAST)]
@@ -140,6 +147,7 @@ def load_library(path: str = LIB_PATH):
         "swimsim_applied_changes": (C.c_int, [P, u32, P, P, P, P, P, sz, C.POINTER(sz), C.POINTER(u32),
                                               C.POINTER(u32), C.POINTER(i32)]),
         "swimsim_protocol_stats": (C.c_int, [P, C.POINTER(ProtocolStatsC)]),
+        "swimsim_memory": (C.c_int, [P, C.POINTER(MemoryC)]),
     }
     for name, (res, args) in sigs.items():
         f = getattr(L, name)
@@ -304,6 +312,12 @@ class Cluster:
             self.watch(o)
             self._listeners[o] = []
         self._listeners[o].append(listener)
+
+    def memory(self):
+        """device memory of the handle (swimsim_memory): bytes per structure, snapshot slots, lazy-C_o fallbacks"""
+        m = MemoryC()
+        self._chk(load_library().swimsim_memory(self.h, C.byref(m)))
+        return {f: getattr(m, f) for f, _ in MemoryC._fields_}
 
     def protocol_stats(self):
         """NodeInterface.ProtocolStats (stats.go:81-104): Timing over protocol rounds (ns), ProtocolRate (ns),

@@ -662,3 +662,37 @@ def test_hashring_lookup_loop_around_kat():
     tree node (the test's precondition, asserted there)."""
     ring = _ring(_gen_addresses(1, 1, 10), 1)
     assert _lookup(ring, "a random key") != ring[0][1]
+
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_openmp_oracle_equals_single_thread():
+    """The OpenMP build of the oracle (CPU baseline, at-size fixtures) runs a phase's per-observer loops in
+    parallel; observers of a phase touch only their own state, so every round must equal the single-threaded
+    parity oracle's (checked in a child process: one process loads one oracle build)."""
+    import json
+    import subprocess
+    import sys
+    code = r"""
+import json, os, sys
+sys.path.insert(0, os.path.join(REPO, 'tests')); sys.path.insert(0, os.path.join(REPO, 'ringpop-go_amd'))
+from oracle_ffi import OracleSim
+from swimsim import workloads as W
+out = []
+for wl in (W.config2(n=200, rounds=25), W.config4(n=96, rounds=70, split_until=20, heals=(20, 35)),
+           W.config5(n=160, rounds=30, every=10)):
+    o = OracleSim(wl.n)
+    for r in range(wl.rounds):
+        o.step(wl.events_for(r))
+        out.append([list(o.digest()), [int(x) for x in o.checksums()], o.counters()])
+print(json.dumps(out))
+"""
+    runs = []
+    for lib_name, threads in (("libswim_oracle.so", "1"), ("libswim_oracle_omp.so", "4")):
+        env = dict(os.environ, ORACLE_LIB=os.path.join(REPO, "oracle", "build", lib_name), OMP_NUM_THREADS=threads)
+        p = subprocess.run([sys.executable, "-c", f"REPO={REPO!r}\n" + code], capture_output=True, text=True,
+                           env=env, timeout=600)
+        assert p.returncode == 0, p.stderr[-2000:]
+        runs.append(json.loads(p.stdout))
+    assert runs[0] == runs[1]
