@@ -168,12 +168,40 @@ __device__ __forceinline__ void wave_finalize(const DS &d, uint32_t ol, const MA
 // message's changes are distinct members, so no load of a batch depends on a store of the same batch).
 constexpr int MB = 4;
 
+// a dense message (MembershipAsChanges: full sync, reverse full sync, heal) streams the whole row. (Kept
+// inline: an out-of-line call makes every launch copy the DS argument block to scratch, 480 B per lane.)
+__device__ __forceinline__ void wave_merge_dense(const DS &d, uint32_t ol, uint32_t o, const MsgDesc &md,
+                                                           uint32_t now_e, uint32_t sched_r, MAcc &acc) {
+    const uint32_t *rowp = d.mw + (size_t)ol * d.NP;
+    const uint32_t slot = md.off_lo;
+    const uint4 meta = d.dense_meta[slot];
+    const uint32_t *snap = d.dense + (size_t)slot * d.NP;
+    for (uint32_t base = 0; base < d.N; base += 64 * MB) {
+        uint32_t w[MB], cur[MB];
+#pragma unroll
+        for (int u = 0; u < MB; u++) {
+            const uint32_t m = base + u * 64 + lane_id();
+            w[u] = m < d.N ? snap[m] : ST_UNKNOWN;
+            cur[u] = m < d.N ? rowp[m] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < MB; u++) {
+            const uint32_t m = base + u * 64 + lane_id();
+            if ((w[u] & 7u) != ST_UNKNOWN)
+                merge_change_w(d, ol, o, m, cur[u], w[u] & 7u, w[u] >> 3, meta.x, meta.y, now_e, sched_r, acc);
+        }
+    }
+}
+
 // merge a whole message into row ol (wave-wide; the changes of one message are distinct members)
 // cset selects the measurement counters (0: k_recv's C_X_MERGED/C_X_APPLIED, 1: k_resp's pair, 2: none)
 __device__ void wave_merge_msg(const DS &d, uint32_t ol, uint32_t o, const MsgDesc &md, uint32_t now_e, uint32_t sched_r,
                                int cset = 0) {
     MAcc acc;
-    const uint32_t *rowp = d.mw + (size_t)ol * d.NP;
+    // a sparse message reads the member words through the dissemination cells' mirror (dent.z == mw always):
+    // the cells a merge touches are the ones RecordChange and this wave's IssueAsReceiver / bump touch next,
+    // mostly the same members, so those gathers find the sectors in L2
+    const uint32_t *mirror = (const uint32_t *)(d.dent + (size_t)ol * d.NP) + 2;
     if (md.kind == 0) {
         const unsigned long long off = ((unsigned long long)md.off_hi << 32) | md.off_lo;
         for (uint32_t base = 0; base < md.len; base += 64 * MB) {
@@ -185,7 +213,7 @@ __device__ void wave_merge_msg(const DS &d, uint32_t ol, uint32_t o, const MsgDe
                 rec[u] = i < md.len ? d.pool[off + i] : make_uint4(0xFFFFFFFFu, 0, 0, 0);
             }
 #pragma unroll
-            for (int u = 0; u < MB; u++) cur[u] = rec[u].x != 0xFFFFFFFFu ? rowp[rec[u].x & 0xFFFFFFu] : 0u;
+            for (int u = 0; u < MB; u++) cur[u] = rec[u].x != 0xFFFFFFFFu ? mirror[(size_t)(rec[u].x & 0xFFFFFFu) * 4] : 0u;
 #pragma unroll
             for (int u = 0; u < MB; u++)
                 if (rec[u].x != 0xFFFFFFFFu)
@@ -193,24 +221,7 @@ __device__ void wave_merge_msg(const DS &d, uint32_t ol, uint32_t o, const MsgDe
                                    sched_r, acc);
         }
     } else if (md.kind == 1) {
-        const uint32_t slot = md.off_lo;
-        const uint4 meta = d.dense_meta[slot];
-        const uint32_t *snap = d.dense + (size_t)slot * d.NP;
-        for (uint32_t base = 0; base < d.N; base += 64 * MB) {
-            uint32_t w[MB], cur[MB];
-#pragma unroll
-            for (int u = 0; u < MB; u++) {
-                const uint32_t m = base + u * 64 + lane_id();
-                w[u] = m < d.N ? snap[m] : ST_UNKNOWN;
-                cur[u] = m < d.N ? rowp[m] : 0u;
-            }
-#pragma unroll
-            for (int u = 0; u < MB; u++) {
-                const uint32_t m = base + u * 64 + lane_id();
-                if ((w[u] & 7u) != ST_UNKNOWN)
-                    merge_change_w(d, ol, o, m, cur[u], w[u] & 7u, w[u] >> 3, meta.x, meta.y, now_e, sched_r, acc);
-            }
-        }
+        wave_merge_dense(d, ol, o, md, now_e, sched_r, acc);
     }
     __threadfence_block();
     wave_finalize(d, ol, acc, cset);
