@@ -5,9 +5,9 @@
 //                      statePrecedence (swim/member.go:112-128), 7 = not in the memberlist.
 //                      (e,status) as one integer makes nonLocalOverride (member.go:79-93) a single
 //                      unsigned compare.
-//   dent u32x4[NL][NP] dissemination entry (disseminator.go:39-42): {source | p << 24, source e,
-//                      member word, 0}; p = 0xFF: no entry. The member word is a copy of mw kept
-//                      equal while the entry exists, so issuing an entry is one 16-byte gather.
+//   dent u32x2[NL][NP] dissemination entry (disseminator.go:39-42): {source | p << 24, source e};
+//                      p = 0xFF: no entry. The entry's (status, incarnation) is the row's member
+//                      word (every Apply is followed by RecordChange, node.go:424-428).
 //   tst u8  [NL][NP]   timer state (suspect 1 / faulty 2 / tombstone 4) | 0x80 fired
 //   tmr u32x2 [NL][NP] timer {deadline round, subject e}
 //   dbit u32 [NL][NBIT] bit m: member m has a dissemination entry (exactly: p != 0xFF)
@@ -60,7 +60,7 @@ struct DS {
     uint32_t ecap;
     uint64_t seed;
     uint32_t *mw;
-    uint4 *dent;            // {source | p << 24, source e, member word, 0}
+    uint2 *dent;            // {source | p << 24, source e}
     uint8_t *tst;
     uint2 *tmr;             // {timer deadline round, timer subject e}
     uint32_t *dbit;         // [NL][NBIT] dissemination presence bits

@@ -1304,10 +1304,16 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
         d.addrw = dev;
     }
     if ((rc = build_tail_table(h, cfg->max_rounds ? cfg->max_rounds : 65536))) return bail(rc);
-    // pools
+    // pools. The message pool holds one round's change records (requests and responses are both live in
+    // phase R). Automatic size: 4 records per (observer, member) pair, bounded by the larger of 8 GB and 45 %
+    // of the HBM left after the rows (large-burst workloads: a buffer holds up to ~25 % of the members and
+    // every live member sends and answers one message per round, DESIGN.md §2 memory budget)
+    size_t free_rows = 0, total_rows = 0;
+    hipMemGetInfo(&free_rows, &total_rows);
+    const uint64_t pool_bound = std::max<uint64_t>(8ull << 30, (uint64_t)(free_rows / 100) * 45) / 16;
     const uint64_t want_records = cfg->message_pool_bytes
                                       ? cfg->message_pool_bytes / 16
-                                      : std::min<uint64_t>(std::max<uint64_t>(4ull * h->NL * h->N, 1ull << 20), (8ull << 30) / 16);
+                                      : std::min<uint64_t>(std::max<uint64_t>(4ull * h->NL * h->N, 1ull << 20), pool_bound);
     d.pool_cap = want_records;
     if ((rc = dalloc(h, &d.pool, want_records, "message pool")) || (rc = dalloc(h, &d.pool_cur, 1, "pool cursor")))
         return bail(rc);
@@ -1611,8 +1617,8 @@ int swimsim_changes(swimsim_t *h, uint32_t o, int32_t *member, int32_t *p, int32
                     size_t cap, size_t *n) {
     if (!h || !own(h, o)) return SWIMSIM_EINVAL;
     const size_t base = (size_t)(o - h->lo) * h->NP;
-    std::vector<uint4> ent(h->NP);
-    HIPCHK(h, hipMemcpyAsync(ent.data(), h->d.dent + base, h->NP * 16, hipMemcpyDeviceToHost, h->s));
+    std::vector<uint2> ent(h->NP);
+    HIPCHK(h, hipMemcpyAsync(ent.data(), h->d.dent + base, h->NP * 8, hipMemcpyDeviceToHost, h->s));
     HIPCHK(h, hipStreamSynchronize(h->s));
     size_t k = 0;
     for (uint32_t m = 0; m < h->N; m++) {
@@ -1882,7 +1888,7 @@ int swimsim_memory(swimsim_t *h, swimsim_memory_t *out) {
     if (!h || !out) return SWIMSIM_EINVAL;
     const uint64_t rows = (uint64_t)h->NL * h->NP;
     out->row_words = rows * 4;
-    out->dissemination = rows * 16 + (uint64_t)h->NL * h->d.NBIT * 4;
+    out->dissemination = rows * sizeof(uint2) + (uint64_t)h->NL * h->d.NBIT * 4;
     out->timers = rows * 9 + (uint64_t)h->NL * h->d.NB * 4;
     out->message_pool = h->d.pool_cap * 16;
     out->dense_snapshots = ((uint64_t)h->d.dense_cap + h->snap_cap) * h->NP * 4;

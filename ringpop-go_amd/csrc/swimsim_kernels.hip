@@ -97,11 +97,11 @@ __device__ __forceinline__ void merge_change_w(const DS &d, uint32_t ol, uint32_
     acc.dfp += fpmix(m, (ne << 3) | nst) - fpmix(m, cur);
     if (m != o) acc.dping += (int)is_pingable(nst) - (int)is_pingable(cur_st);
     // RecordChange (disseminator.go:223-227): entry = {p 0, source, source incarnation}
-    if (de_p(((const uint32_t *)(d.dent + idx))[0]) == DP_NONE) {
+    if (de_p(d.dent[idx].x) == DP_NONE) {
         acc.ddc++;
         atomicOr(&d.dbit[(size_t)ol * d.NBIT + (m >> 5)], 1u << (m & 31));
     }
-    d.dent[idx] = make_uint4(de_x(nsrc, 0), nsinc, nw_, 0);
+    d.dent[idx] = make_uint2(de_x(nsrc, 0), nsinc);
     if (d.wslot) {                                                 // watched row: MemberlistChangesAppliedEvent
         const uint32_t ws = d.wslot[ol];                           // (memberlist.go:378-383)
         if (ws != SRC_NONE) d.wlog[(size_t)ws * d.NP + m] = make_uint4(nw_, nsrc, nsinc, 1u);
@@ -198,10 +198,7 @@ __device__ __forceinline__ void wave_merge_dense(const DS &d, uint32_t ol, uint3
 __device__ void wave_merge_msg(const DS &d, uint32_t ol, uint32_t o, const MsgDesc &md, uint32_t now_e, uint32_t sched_r,
                                int cset = 0) {
     MAcc acc;
-    // a sparse message reads the member words through the dissemination cells' mirror (dent.z == mw always):
-    // the cells a merge touches are the ones RecordChange and this wave's IssueAsReceiver / bump touch next,
-    // mostly the same members, so those gathers find the sectors in L2
-    const uint32_t *mirror = (const uint32_t *)(d.dent + (size_t)ol * d.NP) + 2;
+    const uint32_t *rowp = d.mw + (size_t)ol * d.NP;
     if (md.kind == 0) {
         const unsigned long long off = ((unsigned long long)md.off_hi << 32) | md.off_lo;
         for (uint32_t base = 0; base < md.len; base += 64 * MB) {
@@ -213,7 +210,7 @@ __device__ void wave_merge_msg(const DS &d, uint32_t ol, uint32_t o, const MsgDe
                 rec[u] = i < md.len ? d.pool[off + i] : make_uint4(0xFFFFFFFFu, 0, 0, 0);
             }
 #pragma unroll
-            for (int u = 0; u < MB; u++) cur[u] = rec[u].x != 0xFFFFFFFFu ? mirror[(size_t)(rec[u].x & 0xFFFFFFu) * 4] : 0u;
+            for (int u = 0; u < MB; u++) cur[u] = rec[u].x != 0xFFFFFFFFu ? rowp[rec[u].x & 0xFFFFFFu] : 0u;
 #pragma unroll
             for (int u = 0; u < MB; u++)
                 if (rec[u].x != 0xFFFFFFFFu)
@@ -232,7 +229,7 @@ __device__ void wave_bump(const DS &d, uint32_t ol, const MsgDesc &md) {
     if (md.kind != 0) return;
     const unsigned long long off = ((unsigned long long)md.off_hi << 32) | md.off_lo;
     const int maxp = d.maxp[ol];
-    uint32_t *dx = (uint32_t *)(d.dent + (size_t)ol * d.NP);       // word 0 of each entry, stride 4
+    uint32_t *dx = (uint32_t *)(d.dent + (size_t)ol * d.NP);       // word 0 of each entry, stride 2
     int del = 0;
     for (uint32_t base = 0; base < md.len; base += 64 * MB) {
         uint32_t m[MB], x[MB];
@@ -242,17 +239,17 @@ __device__ void wave_bump(const DS &d, uint32_t ol, const MsgDesc &md) {
             m[u] = i < md.len ? (d.pool[off + i].x & 0xFFFFFFu) : 0xFFFFFFFFu;
         }
 #pragma unroll
-        for (int u = 0; u < MB; u++) x[u] = m[u] != 0xFFFFFFFFu ? dx[(size_t)m[u] * 4] : DE_NONE;
+        for (int u = 0; u < MB; u++) x[u] = m[u] != 0xFFFFFFFFu ? dx[(size_t)m[u] * 2] : DE_NONE;
 #pragma unroll
         for (int u = 0; u < MB; u++) {
             const uint32_t p = de_p(x[u]);
             if (p == DP_NONE) continue;
             if ((int)(p + 1) >= maxp) {
-                dx[(size_t)m[u] * 4] = x[u] | 0xFF000000u;
+                dx[(size_t)m[u] * 2] = x[u] | 0xFF000000u;
                 atomicAnd(&d.dbit[(size_t)ol * d.NBIT + (m[u] >> 5)], ~(1u << (m[u] & 31)));
                 del++;
             } else {
-                dx[(size_t)m[u] * 4] = x[u] + (1u << 24);
+                dx[(size_t)m[u] * 2] = x[u] + (1u << 24);
             }
         }
     }
@@ -324,16 +321,19 @@ __device__ uint32_t wave_issue_t(const DS &d, uint32_t ol, uint32_t sender, uint
                 else if (hi) { m[k] = mbase + 64 + (uint32_t)(__ffsll((long long)hi) - 1); hi &= hi - 1; }
                 else m[k] = 0xFFFFFFFFu;
             }
-            uint4 ce[MB];                                        // one 16-byte gather per entry
+            uint2 ce[MB];                                        // the 8-byte entry and the member word
+            uint32_t wv[MB];
 #pragma unroll
-            for (int k = 0; k < MB; k++) ce[k] = m[k] != 0xFFFFFFFFu ? d.dent[rb + m[k]] : make_uint4(DE_NONE, 0, 0, 0);
-            uint32_t p[MB], wv[MB];
+            for (int k = 0; k < MB; k++) {
+                ce[k] = m[k] != 0xFFFFFFFFu ? d.dent[rb + m[k]] : make_uint2(DE_NONE, 0);
+                wv[k] = m[k] != 0xFFFFFFFFu ? d.mw[rb + m[k]] : 0u;
+            }
+            uint32_t p[MB];
             uint2 sr[MB];
 #pragma unroll
             for (int k = 0; k < MB; k++) {
                 p[k] = de_p(ce[k].x);
                 sr[k] = make_uint2(de_src(ce[k].x), ce[k].y);
-                wv[k] = ce[k].z;
             }
             bool keep[MB];
             uint32_t nk = 0;
@@ -434,7 +434,7 @@ __global__ void k_init_rows(DS d, int mode, uint32_t e0) {
         if (m < d.N && (mode == 0 || m == o)) w = (e0 << 3) | ST_ALIVE;
         if (m < d.N) fp += fpmix(m, w);
         d.mw[idx] = w;
-        d.dent[idx] = make_uint4(DE_NONE, 0, w, 0);
+        d.dent[idx] = make_uint2(DE_NONE, 0);
         d.tst[idx] = 0;
         d.tmr[idx] = make_uint2(NO_DEADLINE, 0);
     }
@@ -470,9 +470,7 @@ __global__ void k_recount(DS d, uint32_t ol) {
         const uint32_t w = d.mw[idx];
         fp += fpmix(m, w);
         if (m != o && is_pingable(w & 7u)) p++;
-        uint32_t *de = (uint32_t *)(d.dent + idx);
-        if (de_p(de[0]) != DP_NONE) c++;
-        de[2] = w;                                                   // re-mirror the member word
+        if (de_p(d.dent[idx].x) != DP_NONE) c++;
         len += reclen(d, w & 7u, w >> 3);
         if ((w & 7u) < 4u) last = (int)m;
     }
@@ -488,7 +486,7 @@ __global__ void k_recount(DS d, uint32_t ol) {
 }
 
 __global__ void k_clear_changes(DS d, uint32_t ol) {
-    for (uint32_t m = threadIdx.x; m < d.NP; m += blockDim.x) ((uint32_t *)(d.dent + (size_t)ol * d.NP + m))[0] = DE_NONE;
+    for (uint32_t m = threadIdx.x; m < d.NP; m += blockDim.x) d.dent[(size_t)ol * d.NP + m].x = DE_NONE;
     for (uint32_t b = threadIdx.x; b < d.NBIT; b += blockDim.x) d.dbit[(size_t)ol * d.NBIT + b] = 0;
     if (threadIdx.x == 0) d.dcnt[ol] = 0;
 }
@@ -572,7 +570,6 @@ __global__ void k_timers(DS d, uint32_t r) {
                     if ((w & 7u) != ST_UNKNOWN && m != o) {
                         if (is_pingable(w & 7u)) acc.dping--;
                         d.mw[idx] = (w & ~7u) | ST_UNKNOWN;
-                        ((uint32_t *)(d.dent + idx))[2] = (w & ~7u) | ST_UNKNOWN;   // entry mirror
                         track_len(d, ol, m, w, (w & ~7u) | ST_UNKNOWN, acc);
                         acc.dfp += fpmix(m, (w & ~7u) | ST_UNKNOWN) - fpmix(m, w);
                         acc.evict++;
@@ -1342,7 +1339,7 @@ __global__ void k_digest(DS d, unsigned long long *out, uint32_t period_div) {
         const size_t idx = (size_t)ol * d.NP + m;
         const uint32_t w = d.mw[idx];
         r += mix4(o, m, w & 7u, w >> 3);
-        const uint4 ce = d.dent[idx];
+        const uint2 ce = d.dent[idx];
         const uint32_t p = de_p(ce.x);
         if (p != DP_NONE) {
             const uint2 a = make_uint2(de_src(ce.x), ce.y);

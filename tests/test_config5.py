@@ -48,6 +48,6 @@ def test_memory_budget_accounting():
     m = eng.memory()
     np_ = (n + 63) // 64 * 64
     assert m["row_words"] == n * np_ * 4
-    assert m["dissemination"] >= n * np_ * 16 and m["timers"] >= n * np_ * 9
+    assert m["dissemination"] >= n * np_ * 8 and m["timers"] >= n * np_ * 9
     assert m["total"] >= m["row_words"] + m["dissemination"] + m["timers"] + m["message_pool"] + m["dense_snapshots"]
     assert m["dense_cap"] >= 64
