@@ -41,6 +41,7 @@ enum Counter {
 };
 
 constexpr int CTR_SHARDS = 64, CTR_STRIDE = 32;   // d.ctr is [CTR_SHARDS][CTR_STRIDE] u64
+constexpr uint32_t POOL_SHARDS = 64, POOL_CUR_STRIDE = 16;   // d.pool_cur is [POOL_SHARDS][POOL_CUR_STRIDE] u64
 
 enum ErrBits : uint32_t {
     E_POOL = 1, E_DENSE = 2, E_ECAP = 4, E_SHORT = 8, E_ITER = 16, E_COUNT = 32, E_XCAP = 64
@@ -81,7 +82,7 @@ struct DS {
     unsigned long long *ctr;
     uint32_t *err;
     uint4 *pool;
-    unsigned long long *pool_cur;
+    unsigned long long *pool_cur;    // sub-pool cursors (pool_alloc)
     unsigned long long pool_cap;
     uint32_t *dense;        // [dense_cap][NP]
     uint4 *dense_meta;      // {source, source e, known count, unused}

@@ -962,7 +962,7 @@ int step_one(swimsim *h, const swimsim_event *ev, size_t nev) {
         HIPCHK(h, hipEventRecord(e, h->s));
         h->round_ev.push_back(e);
     }
-    HIPCHK(h, hipMemsetAsync(h->d.pool_cur, 0, 8, h->s));
+    HIPCHK(h, hipMemsetAsync(h->d.pool_cur, 0, POOL_SHARDS * POOL_CUR_STRIDE * 8, h->s));
     // ---- E: events (the event list is the same on every shard; row events act on owned rows) ----
     std::vector<uint4> batch;
     bool topo_dirty = false;
@@ -1315,7 +1315,7 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
                                       ? cfg->message_pool_bytes / 16
                                       : std::min<uint64_t>(std::max<uint64_t>(4ull * h->NL * h->N, 1ull << 20), pool_bound);
     d.pool_cap = want_records;
-    if ((rc = dalloc(h, &d.pool, want_records, "message pool")) || (rc = dalloc(h, &d.pool_cur, 1, "pool cursor")))
+    if ((rc = dalloc(h, &d.pool, want_records, "message pool")) || (rc = dalloc(h, &d.pool_cur, POOL_SHARDS * POOL_CUR_STRIDE, "pool cursors")))
         return bail(rc);
     {
         // dense snapshots (full-sync payloads, deferred full-sync decisions, reverse-full-sync sources):
@@ -1538,7 +1538,7 @@ int swimsim_heal(swimsim_t *h, uint32_t o, int32_t *targets, size_t cap, size_t 
     if (!h || !own(h, o)) return SWIMSIM_EINVAL;
     if (h->G > 1) return h->fail(SWIMSIM_EINVAL, "sharded clusters heal through SWIMSIM_EV_HEAL events (collective)");
     std::vector<int32_t> ret;
-    HIPCHK(h, hipMemsetAsync(h->d.pool_cur, 0, 8, h->s));
+    HIPCHK(h, hipMemsetAsync(h->d.pool_cur, 0, POOL_SHARDS * POOL_CUR_STRIDE * 8, h->s));
     if (int rc = do_heal(h, o, &ret)) return rc;
     if (int rc = check_err(h)) return rc;
     if (targets)

@@ -258,15 +258,25 @@ __device__ void wave_bump(const DS &d, uint32_t ol, const MsgDesc &md) {
     __threadfence_block();
 }
 
+// The message pool is split into POOL_SHARDS sub-pools with a cursor each (own 128-B line): one returning
+// atomic per issuing wave on a single word saturates at ~88 per us (MI355X_MICROARCH.md row "dequeue"), which
+// serialised the 65,536 issues of a cascade round. A wave starts at the sub-pool of its wave id and moves on
+// to the next one only when its records do not fit, so the pool fails only when every sub-pool is full.
 __device__ __forceinline__ unsigned long long pool_alloc(const DS &d, uint32_t n) {
     unsigned long long off = 0;
-    if (lane_id() == 0 && n) off = atomicAdd(d.pool_cur, (unsigned long long)n);
-    off = bcast64(off);
-    if (off + n > d.pool_cap) {
-        if (lane_id() == 0) atomicOr(d.err, E_POOL);
-        return ~0ull;
+    if (lane_id() == 0 && n) {
+        const unsigned long long sub = d.pool_cap / POOL_SHARDS;
+        off = ~0ull;
+        for (uint32_t t = 0, s = wave_gid() % POOL_SHARDS; t < POOL_SHARDS; t++, s = (s + 1) % POOL_SHARDS) {
+            const unsigned long long old = atomicAdd(d.pool_cur + (size_t)s * POOL_CUR_STRIDE, (unsigned long long)n);
+            if (old + n <= sub) {
+                off = s * sub + old;
+                break;
+            }
+        }
+        if (off == ~0ull) atomicOr(d.err, E_POOL);
     }
-    return off;
+    return bcast64(off);
 }
 
 __device__ __forceinline__ uint32_t wscan_excl(uint32_t v, uint32_t &total) {
@@ -837,7 +847,7 @@ struct RecvArgs {
 // empty and checksums differ. A dirty receiver snapshots its row (the full-sync payload) and the
 // decision waits for one batched checksum of all snapshots after the last wave. Reverse full syncs
 // are queued afterwards in inbox order (k_build_jobs).
-__device__ void recv_one(const DS &d, const RecvArgs &a, uint32_t j, uint32_t sender, uint32_t resp_idx,
+__device__ __forceinline__ void recv_one(const DS &d, const RecvArgs &a, uint32_t j, uint32_t sender, uint32_t resp_idx,
                          uint32_t pair) {
     const uint32_t ol = j - d.lo;
     const uint32_t sender_row = sender;                             // descriptor index = global sender id
@@ -895,8 +905,7 @@ __global__ void k_recv(DS d, RecvArgs a) {
     for (uint32_t w = 0; w < n; w++) {
         const uint32_t pair = off + w;
         const uint32_t v = a.vals[pair];
-        if (a.phase == 0) recv_one(d, a, key, v, v, pair);
-        else recv_one(d, a, key, v / d.K, v, pair);
+        recv_one(d, a, key, a.phase == 0 ? v : v / d.K, v, pair);
     }
 }
 
