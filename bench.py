@@ -41,7 +41,8 @@ HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 VALU_PEAK_GINST = 256 * 4 * 2.4 / 2  # wave-instructions/ns: 1024 SIMDs, one wave64 VALU op per 2 cycles at 2.4 GHz
 KILL_ROUND = 10
 # kernel family (swimsim_kernel_times) -> kernel symbols in the rocprofv3 PMC summary
-FAMILY_KERNELS = {"checksum": ["swimdev::k_checksum<19, 11, 9, 0>", "swimdev::k_checksum_n16<19, 11, 9, 0>"],
+# (template arguments are ignored: every instantiation of the named kernel counts)
+FAMILY_KERNELS = {"checksum": ["swimdev::k_checksum", "swimdev::k_checksum2", "swimdev::k_checksum_n16"],
                   "recv_merge": ["swimdev::k_recv"], "issue": ["swimdev::k_issue"], "resp_merge": ["swimdev::k_resp"],
                   "timers": ["swimdev::k_timers"]}
 FAMILY_SYMBOL = {"checksum": "k_checksum", "recv_merge": "k_recv", "resp_merge": "k_resp", "issue": "k_issue",
@@ -58,7 +59,8 @@ def pmc_family(family, workload):
             t = json.load(f)
         if t.get("_workload") != workload:
             return None
-        ks = [t[k] for k in FAMILY_KERNELS.get(family, []) if k in t]
+        names = set(FAMILY_KERNELS.get(family, []))
+        ks = [v for k, v in t.items() if not k.startswith("_") and k.split("<")[0].strip() in names]
     except (OSError, KeyError, ValueError):
         return None
     n = sum(k["launches"] for k in ks)

@@ -107,6 +107,13 @@ int swimsim_set_row(swimsim_t *h, uint32_t observer, const uint8_t *status, cons
 int swimsim_make_change(swimsim_t *h, uint32_t observer, uint32_t member, int64_t inc_ms, int32_t status);
 /* disseminator.ClearChanges (disseminator.go:217-221) */
 int swimsim_clear_changes(swimsim_t *h, uint32_t observer);
+/* memberlist.AddJoinList (memberlist.go:398-406), called by the joiner for each joinResponse
+ * (join_sender.go:411): Update of the n changes (distinct members, as MembershipAsChanges lists them;
+ * source -1 = not a member, source/source_inc_ms may be NULL), then ClearChange of every applied change
+ * except the observer's own. One device launch. *applied = number of applied changes. */
+int swimsim_add_join_list(swimsim_t *h, uint32_t observer, const int32_t *member, const int32_t *status,
+                          const int64_t *inc_ms, const int32_t *source, const int64_t *source_inc_ms, size_t n,
+                          uint32_t *applied);
 int swimsim_set_live(swimsim_t *h, uint32_t member, int32_t live);
 int swimsim_set_partition(swimsim_t *h, uint32_t member, int32_t label);
 int swimsim_set_round(swimsim_t *h, uint32_t round);
@@ -230,6 +237,12 @@ typedef struct swimsim_host_transport {
     int (*bcast)(void *ctx, void *buf, size_t bytes, uint32_t root);
 } swimsim_host_transport;
 int swimsim_comm_attach_host(swimsim_t *h, uint32_t nranks, uint32_t rank, const swimsim_host_transport *t);
+/* diagnostics (transport conformance): one collective exchange of caller bytes through the handle's shard
+ * transport, exactly as the round's parcel exchange moves them (size exchange, then the segments). send holds
+ * the segments for shards 0..G-1 back to back (sbytes[G]); recv receives the segments from shards 0..G-1 back
+ * to back (rbytes[G] = their sizes). Every shard calls it. */
+int swimsim_debug_exchange(swimsim_t *h, const uint8_t *send, const uint64_t *sbytes, uint8_t *recv, size_t rcap,
+                           uint64_t *rbytes);
 
 #ifdef __cplusplus
 }

@@ -266,6 +266,7 @@ void or_set_partition(or_sim *s, uint32_t o, int32_t label) { s->o[o].part = lab
 void or_set_round(or_sim *s, uint32_t r) { s->round = r; }
 void or_set_maxp(or_sim *s, uint32_t o, int32_t maxp, int32_t pf) { s->o[o].maxp = maxp; s->o[o].pfactor = pf; }
 void or_clear_changes(or_sim *s, uint32_t o) { omap_clear(&s->o[o].dis); } /* disseminator.go:217-221 */
+void or_clear_change(or_sim *s, uint32_t o, uint32_t m) { omap_erase(&s->o[o].dis, (int32_t)m); } /* 229-233 */
 
 static int reach(const or_sim *s, uint32_t a, uint32_t b) {
     return s->o[a].live && s->o[b].live && s->o[a].part == s->o[b].part;
@@ -647,6 +648,18 @@ static or_change *issue_changes(or_sim *s, uint32_t j, int32_t *n_out) {
     qsort(v, (size_t)k, sizeof(or_change), cmp_change_member);
     *n_out = k;
     return v;
+}
+
+/* memberlist.AddJoinList (memberlist.go:398-406): Update, then ClearChange of every applied change whose
+ * address is not the node's own. Returns the number of applied changes. */
+int32_t or_add_join_list(or_sim *s, uint32_t j, const or_change *ch, int32_t n) {
+    if (n <= 0) return 0;
+    or_change *applied = (or_change *)malloc(sizeof(or_change) * (size_t)n);
+    const int32_t na = or_update(s, j, ch, n, applied, n);
+    for (int32_t i = 0; i < na; i++)
+        if ((uint32_t)applied[i].member != j) or_clear_change(s, j, (uint32_t)applied[i].member);
+    free(applied);
+    return na;
 }
 
 int32_t or_issue_as_sender(or_sim *s, uint32_t j, or_change *out, int32_t cap) {

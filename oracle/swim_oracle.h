@@ -82,6 +82,8 @@ void or_set_round(or_sim *s, uint32_t r);
 void or_set_maxp(or_sim *s, uint32_t o, int32_t maxp, int32_t p_factor);
 int or_make_change(or_sim *s, uint32_t o, uint32_t m, int64_t inc, int32_t status); /* #applied */
 void or_clear_changes(or_sim *s, uint32_t o);
+void or_clear_change(or_sim *s, uint32_t o, uint32_t m);   /* disseminator.ClearChange */
+int32_t or_add_join_list(or_sim *s, uint32_t j, const or_change *ch, int32_t n);  /* memberlist.AddJoinList */
 void or_recompute_pingable(or_sim *s, uint32_t o);
 
 /* --- round driver (docs/ROUND_SEMANTICS.md §4) --- */

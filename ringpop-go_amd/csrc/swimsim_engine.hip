@@ -287,6 +287,7 @@ struct swimsim {
     uint4 *evbuf = nullptr;
     uint32_t *ev_applied = nullptr;
     uint32_t evcap = 0;
+    uint4 *jl = nullptr;                          // join list records (swimsim_add_join_list), N of them
     unsigned long long *digest_buf = nullptr;
     uint32_t *hinfo = nullptr;  // pinned
     std::vector<void *> allocs;
@@ -1491,6 +1492,44 @@ int swimsim_clear_changes(swimsim_t *h, uint32_t o) {
     return SWIMSIM_OK;
 }
 
+int swimsim_add_join_list(swimsim_t *h, uint32_t o, const int32_t *member, const int32_t *status, const int64_t *inc_ms,
+                          const int32_t *source, const int64_t *source_inc_ms, size_t n, uint32_t *applied) {
+    if (!h || !own(h, o) || (n && (!member || !status || !inc_ms))) return SWIMSIM_EINVAL;
+    if (n > h->N) return h->fail(SWIMSIM_EINVAL, "join list of %zu changes for %u members", n, h->N);
+    std::vector<uint4> rec(n);
+    std::vector<uint8_t> seen(h->N, 0);
+    uint32_t emax = 0;
+    for (size_t i = 0; i < n; i++) {
+        const int32_t m = member[i], st = status[i];
+        if (m < 0 || (uint32_t)m >= h->N) return h->fail(SWIMSIM_EINVAL, "join list change %zu: member %d", i, m);
+        if (st < 0 || st > 4) return h->fail(SWIMSIM_EINVAL, "join list change %zu: status %d", i, st);
+        if (seen[m]++) return h->fail(SWIMSIM_EINVAL, "join list names member %d twice (MembershipAsChanges lists each once)", m);
+        uint32_t e = 0, se = 0, src = SRC_NONE;
+        if (int rc = to_e(h, inc_ms[i], &e)) return rc;
+        if (source && source[i] >= 0) {
+            if ((uint32_t)source[i] >= h->N) return h->fail(SWIMSIM_EINVAL, "join list change %zu: source %d", i, source[i]);
+            src = (uint32_t)source[i];
+            if (source_inc_ms)
+                if (int rc = to_e(h, source_inc_ms[i], &se)) return rc;
+        }
+        emax = std::max(emax, e);
+        rec[i] = make_uint4((uint32_t)m | ((uint32_t)st << 24), e, src, se);
+    }
+    if (int rc = ensure_ecap(h, std::max(emax, h->round) + 1)) return rc;
+    if (!h->jl)
+        if (int rc = dalloc(h, &h->jl, h->N, "join list")) return rc;
+    uint32_t napp = 0;
+    if (n) {
+        HIPCHK(h, hipMemcpyAsync(h->jl, rec.data(), n * sizeof(uint4), hipMemcpyHostToDevice, h->s));
+        hipLaunchKernelGGL(k_add_join_list, dim3(1), dim3(64), 0, h->s, h->d, o - h->lo, h->jl, (uint32_t)n, h->round,
+                           h->ev_applied);
+        HIPCHK(h, hipMemcpyAsync(&napp, h->ev_applied, 4, hipMemcpyDeviceToHost, h->s));
+    }
+    HIPCHK(h, hipStreamSynchronize(h->s));
+    if (applied) *applied = napp;
+    return check_err(h);
+}
+
 int swimsim_set_live(swimsim_t *h, uint32_t m, int32_t live) {
     if (!h || m >= h->N) return SWIMSIM_EINVAL;
     h->live[m] = live ? 1 : 0;
@@ -2039,6 +2078,52 @@ int swimsim_comm_attach_host(swimsim_t *h, uint32_t nranks, uint32_t rank, const
     port->t = *t;
     h->xp = std::move(port);
     return SWIMSIM_OK;
+}
+
+int swimsim_debug_exchange(swimsim_t *h, const uint8_t *send, const uint64_t *sbytes, uint8_t *recv, size_t rcap,
+                           uint64_t *rbytes) {
+    if (!h || !h->xp || !sbytes || !rbytes) return SWIMSIM_EINVAL;
+    const uint32_t G = h->xp->G;
+    std::vector<uint64_t> soff(G), sz(sbytes, sbytes + G), rsz(G), roff(G), rb(G);
+    uint64_t stot = 0, spacked = 0;
+    for (uint32_t p = 0; p < G; p++) {
+        soff[p] = stot;
+        stot += (sz[p] + 15) & ~15ull;
+        spacked += sz[p];
+    }
+    if (spacked && !send) return SWIMSIM_EINVAL;
+    if (int rc = h->xp->sizes(sz.data(), rsz.data(), 1)) return h->fail(rc, "debug exchange: sizes (%s)", h->xp->name());
+    uint64_t rtot = 0, rpacked = 0;
+    for (uint32_t p = 0; p < G; p++) {
+        roff[p] = rtot;
+        rtot += (rsz[p] + 15) & ~15ull;
+        rpacked += rsz[p];
+        rbytes[p] = rsz[p];
+    }
+    if (rpacked > rcap) return h->fail(SWIMSIM_ECAPACITY, "debug exchange: %llu bytes to receive, room for %zu",
+                                       (unsigned long long)rpacked, rcap);
+    uint8_t *ds = nullptr, *dr = nullptr;
+    HIPCHK(h, hipMalloc(&ds, std::max<uint64_t>(stot, 16)));
+    if (hipMalloc(&dr, std::max<uint64_t>(rtot, 16)) != hipSuccess) {
+        hipFree(ds);
+        return h->fail(SWIMSIM_ENOMEM, "debug exchange: receive buffer");
+    }
+    int rc = 0;
+    uint64_t at = 0;
+    for (uint32_t p = 0; p < G && !rc; p++) {
+        if (sz[p] && hipMemcpyAsync(ds + soff[p], send + at, sz[p], hipMemcpyHostToDevice, h->s) != hipSuccess) rc = SWIMSIM_EHIP;
+        at += sz[p];
+    }
+    if (!rc) rc = h->xp->data(ds, soff.data(), sz.data(), dr, roff.data(), rsz.data(), h->s);
+    at = 0;
+    for (uint32_t p = 0; p < G && !rc; p++) {
+        if (rsz[p] && hipMemcpyAsync(recv + at, dr + roff[p], rsz[p], hipMemcpyDeviceToHost, h->s) != hipSuccess) rc = SWIMSIM_EHIP;
+        at += rsz[p];
+    }
+    if (!rc && hipStreamSynchronize(h->s) != hipSuccess) rc = SWIMSIM_EHIP;
+    hipFree(ds);
+    hipFree(dr);
+    return rc ? h->fail(rc, "debug exchange: data (%s)", h->xp->name()) : SWIMSIM_OK;
 }
 
 int swimsim_shard_info(swimsim_t *h, uint32_t *nshards, uint32_t *rank, uint32_t *lo, uint32_t *hi,

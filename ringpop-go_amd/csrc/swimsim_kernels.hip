@@ -501,6 +501,48 @@ __global__ void k_clear_changes(DS d, uint32_t ol) {
     if (threadIdx.x == 0) d.dcnt[ol] = 0;
 }
 
+// memberlist.AddJoinList (memberlist.go:398-406) on observer row ol, one wave: Update of the join list
+// (records {member | status << 24, e, source, source e}, distinct members, as MembershipAsChanges makes them,
+// disseminator.go:107-123), then ClearChange (disseminator.go:229-233) of every applied change except the
+// observer's own, so the join list is not gossiped. A change applies exactly as in any other Update
+// (override rules, refute, timers, maxP, applied-change log); the entry it records is removed again right
+// away, which equals clearing after the whole Update because the members are distinct. applied_out = the
+// number of applied changes.
+__global__ void k_add_join_list(DS d, uint32_t ol, const uint4 *__restrict__ rec, uint32_t n, uint32_t r,
+                                uint32_t *applied_out) {
+    const uint32_t o = d.lo + ol;
+    const uint32_t *rowp = d.mw + (size_t)ol * d.NP;
+    MAcc acc;
+    for (uint32_t base = 0; base < n; base += 64 * MB) {
+        uint4 c[MB];
+        uint32_t cur[MB];
+#pragma unroll
+        for (int u = 0; u < MB; u++) {
+            const uint32_t i = base + u * 64 + lane_id();
+            c[u] = i < n ? rec[i] : make_uint4(0xFFFFFFFFu, 0, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < MB; u++) cur[u] = c[u].x != 0xFFFFFFFFu ? rowp[c[u].x & 0xFFFFFFu] : 0u;
+#pragma unroll
+        for (int u = 0; u < MB; u++) {
+            if (c[u].x == 0xFFFFFFFFu) continue;
+            const uint32_t m = c[u].x & 0xFFFFFFu;
+            const int before = acc.napp;
+            merge_change_w(d, ol, o, m, cur[u], c[u].x >> 24, c[u].y, c[u].z, c[u].w, r, r, acc);
+            if (acc.napp != before && m != o) {                    // ClearChange(member)
+                const size_t idx = (size_t)ol * d.NP + m;
+                d.dent[idx].x = DE_NONE;
+                atomicAnd(&d.dbit[(size_t)ol * d.NBIT + (m >> 5)], ~(1u << (m & 31)));
+                acc.ddc--;
+            }
+        }
+    }
+    const int napp = wsum(acc.napp);
+    __threadfence_block();
+    wave_finalize(d, ol, acc, 2);
+    if (lane_id() == 0) *applied_out = (uint32_t)napp;
+}
+
 // ---------------------------------------------------------------------------------------------
 // phase E: host events, applied in order by one thread (few per round)
 // ---------------------------------------------------------------------------------------------

@@ -114,6 +114,7 @@ def load_library(path: str = LIB_PATH):
         "swimsim_set_row": (C.c_int, [P, u32, P, P]),
         "swimsim_make_change": (C.c_int, [P, u32, u32, i64, i32]),
         "swimsim_clear_changes": (C.c_int, [P, u32]),
+        "swimsim_add_join_list": (C.c_int, [P, u32, P, P, P, P, P, sz, C.POINTER(u32)]),
         "swimsim_set_live": (C.c_int, [P, u32, i32]),
         "swimsim_set_partition": (C.c_int, [P, u32, i32]),
         "swimsim_set_round": (C.c_int, [P, u32]),
@@ -143,6 +144,7 @@ def load_library(path: str = LIB_PATH):
         "swimsim_shard_info": (C.c_int, [P, C.POINTER(u32), C.POINTER(u32), C.POINTER(u32), C.POINTER(u32),
                                          C.POINTER(u64), C.POINTER(u64)]),
         "swimsim_comm_attach_host": (C.c_int, [P, u32, u32, C.POINTER(HostTransport)]),
+        "swimsim_debug_exchange": (C.c_int, [P, P, P, P, sz, P]),
         "swimsim_watch": (C.c_int, [P, u32, i32]),
         "swimsim_applied_changes": (C.c_int, [P, u32, P, P, P, P, P, sz, C.POINTER(sz), C.POINTER(u32),
                                               C.POINTER(u32), C.POINTER(i32)]),
@@ -360,6 +362,23 @@ class Cluster:
     def clear_changes(self, o):
         self._chk(load_library().swimsim_clear_changes(self.h, o))
 
+    def add_join_list(self, o, member, status, inc, source=None, source_inc=None):
+        """memberlist.AddJoinList (memberlist.go:398-406) on observer o in one device launch
+        (swimsim_add_join_list): Update of the list, then ClearChange of every applied change except o's own.
+        Columns as swimsim.wire.changes_to_arrays makes them; returns the number of applied changes."""
+        cols = [np.ascontiguousarray(member, np.int32), np.ascontiguousarray(status, np.int32),
+                np.ascontiguousarray(inc, np.int64)]
+        n = len(cols[0])
+        if any(len(c) != n for c in cols):
+            raise ValueError("add_join_list: columns of different lengths")
+        src = None if source is None else np.ascontiguousarray(source, np.int32)
+        sinc = None if source_inc is None else np.ascontiguousarray(source_inc, np.int64)
+        ptr = lambda a: None if a is None else a.ctypes.data
+        applied = C.c_uint32(0)
+        self._chk(load_library().swimsim_add_join_list(self.h, o, ptr(cols[0]), ptr(cols[1]), ptr(cols[2]), ptr(src),
+                                                       ptr(sinc), n, C.byref(applied)))
+        return int(applied.value)
+
     def set_live(self, m, live):
         self._chk(load_library().swimsim_set_live(self.h, m, int(live)))
 
@@ -484,6 +503,24 @@ class Cluster:
 
     def node(self, o):
         return Node(self, o)
+
+    def debug_exchange(self, segments):
+        """diagnostics (transport conformance): send segments[p] (bytes) to shard p through this handle's shard
+        transport, as a round's parcel exchange moves them; returns the segments received from each shard.
+        Collective: every shard calls it."""
+        G = len(segments)
+        sb = np.array([len(x) for x in segments], np.uint64)
+        send = np.frombuffer(b"".join(segments) or b"\0", np.uint8).copy()
+        cap = 1 << 22
+        recv = np.empty(cap, np.uint8)
+        rb = np.zeros(G, np.uint64)
+        self._chk(load_library().swimsim_debug_exchange(self.h, send.ctypes.data, sb.ctypes.data, recv.ctypes.data, cap,
+                                                        rb.ctypes.data))
+        out, at = [], 0
+        for k in rb.tolist():
+            out.append(recv[at:at + int(k)].tobytes())
+            at += int(k)
+        return out
 
 
 @dataclass
@@ -620,6 +657,9 @@ class ShardedCluster:
 
     def clear_changes(self, o):
         self.owner(o).clear_changes(o)
+
+    def add_join_list(self, o, *cols, **kw):
+        return self.owner(o).add_join_list(o, *cols, **kw)
 
     def set_live(self, m, live):
         self.live[m] = bool(live)

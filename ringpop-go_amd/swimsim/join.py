@@ -41,14 +41,23 @@ def now_ms(cluster) -> int:
 
 
 def join(cluster, joiner: int, coordinators: Iterable[int], app: str = "ringpop") -> dict:
-    """Join member `joiner` through `coordinators`; returns {"applied", "responses", "incarnation"}."""
+    """Join member `joiner` through `coordinators`; returns {"applied", "responses", "incarnation"}.
+
+    On a cluster with ``add_join_list`` (the engine) the joiner runs the reference's order: Reincarnate, then
+    one AddJoinList device launch per joinResponse. Elsewhere (the oracle view) the merges are replayed one
+    ``make_change`` at a time and the Reincarnate comes last (see the module docstring: both orders leave the
+    same state for a fresh joiner)."""
     coordinators = [int(c) for c in coordinators]
     if not coordinators:
         raise ValueError("join needs at least one coordinator (join_sender.go: no hosts to join)")
     if joiner in coordinators:
         # join_handler.go:36-42: a node may not join itself
         raise ValueError(f"member {joiner} tried to join the cluster by joining itself")
+    device = hasattr(cluster, "add_join_list")
     applied = 0
+    inc = now_ms(cluster)
+    if device:
+        cluster.make_change(joiner, joiner, inc, 0)     # Reincarnate: MakeAlive(self, now)
     req = W.JoinRequest(app, address_of(joiner), now_ms(cluster), 1_000_000_000)
     for c in coordinators:
         body = W.join_response(cluster, c, W.JoinRequest.from_json(req.to_json()).app).to_json()
@@ -56,13 +65,17 @@ def join(cluster, joiner: int, coordinators: Iterable[int], app: str = "ringpop"
         if resp.app != app:
             raise ValueError(f"coordinator {c} belongs to app {resp.app!r}, not {app!r}")
         cols = W.changes_to_arrays(resp.membership or [], cluster.n)
-        for m, st, inc in zip(cols["member"].tolist(), cols["status"].tolist(), cols["incarnation"].tolist()):
+        if device:
+            applied += cluster.add_join_list(joiner, cols["member"], cols["status"], cols["incarnation"],
+                                             cols["source"], cols["source_incarnation"])
+            continue
+        for m, st, ic in zip(cols["member"].tolist(), cols["status"].tolist(), cols["incarnation"].tolist()):
             if m == joiner or st == UNKNOWN:
                 continue
-            applied += int(cluster.make_change(joiner, m, inc, st) or 0)
-    cluster.clear_changes(joiner)                       # AddJoinList: ClearChange of every applied change
-    inc = now_ms(cluster)
-    cluster.make_change(joiner, joiner, inc, 0)         # Reincarnate: MakeAlive(self, now)
+            applied += int(cluster.make_change(joiner, m, ic, st) or 0)
+    if not device:
+        cluster.clear_changes(joiner)                   # AddJoinList: ClearChange of every applied change
+        cluster.make_change(joiner, joiner, inc, 0)     # Reincarnate: MakeAlive(self, now)
     cluster.set_live(joiner, 1)
     return {"applied": applied, "responses": len(coordinators), "incarnation": inc}
 

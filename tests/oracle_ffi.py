@@ -97,6 +97,8 @@ def lib():
             "or_non_local_override": (i32, [i64, i32, i64, i32]),
             "or_local_override": (i32, [i32, i64, i64, i32]),
             "or_update": (i32, [P, u32, C.POINTER(OrChange), i32, C.POINTER(OrChange), i32]),
+            "or_add_join_list": (i32, [P, u32, C.POINTER(OrChange), i32]),
+            "or_clear_change": (None, [P, u32, u32]),
             "or_issue_as_sender": (i32, [P, u32, C.POINTER(OrChange), i32]),
             "or_issue_as_receiver": (i32, [P, u32, i32, i64, u32, C.POINTER(OrChange), i32, C.POINTER(i32)]),
             "or_bump": (None, [P, u32, C.POINTER(OrChange), i32]),
@@ -328,6 +330,10 @@ class OracleSim:
         out = (OrChange * max(1, len(changes)))()
         k = lib().or_update(self.h, j, arr, len(changes), out, len(changes))
         return _unpack(out, k)
+
+    def add_join_list_changes(self, j, changes):
+        """memberlist.AddJoinList of (member, status, inc, source, source_inc) tuples; #applied"""
+        return lib().or_add_join_list(self.h, j, _changes(changes), len(changes))
 
     def issue_as_sender(self, j):
         out = (OrChange * self.n)()

@@ -111,3 +111,67 @@ def test_gpu_sharded_bootstrap_matches_single(nshards):
         assert one.digest() == sh.digest(), f"round {r}: state digests differ"
 
     _run([one, sh], n, 1 + n * every + 30, every, check)
+
+
+def _join_list_case(n, seed):
+    """a 3-row scenario: observer 1 knows a few members; the join list names most members with mixed statuses,
+    unseen tombstones (Apply refuses to create them, memberlist.go:424-426), stale and newer incarnations, and
+    observer 1 itself as suspect at its own incarnation (a refute, memberlist.go:337-354)"""
+    rng = np.random.default_rng(seed)
+    t0, per = swimsim.T0_MS, 200
+    known = {m: (int(rng.integers(0, 3)), t0 + per * int(rng.integers(0, 4))) for m in range(0, n, 3)}
+    known[1] = (swimsim.ALIVE, t0 + per * 5)
+    lst = []
+    for m in rng.permutation(n).tolist():
+        if rng.random() < 0.15:
+            continue
+        st = int(rng.choice([0, 1, 2, 3, 4], p=[0.5, 0.15, 0.15, 0.05, 0.15]))
+        lst.append((m, st, t0 + per * int(rng.integers(0, 6)), 0, t0 + per * 2))
+    lst = [c for c in lst if c[0] != 1] + [(1, swimsim.SUSPECT, t0 + per * 5, 0, t0 + per * 2)]
+    return known, lst
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_add_join_list_on_oracle_clears_all_but_own(seed):
+    n = 64
+    known, lst = _join_list_case(n, seed)
+    ora = OracleSim(n, init="self")
+    ora.set_round(6)
+    for m, (st, inc) in known.items():
+        ora.set_member(1, m, st, inc)
+    ora.make_change(1, 1, swimsim.T0_MS + 6 * 200, swimsim.ALIVE)       # Reincarnate
+    k = ora.add_join_list_changes(1, lst)
+    assert k > 0
+    assert list(ora.dis_entries(1)) == [1], "only the node's own change stays in the disseminator"
+    st, _ = ora.row(1)
+    unseen_tomb = [m for (m, s, *_r) in lst if s == swimsim.TOMBSTONE and m not in known]
+    assert all(st[m] == swimsim.UNKNOWN for m in unseen_tomb)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_gpu_add_join_list_matches_oracle(seed):
+    """swimsim_add_join_list (one device launch) against the oracle's AddJoinList restatement: the applied count,
+    the row, the dissemination buffer and the timer table (per-row digests), the applied-change event"""
+    n = 64
+    known, lst = _join_list_case(n, seed)
+    eng = swimsim.Cluster(n, device=0, init="self")
+    ora = OracleSim(n, init="self")
+    for c in (eng, ora):
+        c.set_round(6)
+        for m, (st, inc) in known.items():
+            c.set_member(1, m, st, inc)
+    eng.watch(1, True)
+    ora.watch(1, True)
+    for c in (eng, ora):
+        c.make_change(1, 1, swimsim.T0_MS + 6 * 200, swimsim.ALIVE)
+    cols = np.array(lst, dtype=np.int64)
+    k_eng = eng.add_join_list(1, cols[:, 0], cols[:, 1], cols[:, 2], cols[:, 3], cols[:, 4])
+    k_ora = ora.add_join_list_changes(1, lst)
+    assert k_eng == k_ora > 0
+    assert eng.digest() == ora.digest()
+    assert (eng.checksums() == ora.checksums()).all()
+    assert eng.changes(1).keys() == {1}
+    ns = eng.node_stats(1)
+    assert (ns["pingable"], ns["maxp"], ns["changes"]) == (ora.num_pingable(1), ora.maxp(1), 1)
+    assert eng.applied_changes(1) == ora.drain_applied(1)          # MemberlistChangesAppliedEvent
