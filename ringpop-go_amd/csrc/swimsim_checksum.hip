@@ -705,12 +705,14 @@ void launch_cs_w(const DS &d, const uint32_t *list, const uint32_t *count, uint3
 }
 
 #include "swimsim_checksum2.hip"
+#include "swimsim_checksum3.hip"
 
 // up to CS_NARROW_ROWS rows (measured crossover) the launch is latency-bound: k_checksum_n16 (16 rows per
-// workgroup, ~40 % shorter); above, the 64-row throughput kernel k_checksum2 (k_checksum, its 4-wave
-// predecessor, stays selectable for measurements: SWIMSIM_CS_KERNEL=1)
+// workgroup, ~40 % shorter); above, the 64-row throughput kernel k_checksum3 (17.8 vs 19.4-20.1 ms for its
+// predecessor k_checksum2 at 65,536 rows, tools/cs_bench.py; k_checksum2 and the 4-wave k_checksum stay
+// selectable for measurements: SWIMSIM_CS_KERNEL=2 / 1)
 constexpr uint32_t CS_NARROW_ROWS = 12288;
-static int g_cs_kernel = 2;
+static int g_cs_kernel = 3;
 static uint32_t g_cs_narrow_rows = CS_NARROW_ROWS;     // SWIMSIM_CS_NARROW_ROWS (tests: 0 = wide kernel only)
 
 void launch_checksum(const DS &d, const uint32_t *list, const uint32_t *count, uint32_t maxn, uint32_t nrows,
@@ -719,9 +721,13 @@ void launch_checksum(const DS &d, const uint32_t *list, const uint32_t *count, u
     const uint32_t grid = (n + CS_ROWS - 1) / CS_ROWS;
     if (grid == 0) return;
     const uint32_t ngrid = n <= g_cs_narrow_rows ? (n + CN_ROWS - 1) / CN_ROWS : 0u;
-    if (g_cs_kernel == 2 && ngrid == 0) {
+    if (g_cs_kernel >= 2 && ngrid == 0) {
         switch (d.W) {
-#define CS_CASE(Wv) case Wv: launch_cs2_w<Wv>(d, list, count, grid, s); break;
+#define CS_CASE(Wv)                                                                         \
+    case Wv:                                                                                \
+        if (g_cs_kernel == 3) launch_cs3_w<Wv>(d, list, count, grid, s);                   \
+        else launch_cs2_w<Wv>(d, list, count, grid, s);                                    \
+        break;
             CS_CASE(13) CS_CASE(14) CS_CASE(15) CS_CASE(16) CS_CASE(17) CS_CASE(18) CS_CASE(19) CS_CASE(20)
 #undef CS_CASE
         default: break;
@@ -748,6 +754,12 @@ void launch_checksum_mode(const DS &d, const uint32_t *list, const uint32_t *cou
     if (grid == 0 || d.W != 19) return;
     const uint32_t ngrid = (maxn + CN_ROWS - 1) / CN_ROWS;
     if (mode == 20) launch_cs2_w<19>(d, list, count, grid, s);
+    else if (mode == 21) launch_cs3_w<19>(d, list, count, grid, s);
+    else if (mode == 22) launch_cs3_w<19, 1>(d, list, count, grid, s);
+    else if (mode == 23) launch_cs3_w<19, 2>(d, list, count, grid, s);
+    else if (mode == 24) launch_cs3_w<19, 3>(d, list, count, grid, s);
+    else if (mode == 25) launch_cs3_w<19, 4>(d, list, count, grid, s);
+    else if (mode == 26) launch_cs3_w<19, 5>(d, list, count, grid, s);
     else if (mode == 6) launch_cs_w<19, 0>(d, list, count, grid, s, nullptr, 0, ngrid);
     else if (mode == 7) launch_cs_w<19, 7>(d, list, count, grid, s, nullptr, 0, ngrid);
     else if (mode == 8) launch_cs_w<19, 8>(d, list, count, grid, s, nullptr, 0, ngrid);

@@ -2114,6 +2114,9 @@ int swimsim_debug_exchange(swimsim_t *h, const uint8_t *send, const uint64_t *sb
         if (sz[p] && hipMemcpyAsync(ds + soff[p], send + at, sz[p], hipMemcpyHostToDevice, h->s) != hipSuccess) rc = SWIMSIM_EHIP;
         at += sz[p];
     }
+    // the staged segments must be complete before any peer reads them (LocalPort copies from the peers' buffers
+    // on its own stream), as xchg() synchronises before its exchange
+    if (!rc && hipStreamSynchronize(h->s) != hipSuccess) rc = SWIMSIM_EHIP;
     if (!rc) rc = h->xp->data(ds, soff.data(), sz.data(), dr, roff.data(), rsz.data(), h->s);
     at = 0;
     for (uint32_t p = 0; p < G && !rc; p++) {
