@@ -60,6 +60,9 @@ struct Transport {
     // host bytes of shard root to every shard
     virtual int bcast(void *buf, size_t bytes, uint32_t root) = 0;
     virtual const char *name() const = 0;
+    // true: data() moves the segments in order on the caller's stream (no host synchronisation before the
+    // segments are read, none after they land: later kernels on the stream are ordered after the transfer)
+    virtual bool stream_ordered() const { return false; }
 };
 
 // shards of one process (threads): device-to-device (peer) copies between the shards' buffers
@@ -137,6 +140,7 @@ struct RcclPort : Transport {
     uint64_t *dsz = nullptr;      // device staging for sizes / broadcasts
     size_t dsz_cap = 0;
     const char *name() const override { return "rccl"; }
+    bool stream_ordered() const override { return true; }
     ~RcclPort() override {
         if (comm) ncclCommDestroy(comm);
         if (dsz) hipFree(dsz);
@@ -168,8 +172,7 @@ struct RcclPort : Transport {
             if (sbytes[p]) ncclSend(sbuf + soff[p], sbytes[p], ncclUint8, (int)p, comm, s);
             if (rbytes[p]) ncclRecv(rbuf + roff[p], rbytes[p], ncclUint8, (int)p, comm, s);
         }
-        if (ncclGroupEnd() != ncclSuccess) return SWIMSIM_EHIP;
-        return hipStreamSynchronize(s) == hipSuccess ? 0 : SWIMSIM_EHIP;
+        return ncclGroupEnd() == ncclSuccess ? 0 : SWIMSIM_EHIP;     // stream-ordered: the unpack follows on s
     }
     int bcast(void *buf, size_t bytes, uint32_t root) override {
         if (int rc = stage(bytes)) return rc;
@@ -573,7 +576,9 @@ int xchg(swimsim *h) {
     if (nitems)
         hipLaunchKernelGGL(k_x_pack, dim3(blocks_for_waves(nitems)), dim3(SWIM_WAVE_BLOCK), 0, h->s, h->d, x, h->xitems, h->xcnt,
                            h->xcap, h->sbuf, h->xseg, h->xtcur, h->xdcur);
-    HIPCHK(h, hipStreamSynchronize(h->s));
+    // the packed segments are read by the peers (local copies) or staged through the host: complete them first;
+    // RCCL sends them in stream order after the pack
+    if (!h->xp->stream_ordered()) HIPCHK(h, hipStreamSynchronize(h->s));
     if (int rc = h->xp->sizes(sendsz.data(), recvsz.data(), 2)) return h->fail(rc, "shard size exchange failed (%s)", h->xp->name());
     std::vector<uint64_t> roff(G), rbytes(G);
     std::vector<ulonglong2> srcs(G);
