@@ -107,7 +107,22 @@ struct DS {
     uint32_t *wslot;          // [NL] watched row -> slot of wlog, SRC_NONE if unwatched; nullptr: no row watched
     uint4 *wlog;              // [slots][NP] per member, the last change applied since the last drain:
                               // {member word, source, source e, 1}; .w = 0: none
+    // hot columns: compact copies of the row words and dissemination cells of the members that
+    // sit in dissemination buffers, so that issue, merge and bump gather from a few KB per row instead of one
+    // 64-B sector per member. hmw[ol][k] == mw[ol][hlist[k]] and hde[ol][k] == dent[ol][hlist[k]] for every
+    // slot k < hot_cnt[0]: every write of a hot member's word or cell goes to both copies, so reads may use
+    // either. hidx = nullptr: off.
+    uint32_t *hidx;           // [N] member -> hot slot, SRC_NONE if not hot
+    uint32_t *hlist;          // [HP] slot -> member
+    uint32_t *hmw;            // [NL][HP]
+    uint2 *hde;               // [NL][HP]
+    uint32_t *hotnew;         // [NBIT] members that got a new dissemination entry while not hot
+    uint32_t *hot_cnt;        // {slots in use, slots filled}
+    uint32_t HP;              // hot slots per row
 };
+
+// hot slot of member m, SRC_NONE when m has none (or hot columns are off)
+__device__ __forceinline__ uint32_t hot_slot(const DS &d, uint32_t m) { return d.hidx ? d.hidx[m] : SRC_NONE; }
 
 __host__ __device__ inline bool is_pingable(uint32_t st) { return st <= ST_SUSPECT; }
 

@@ -631,6 +631,22 @@ void hash_rows(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t m
     launch_checksum(h->d, list, cnt, maxn, nrows, st ? st : h->s);
 }
 
+// hot columns: forget every hot member (raw row writes bypass the copies)
+void hot_reset(swimsim *h) {
+    if (!h->d.hidx) return;
+    hipMemsetAsync(h->d.hidx, 0xFF, (size_t)h->N * 4, h->s);
+    hipMemsetAsync(h->d.hotnew, 0, (size_t)h->d.NBIT * 4, h->s);
+    hipMemsetAsync(h->d.hot_cnt, 0, 8, h->s);
+}
+
+// hot columns, start of phase I: members that got a first dissemination entry since the last call take free
+// slots, and the new slots' columns are copied from the rows
+void hot_update(swimsim *h) {
+    if (!h->d.hidx) return;
+    hipLaunchKernelGGL(k_hot_extend, dim3(1), dim3(1024), 0, h->s, h->d);
+    hipLaunchKernelGGL(k_hot_fill, dim3(blocks_for_waves(h->NL)), dim3(SWIM_WAVE_BLOCK), 0, h->s, h->d);
+}
+
 // order the main stream after the side-stream checksums of the previous phase C; from here on every
 // row's cs[] is current and no row refers to a side slot
 int sync_side(swimsim *h) {
@@ -758,9 +774,12 @@ int resolve_deferred(swimsim *h, int phase, MsgDesc *rdesc, uint32_t maxn) {
         HIPCHK(h, hipMemcpyAsync(hc, h->cnt, 4, hipMemcpyDeviceToHost, h->s));
         HIPCHK(h, hipMemcpyAsync(hc + 1, h->cnt + 1, 4, hipMemcpyDeviceToHost, h->s));
         HIPCHK(h, hipStreamSynchronize(h->s));
+        // the list holds main-stream snapshot slots only (k_defer_ids), so their hash needs nothing from the side
+        // stream and runs beside the previous phase C's side-stream launch (both are latency-bound launches of
+        // few rows); k_recv_finish then compares with side-stream checksums, so it waits for the side stream
+        hash_rows(h, h->list, h->cnt, maxlist, *hc);
         if (hc[1])
             if (int rc = sync_side(h)) return rc;
-        hash_rows(h, h->list, h->cnt, maxlist, *hc);
     }
     if (remote) {
         hipLaunchKernelGGL(k_x_csresp, dim3(blocks_for_threads(h->keycap)), dim3(256), 0, h->s, h->d, h->csreq,
@@ -1019,6 +1038,7 @@ int step_one(swimsim *h, const swimsim_event *ev, size_t nev) {
     uint32_t ninbox = h->NL;
     if (int rc = bound_lazy_snapshots(h, 1)) return rc;
     HIPCHK(h, hipMemsetAsync(h->d.dense_cur, 0, 4, h->s));         // dense snapshots live from here through R
+    hot_update(h);
     {
         {
             Scope sc(h, F_ISSUE);
@@ -1294,6 +1314,24 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
         (rc = dalloc(h, &d.cpslot, h->NL, "cpslot")))
         return bail(rc);
     hipMemset(d.cpslot, 0xFF, (size_t)h->NL * 4);
+    {
+        // hot columns: 2,048 slots per row (1.6 GB at 65,536 rows); SWIMSIM_HOT_SLOTS=0 turns
+        // them off (results are the same either way: the columns are copies)
+        uint32_t hp = std::min<uint32_t>(2048u, h->NP);
+        if (const char *v = getenv("SWIMSIM_HOT_SLOTS")) hp = std::min<uint32_t>((uint32_t)strtoul(v, nullptr, 10), h->NP);
+        hp = (hp + 63) & ~63u;
+        d.hidx = nullptr; d.hlist = nullptr; d.hmw = nullptr; d.hde = nullptr; d.hotnew = nullptr; d.hot_cnt = nullptr;
+        d.HP = 0;
+        if (hp) {
+            if ((rc = dalloc(h, &d.hidx, h->N, "hot index")) || (rc = dalloc(h, &d.hlist, hp, "hot list")) ||
+                (rc = dalloc(h, &d.hmw, (size_t)h->NL * hp, "hot member words")) ||
+                (rc = dalloc(h, &d.hde, (size_t)h->NL * hp, "hot dissemination cells")) ||
+                (rc = dalloc(h, &d.hotnew, d.NBIT, "hot candidates")) || (rc = dalloc(h, &d.hot_cnt, 2, "hot count")))
+                return bail(rc);
+            d.HP = hp;
+            hot_reset(h);
+        }
+    }
     // address words
     {
         std::vector<uint32_t> aw((size_t)h->N * 6, 0u);
@@ -1438,6 +1476,7 @@ int swimsim_destroy(swimsim_t *h) {
 }
 
 static int init_rows(swimsim_t *h, int mode) {
+    hot_reset(h);
     hipLaunchKernelGGL(k_init_rows, dim3(blocks_for_waves(h->NL)), dim3(SWIM_WAVE_BLOCK), 0, h->s, h->d, mode, 0u);
     if (int rc = checksum_dirty(h, 0)) return rc;
     return check_err(h);
@@ -1454,6 +1493,7 @@ int swimsim_set_member(swimsim_t *h, uint32_t o, uint32_t m, int32_t status, int
     if (status != SWIMSIM_UNKNOWN)
         if (int rc = to_e(h, inc_ms, &e)) return rc;
     const uint32_t w = (e << 3) | (uint32_t)status;
+    hot_reset(h);
     HIPCHK(h, hipMemcpyAsync(h->d.mw + (size_t)(o - h->lo) * h->NP + m, &w, 4, hipMemcpyHostToDevice, h->s));
     hipLaunchKernelGGL(k_recount, dim3(1), dim3(64), 0, h->s, h->d, o - h->lo);
     HIPCHK(h, hipStreamSynchronize(h->s));
@@ -1471,6 +1511,7 @@ int swimsim_set_row(swimsim_t *h, uint32_t o, const uint8_t *status, const int64
         if (int rc = to_e(h, inc_ms[m], &e)) return rc;
         row[m] = (e << 3) | (uint32_t)s;
     }
+    hot_reset(h);
     HIPCHK(h, hipMemcpyAsync(h->d.mw + (size_t)(o - h->lo) * h->NP, row.data(), (size_t)h->N * 4,
                              hipMemcpyHostToDevice, h->s));
     hipLaunchKernelGGL(k_recount, dim3(1), dim3(64), 0, h->s, h->d, o - h->lo);

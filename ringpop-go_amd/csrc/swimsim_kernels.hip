@@ -92,7 +92,10 @@ __device__ __forceinline__ void merge_change_w(const DS &d, uint32_t ol, uint32_
         return;
     }
     const uint32_t nw_ = (ne << 3) | nst;
+    const uint32_t hk = hot_slot(d, m);
+    const size_t hx = (size_t)ol * d.HP + hk;
     d.mw[idx] = nw_;
+    if (hk != SRC_NONE) d.hmw[hx] = nw_;
     track_len(d, ol, m, cur, nw_, acc);
     acc.dfp += fpmix(m, (ne << 3) | nst) - fpmix(m, cur);
     if (m != o) acc.dping += (int)is_pingable(nst) - (int)is_pingable(cur_st);
@@ -100,8 +103,15 @@ __device__ __forceinline__ void merge_change_w(const DS &d, uint32_t ol, uint32_
     if (de_p(d.dent[idx].x) == DP_NONE) {
         acc.ddc++;
         atomicOr(&d.dbit[(size_t)ol * d.NBIT + (m >> 5)], 1u << (m & 31));
+        if (hk == SRC_NONE && d.hidx) {                           // a candidate for the next round's hot columns
+            uint32_t *hw = d.hotnew + (m >> 5);
+            if (!(__hip_atomic_load(hw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & (1u << (m & 31))))
+                atomicOr(hw, 1u << (m & 31));
+        }
     }
-    d.dent[idx] = make_uint2(de_x(nsrc, 0), nsinc);
+    const uint2 cell = make_uint2(de_x(nsrc, 0), nsinc);
+    d.dent[idx] = cell;
+    if (hk != SRC_NONE) d.hde[hx] = cell;
     if (d.wslot) {                                                 // watched row: MemberlistChangesAppliedEvent
         const uint32_t ws = d.wslot[ol];                           // (memberlist.go:378-383)
         if (ws != SRC_NONE) d.wlog[(size_t)ws * d.NP + m] = make_uint4(nw_, nsrc, nsinc, 1u);
@@ -199,18 +209,22 @@ __device__ void wave_merge_msg(const DS &d, uint32_t ol, uint32_t o, const MsgDe
                                int cset = 0) {
     MAcc acc;
     const uint32_t *rowp = d.mw + (size_t)ol * d.NP;
+    const uint32_t *hrow = d.hmw + (size_t)ol * d.HP;
     if (md.kind == 0) {
         const unsigned long long off = ((unsigned long long)md.off_hi << 32) | md.off_lo;
         for (uint32_t base = 0; base < md.len; base += 64 * MB) {
             uint4 rec[MB];
-            uint32_t cur[MB];
+            uint32_t cur[MB], hk[MB];
 #pragma unroll
             for (int u = 0; u < MB; u++) {
                 const uint32_t i = base + u * 64 + lane_id();
                 rec[u] = i < md.len ? d.pool[off + i] : make_uint4(0xFFFFFFFFu, 0, 0, 0);
             }
 #pragma unroll
-            for (int u = 0; u < MB; u++) cur[u] = rec[u].x != 0xFFFFFFFFu ? rowp[rec[u].x & 0xFFFFFFu] : 0u;
+            for (int u = 0; u < MB; u++) hk[u] = rec[u].x != 0xFFFFFFFFu ? hot_slot(d, rec[u].x & 0xFFFFFFu) : SRC_NONE;
+#pragma unroll
+            for (int u = 0; u < MB; u++)
+                cur[u] = rec[u].x == 0xFFFFFFFFu ? 0u : hk[u] != SRC_NONE ? hrow[hk[u]] : rowp[rec[u].x & 0xFFFFFFu];
 #pragma unroll
             for (int u = 0; u < MB; u++)
                 if (rec[u].x != 0xFFFFFFFFu)
@@ -230,27 +244,34 @@ __device__ void wave_bump(const DS &d, uint32_t ol, const MsgDesc &md) {
     const unsigned long long off = ((unsigned long long)md.off_hi << 32) | md.off_lo;
     const int maxp = d.maxp[ol];
     uint32_t *dx = (uint32_t *)(d.dent + (size_t)ol * d.NP);       // word 0 of each entry, stride 2
+    uint32_t *hx = (uint32_t *)(d.hde + (size_t)ol * d.HP);        // the same in the hot columns
     int del = 0;
     for (uint32_t base = 0; base < md.len; base += 64 * MB) {
-        uint32_t m[MB], x[MB];
+        uint32_t m[MB], x[MB], hk[MB];
 #pragma unroll
         for (int u = 0; u < MB; u++) {
             const uint32_t i = base + u * 64 + lane_id();
             m[u] = i < md.len ? (d.pool[off + i].x & 0xFFFFFFu) : 0xFFFFFFFFu;
         }
 #pragma unroll
-        for (int u = 0; u < MB; u++) x[u] = m[u] != 0xFFFFFFFFu ? dx[(size_t)m[u] * 2] : DE_NONE;
+        for (int u = 0; u < MB; u++) hk[u] = m[u] != 0xFFFFFFFFu ? hot_slot(d, m[u]) : SRC_NONE;
+#pragma unroll
+        for (int u = 0; u < MB; u++)
+            x[u] = m[u] == 0xFFFFFFFFu ? DE_NONE : hk[u] != SRC_NONE ? hx[(size_t)hk[u] * 2] : dx[(size_t)m[u] * 2];
 #pragma unroll
         for (int u = 0; u < MB; u++) {
             const uint32_t p = de_p(x[u]);
             if (p == DP_NONE) continue;
+            uint32_t nx;
             if ((int)(p + 1) >= maxp) {
-                dx[(size_t)m[u] * 2] = x[u] | 0xFF000000u;
+                nx = x[u] | 0xFF000000u;
                 atomicAnd(&d.dbit[(size_t)ol * d.NBIT + (m[u] >> 5)], ~(1u << (m[u] & 31)));
                 del++;
             } else {
-                dx[(size_t)m[u] * 2] = x[u] + (1u << 24);
+                nx = x[u] + (1u << 24);
             }
+            dx[(size_t)m[u] * 2] = nx;
+            if (hk[u] != SRC_NONE) hx[(size_t)hk[u] * 2] = nx;
         }
     }
     del = wsum(del);
@@ -305,7 +326,7 @@ __device__ uint32_t wave_issue_t(const DS &d, uint32_t ol, uint32_t sender, uint
     const unsigned long long off = pool_alloc(d, cnt);
     if (off == ~0ull) return 0;
     const int maxp = RECV ? d.maxp[ol] : 0;
-    const size_t rb = (size_t)ol * d.NP;
+    const size_t rb = (size_t)ol * d.NP, hb = (size_t)ol * d.HP;
     uint32_t *bits = d.dbit + (size_t)ol * d.NBIT;
     uint32_t pos = 0;
     int del = 0;
@@ -332,11 +353,21 @@ __device__ uint32_t wave_issue_t(const DS &d, uint32_t ol, uint32_t sender, uint
                 else m[k] = 0xFFFFFFFFu;
             }
             uint2 ce[MB];                                        // the 8-byte entry and the member word
-            uint32_t wv[MB];
+            uint32_t wv[MB], hk[MB];
+#pragma unroll
+            for (int k = 0; k < MB; k++) hk[k] = m[k] != 0xFFFFFFFFu ? hot_slot(d, m[k]) : SRC_NONE;
 #pragma unroll
             for (int k = 0; k < MB; k++) {
-                ce[k] = m[k] != 0xFFFFFFFFu ? d.dent[rb + m[k]] : make_uint2(DE_NONE, 0);
-                wv[k] = m[k] != 0xFFFFFFFFu ? d.mw[rb + m[k]] : 0u;
+                if (m[k] == 0xFFFFFFFFu) {
+                    ce[k] = make_uint2(DE_NONE, 0);
+                    wv[k] = 0u;
+                } else if (hk[k] != SRC_NONE) {
+                    ce[k] = d.hde[hb + hk[k]];
+                    wv[k] = d.hmw[hb + hk[k]];
+                } else {
+                    ce[k] = d.dent[rb + m[k]];
+                    wv[k] = d.mw[rb + m[k]];
+                }
             }
             uint32_t p[MB];
             uint2 sr[MB];
@@ -361,15 +392,17 @@ __device__ uint32_t wave_issue_t(const DS &d, uint32_t ol, uint32_t sender, uint
                 if (at < cnt) d.pool[off + at] = make_uint4(m[k] | (st << 24), wv[k] >> 3, sr[k].x, sr[k].y);
                 at++;
                 if (RECV) {                                                   // bump
-                    uint32_t *dxk = (uint32_t *)(d.dent + rb + m[k]);
+                    uint32_t nx;
                     if ((int)(p[k] + 1) >= maxp) {
-                        *dxk = ce[k].x | 0xFF000000u;
+                        nx = ce[k].x | 0xFF000000u;
                         const uint32_t l = m[k] - mbase;
                         if (l < 64) dlo |= 1ull << l; else dhi |= 1ull << (l - 64);
                         del++;
                     } else {
-                        *dxk = ce[k].x + (1u << 24);
+                        nx = ce[k].x + (1u << 24);
                     }
+                    d.dent[rb + m[k]].x = nx;
+                    if (hk[k] != SRC_NONE) d.hde[hb + hk[k]].x = nx;
                 }
             }
             pos += tot;
@@ -497,8 +530,52 @@ __global__ void k_recount(DS d, uint32_t ol) {
 
 __global__ void k_clear_changes(DS d, uint32_t ol) {
     for (uint32_t m = threadIdx.x; m < d.NP; m += blockDim.x) d.dent[(size_t)ol * d.NP + m].x = DE_NONE;
+    if (d.hidx)
+        for (uint32_t k = threadIdx.x; k < d.HP; k += blockDim.x) d.hde[(size_t)ol * d.HP + k].x = DE_NONE;
     for (uint32_t b = threadIdx.x; b < d.NBIT; b += blockDim.x) d.dbit[(size_t)ol * d.NBIT + b] = 0;
     if (threadIdx.x == 0) d.dcnt[ol] = 0;
+}
+
+// hot columns, start of phase I: members that got a first dissemination entry while not hot take free slots
+// (one workgroup; hot_cnt[1] = the first new slot). Members beyond the HP slots stay on the dense path, so the
+// hot set only grows; which members are hot changes no result (the columns are copies).
+__global__ void __launch_bounds__(1024) k_hot_extend(DS d) {
+    __shared__ uint32_t n;
+    if (threadIdx.x == 0) {
+        n = d.hot_cnt[0];
+        d.hot_cnt[1] = n;
+    }
+    __syncthreads();
+    for (uint32_t w = threadIdx.x; w < d.NBIT; w += blockDim.x) {
+        uint32_t bits = d.hotnew[w];
+        if (!bits) continue;
+        d.hotnew[w] = 0;
+        while (bits) {
+            const uint32_t m = w * 32 + (uint32_t)(__ffs(bits) - 1);
+            bits &= bits - 1;
+            if (m >= d.N || d.hidx[m] != SRC_NONE) continue;
+            const uint32_t k = atomicAdd(&n, 1u);
+            if (k < d.HP) {
+                d.hidx[m] = k;
+                d.hlist[k] = m;
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) d.hot_cnt[0] = min(n, d.HP);
+}
+
+// the columns of the slots k_hot_extend added, one wave per observer row
+__global__ void k_hot_fill(DS d) {
+    const uint32_t ol = wave_gid();
+    if (ol >= d.NL) return;
+    const uint32_t k0 = d.hot_cnt[1], k1 = d.hot_cnt[0];
+    const size_t rb = (size_t)ol * d.NP, hb = (size_t)ol * d.HP;
+    for (uint32_t k = k0 + lane_id(); k < k1; k += 64) {
+        const uint32_t m = d.hlist[k];
+        d.hmw[hb + k] = d.mw[rb + m];
+        d.hde[hb + k] = d.dent[rb + m];
+    }
 }
 
 // memberlist.AddJoinList (memberlist.go:398-406) on observer row ol, one wave: Update of the join list
@@ -532,6 +609,8 @@ __global__ void k_add_join_list(DS d, uint32_t ol, const uint4 *__restrict__ rec
             if (acc.napp != before && m != o) {                    // ClearChange(member)
                 const size_t idx = (size_t)ol * d.NP + m;
                 d.dent[idx].x = DE_NONE;
+                const uint32_t hk = hot_slot(d, m);
+                if (hk != SRC_NONE) d.hde[(size_t)ol * d.HP + hk].x = DE_NONE;
                 atomicAnd(&d.dbit[(size_t)ol * d.NBIT + (m >> 5)], ~(1u << (m & 31)));
                 acc.ddc--;
             }
@@ -622,6 +701,8 @@ __global__ void k_timers(DS d, uint32_t r) {
                     if ((w & 7u) != ST_UNKNOWN && m != o) {
                         if (is_pingable(w & 7u)) acc.dping--;
                         d.mw[idx] = (w & ~7u) | ST_UNKNOWN;
+                        const uint32_t hk = hot_slot(d, m);
+                        if (hk != SRC_NONE) d.hmw[(size_t)ol * d.HP + hk] = (w & ~7u) | ST_UNKNOWN;
                         track_len(d, ol, m, w, (w & ~7u) | ST_UNKNOWN, acc);
                         acc.dfp += fpmix(m, (w & ~7u) | ST_UNKNOWN) - fpmix(m, w);
                         acc.evict++;
