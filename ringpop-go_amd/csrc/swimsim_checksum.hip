@@ -706,6 +706,7 @@ void launch_cs_w(const DS &d, const uint32_t *list, const uint32_t *count, uint3
 
 #include "swimsim_checksum2.hip"
 #include "swimsim_checksum3.hip"
+#include "swimsim_checksum4.hip"
 
 // up to CS_NARROW_ROWS rows (measured crossover) the launch is latency-bound: k_checksum_n16 (16 rows per
 // workgroup, ~40 % shorter); above, the 64-row throughput kernel k_checksum3 (17.8 vs 19.4-20.1 ms for its
@@ -713,6 +714,8 @@ void launch_cs_w(const DS &d, const uint32_t *list, const uint32_t *count, uint3
 // selectable for measurements: SWIMSIM_CS_KERNEL=2 / 1)
 constexpr uint32_t CS_NARROW_ROWS = 12288;
 static int g_cs_kernel = 3;
+static int g_cs_narrow = 4;                            // SWIMSIM_CS_NARROW: 4 = k_checksum_q16, 1 = k_checksum_n16
+static uint32_t g_csq16_groups = 256;                  // q16 row groups up to which 16 records per step are used
 static uint32_t g_cs_narrow_rows = CS_NARROW_ROWS;     // SWIMSIM_CS_NARROW_ROWS (tests: 0 = wide kernel only)
 
 void launch_checksum(const DS &d, const uint32_t *list, const uint32_t *count, uint32_t maxn, uint32_t nrows,
@@ -727,6 +730,19 @@ void launch_checksum(const DS &d, const uint32_t *list, const uint32_t *count, u
     case Wv:                                                                                \
         if (g_cs_kernel == 3) launch_cs3_w<Wv>(d, list, count, grid, s);                   \
         else launch_cs2_w<Wv>(d, list, count, grid, s);                                    \
+        break;
+            CS_CASE(13) CS_CASE(14) CS_CASE(15) CS_CASE(16) CS_CASE(17) CS_CASE(18) CS_CASE(19) CS_CASE(20)
+#undef CS_CASE
+        default: break;
+        }
+        return;
+    }
+    if (ngrid && g_cs_narrow == 4) {
+        switch (d.W) {
+#define CS_CASE(Wv)                                                                         \
+    case Wv:                                                                                \
+        if (ngrid <= g_csq16_groups) launch_csq_w<Wv, 16>(d, list, count, ngrid, s);        \
+        else launch_csq_w<Wv, 8>(d, list, count, ngrid, s);                                 \
         break;
             CS_CASE(13) CS_CASE(14) CS_CASE(15) CS_CASE(16) CS_CASE(17) CS_CASE(18) CS_CASE(19) CS_CASE(20)
 #undef CS_CASE
@@ -753,7 +769,17 @@ void launch_checksum_mode(const DS &d, const uint32_t *list, const uint32_t *cou
     const uint32_t grid = (maxn + CS_ROWS - 1) / CS_ROWS;
     if (grid == 0 || d.W != 19) return;
     const uint32_t ngrid = (maxn + CN_ROWS - 1) / CN_ROWS;
-    if (mode == 20) launch_cs2_w<19>(d, list, count, grid, s);
+    if (mode == 30) launch_csq_w<19, 8>(d, list, count, ngrid, s);
+    else if (mode == 31) launch_csq_w<19, 8, 1>(d, list, count, ngrid, s);
+    else if (mode == 32) launch_csq_w<19, 8, 2>(d, list, count, ngrid, s);
+    else if (mode == 33) launch_csq_w<19, 16>(d, list, count, ngrid, s);
+    else if (mode == 34) launch_csq_w<19, 16, 1>(d, list, count, ngrid, s);
+    else if (mode == 35) launch_csq_w<19, 16, 2>(d, list, count, ngrid, s);
+    else if (mode == 36) launch_csq_w<19, 16, 3>(d, list, count, ngrid, s);
+    else if (mode == 37) launch_csq_w<19, 16, 4>(d, list, count, ngrid, s);
+    else if (mode == 38) launch_csq_w<19, 16, 5>(d, list, count, ngrid, s);
+    else if (mode == 39) launch_csq_w<19, 16, 7>(d, list, count, ngrid, s);
+    else if (mode == 20) launch_cs2_w<19>(d, list, count, grid, s);
     else if (mode == 21) launch_cs3_w<19>(d, list, count, grid, s);
     else if (mode == 22) launch_cs3_w<19, 1>(d, list, count, grid, s);
     else if (mode == 23) launch_cs3_w<19, 2>(d, list, count, grid, s);

@@ -1288,6 +1288,7 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
     }
     if (const char *v = getenv("SWIMSIM_CS_ASYNC")) h->cs_async = atoi(v) != 0;
     if (const char *v = getenv("SWIMSIM_CS_KERNEL")) g_cs_kernel = atoi(v);
+    if (const char *v = getenv("SWIMSIM_CS_NARROW")) g_cs_narrow = atoi(v);
     if (const char *v = getenv("SWIMSIM_CS_NARROW_ROWS")) g_cs_narrow_rows = (uint32_t)strtoul(v, nullptr, 10);
     DS &d = h->d;
     d.N = h->N; d.NP = h->NP; d.NL = h->NL; d.lo = h->lo;
