@@ -779,6 +779,9 @@ void launch_checksum_mode(const DS &d, const uint32_t *list, const uint32_t *cou
     else if (mode == 37) launch_csq_w<19, 16, 4>(d, list, count, ngrid, s);
     else if (mode == 38) launch_csq_w<19, 16, 5>(d, list, count, ngrid, s);
     else if (mode == 39) launch_csq_w<19, 16, 7>(d, list, count, ngrid, s);
+    else if (mode == 44) launch_csq_w<19, 16, 8>(d, list, count, ngrid, s);
+    else if (mode == 46) launch_cs3_w<19, 7>(d, list, count, grid, s);
+    else if (mode == 45) launch_csq_w<19, 8, 8>(d, list, count, ngrid, s);
     else if (mode == 20) launch_cs2_w<19>(d, list, count, grid, s);
     else if (mode == 21) launch_cs3_w<19>(d, list, count, grid, s);
     else if (mode == 22) launch_cs3_w<19, 1>(d, list, count, grid, s);

@@ -46,7 +46,7 @@ __global__ void __launch_bounds__(128) k_checksum3(DS d, const uint32_t *list, c
         // The formatter sets the pace of a step (10.5 ms alone for one row group against the hasher's 9.6), and the
         // SIMD arbitrates VALU issue between its two waves by priority, then age: raised, it takes its issue slots
         // ahead of the co-resident hasher wave (17.8 -> 14.6 ms at 65,536 rows, 17.1 -> 13.6 ms at 32,768)
-        __builtin_amdgcn_s_setprio(2);
+        if (MODE != 7) __builtin_amdgcn_s_setprio(2);             // (MODE 7: diagnostics without it)
         const uint32_t ecap1 = d.ecap - 1;
         uint32_t pos = 0, hc = 0;                                  // bytes formatted; the stream's last 4 bytes
         uint4 cur[4], pre[4];                                      // row words: this super step, the next

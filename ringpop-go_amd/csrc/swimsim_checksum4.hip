@@ -102,6 +102,7 @@ __global__ void __launch_bounds__(QGeo<IT>::THREADS) k_checksum_q16(DS d, const 
 
     if (wave >= 1 && wave <= (uint32_t)G::FW) {
         // ------------------------------- formatters (as k_checksum_n16) -------------------------------
+        if (QMODE == 8) __builtin_amdgcn_s_setprio(2);
         const uint32_t r = (wave - 1) * (64 / IT) + lane / IT, k = lane % IT;
         uint32_t id; bool is_row;
         const uint32_t *row = row_of(r, id, is_row);

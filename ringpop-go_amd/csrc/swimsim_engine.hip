@@ -715,7 +715,18 @@ int checksum_dirty(swimsim *h, int mode, bool async = false) {
     }
     HIPCHK(h, hipStreamSynchronize(h->s));                                         // picks the variant
     if (side_ok && hn[1] <= h->snap_cap) return go_side(h->fplist, hn[1], h->fpv_s, h->dup_of);
-    hash_rows(h, h->fplist, h->fpcnt, n, hn[1]);
+    // a wide launch hashes its rows in row order: the list comes out of k_list_flagged in atomic order, and a
+    // workgroup whose 64 rows lie anywhere in the 16 GB of rows touches 64 distant pages per load (the address
+    // translation of the row streams, not their bandwidth, then sets the pace)
+    const uint32_t *hl = h->fplist;
+    if (hn[1] > CS_NARROW_ROWS) {
+        Scope sc(h, F_CSPREP);
+        size_t bytes = h->cub_bytes;
+        HIPCHK(h, hipcub::DeviceRadixSort::SortKeys(h->cub_tmp, bytes, h->fplist, h->list, (int)hn[1], 0,
+                                                    32 - __builtin_clz(std::max(h->NL, 2u) - 1), h->s));
+        hl = h->list;
+    }
+    hash_rows(h, hl, h->fpcnt, n, hn[1]);
     Scope sc(h, F_CSPREP);
     hipLaunchKernelGGL(k_fp_copy, dim3(blocks_for_threads(n)), dim3(256), 0, h->s, h->d, h->fpv_s, n, h->dup_of);
     return 0;
@@ -1427,7 +1438,9 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
         hipcub::DeviceScan::ExclusiveSum(nullptr, b3, h->counts, h->offs, (int)KC);
         hipcub::DeviceRadixSort::SortPairs(nullptr, b4, h->keys, h->keys_sorted, h->fpv, h->fpv_s, (int)h->NL, 0, 64);
         hipcub::DeviceScan::InclusiveScan(nullptr, b5, h->fph, h->fph_s, hipcub::Max(), (int)h->NL);
-        h->cub_bytes = std::max(std::max(b1, std::max(b2, b3)), std::max(b4, b5));
+        size_t b6 = 0;
+        hipcub::DeviceRadixSort::SortKeys(nullptr, b6, h->fplist, h->list, (int)h->NL, 0, 32);
+        h->cub_bytes = std::max(std::max(std::max(b1, b6), std::max(b2, b3)), std::max(b4, b5));
         if ((rc = dalloc(h, (uint8_t **)&h->cub_tmp, h->cub_bytes, "cub temp"))) return bail(rc);
     }
     // single shard until swimsim_comm_attach / swimsim_group_create says otherwise
