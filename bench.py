@@ -42,7 +42,8 @@ VALU_PEAK_GINST = 256 * 4 * 2.4 / 2  # wave-instructions/ns: 1024 SIMDs, one wav
 KILL_ROUND = 10
 # kernel family (swimsim_kernel_times) -> kernel symbols in the rocprofv3 PMC summary
 # (template arguments are ignored: every instantiation of the named kernel counts)
-FAMILY_KERNELS = {"checksum": ["swimdev::k_checksum", "swimdev::k_checksum2", "swimdev::k_checksum3", "swimdev::k_checksum_n16"],
+FAMILY_KERNELS = {"checksum": ["swimdev::k_checksum", "swimdev::k_checksum2", "swimdev::k_checksum3", "swimdev::k_checksum_n16",
+                               "swimdev::k_checksum_q16"],
                   "recv_merge": ["swimdev::k_recv"], "issue": ["swimdev::k_issue"], "resp_merge": ["swimdev::k_resp"],
                   "timers": ["swimdev::k_timers"]}
 FAMILY_SYMBOL = {"checksum": "k_checksum", "recv_merge": "k_recv", "resp_merge": "k_resp", "issue": "k_issue",
