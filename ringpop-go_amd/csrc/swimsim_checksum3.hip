@@ -86,7 +86,10 @@ __global__ void __launch_bounds__(128) k_checksum3(DS d, const uint32_t *list, c
         for (int k = 0; k < C2_IT; k++)
 #pragma unroll
             for (int i = 0; i <= Q; i++) AN[k][i] = ast[0][k * 6 + i];
-        for (uint32_t sc = 0; sc < nsup; sc++) {
+        // one super step with row words C (this one) and P (the next). The two alternate between super steps instead of
+        // being copied: a copy of just-loaded registers at the loop's back edge made every super step wait for the
+        // next one's row loads (s_waitcnt vmcnt(0) at the top of the loop)
+        auto sstep = [&](uint32_t sc, uint4 (&cur)[4], uint4 (&pre)[4]) {
             ast[(sc + 1) & 1u][lane] = ap0;                         // stage super step sc + 1, load sc + 2
             if (lane < 32) ast[(sc + 1) & 1u][64 + lane] = ap1;
             aload(sc + 2, ap0, ap1);
@@ -148,16 +151,16 @@ __global__ void __launch_bounds__(128) k_checksum3(DS d, const uint32_t *list, c
                 bend[pb][lane] = b1;
 #pragma unroll
                 for (int i = 0; i < 5; i++) cw[i] = B[(5 * (b1 - b0) + i) * C2_ROWS];     // the next carry
-                if (u == 3) {                                               // next super step's row words
+                if (u == 3 && sc + 2 < nsup) {                             // row words of super step sc + 2
 #pragma unroll
-                    for (int k = 0; k < 4; k++) cur[k] = pre[k];
-                    if (sc + 2 < nsup) {
-#pragma unroll
-                        for (int k = 0; k < 4; k++) pre[k] = *(const uint4 *)(row + (sc + 2) * 16 + 4 * k);
-                    }
+                    for (int k = 0; k < 4; k++) cur[k] = *(const uint4 *)(row + (sc + 2) * 16 + 4 * k);
                 }
                 lds_barrier();
             }
+        };
+        for (uint32_t sc = 0; sc < nsup; sc += 2) {
+            sstep(sc, cur, pre);
+            if (sc + 1 < nsup) sstep(sc + 1, pre, cur);
         }
         if (MODE == 5 && sink == 0x12345678u) d.ctr[0] = sink;  // keeps the folded words alive (never true)
         return;
