@@ -25,7 +25,7 @@ for rows in rows_list:
     ref = None
     for mode in modes:
         out[f"rows{rows}_mode{mode}"] = round(c.bench_checksum(rows, mode, reps=reps), 3)
-        if verify and mode in (0, 6, 20, 21, 30, 33):
+        if verify and mode in (0, 6, 20, 21, 30, 33, 44, 45):
             cs = c.checksums()[:rows].copy()
             if ref is None:
                 ref = cs
