@@ -89,7 +89,8 @@ __global__ void __launch_bounds__(128) k_checksum3(DS d, const uint32_t *list, c
         // one super step with row words C (this one) and P (the next). The two alternate between super steps instead of
         // being copied: a copy of just-loaded registers at the loop's back edge made every super step wait for the
         // next one's row loads (s_waitcnt vmcnt(0) at the top of the loop)
-        auto sstep = [&](uint32_t sc, uint4 (&cur)[4], uint4 (&pre)[4]) {
+        auto sstep = [&](uint32_t sc, uint4 (&cur)[4], uint4 (&pre)[4], auto FULLC) {
+            constexpr bool FULL = decltype(FULLC)::value;               // every member of the super step is < N
             ast[(sc + 1) & 1u][lane] = ap0;                         // stage super step sc + 1, load sc + 2
             if (lane < 32) ast[(sc + 1) & 1u][64 + lane] = ap1;
             aload(sc + 2, ap0, ap1);
@@ -129,7 +130,7 @@ __global__ void __launch_bounds__(128) k_checksum3(DS d, const uint32_t *list, c
 #pragma unroll
                 for (int k = 0; k < C2_IT; k++) {
                     const uint32_t m = mb + k;
-                    const uint32_t L = ((ws[k] & 7u) < 4u && m < N) ? (tb[k].z >> 24) : 0u;
+                    const uint32_t L = ((ws[k] & 7u) < 4u && (FULL || m < N)) ? (tb[k].z >> 24) : 0u;
                     const uint32_t sh = pos & 3u;
                     // sh * 0x01010101 as a byte broadcast (one full-rate v_perm, not a multiply)
                     const uint32_t sel = 0x07060504u - __builtin_amdgcn_perm(0u, sh, 0u);
@@ -158,9 +159,19 @@ __global__ void __launch_bounds__(128) k_checksum3(DS d, const uint32_t *list, c
                 lds_barrier();
             }
         };
-        for (uint32_t sc = 0; sc < nsup; sc += 2) {
-            sstep(sc, cur, pre);
-            if (sc + 1 < nsup) sstep(sc + 1, pre, cur);
+        // super steps whose 16 members all exist skip the per-record bounds test (scalar compares that a lone wave
+        // pays issue slots for); at most the last super step is partial
+        const std::integral_constant<bool, true> full{};
+        const std::integral_constant<bool, false> part{};
+        const uint32_t nfull = N / 16;
+        uint32_t sc = 0;
+        for (; sc + 1 < nfull; sc += 2) {
+            sstep(sc, cur, pre, full);
+            sstep(sc + 1, pre, cur, full);
+        }
+        if (sc < nsup) {
+            sstep(sc, cur, pre, part);
+            if (sc + 1 < nsup) sstep(sc + 1, pre, cur, part);
         }
         if (MODE == 5 && sink == 0x12345678u) d.ctr[0] = sink;  // keeps the folded words alive (never true)
         return;
