@@ -17,13 +17,14 @@ cross-shard message moves over RCCL point-to-point (xGMI) inside libswimsim. Tot
 "scaling" is "strong".
 
 The JSON line carries:
-  roofline     : the kernel with the most device time (rank 0): its algorithmic bytes per launch
-                 (DESIGN.md §8 per-unit figures x the units the launch processed, counted on the device
-                 during the timed rounds) / its average launch time (HIP events on the engine's own
-                 stream), against the 8 TB/s HBM peak. `traffic` is FETCH_SIZE + WRITE_SIZE per launch from
-                 the rocprofv3 PMC passes of THIS command (profiles/r02_pmc_summary.json; null when that
-                 summary was taken on another workload). `merge` gives the same figures for the merge
-                 kernels (k_recv, k_resp, k_issue); `merge_kernel` repeats k_recv, the north-star kernel.
+  roofline     : the kernel with the most device time (rank 0): units per launch (rows hashed, changes
+                 merged; counted on the device over the timed rounds) x SURVEY.md §8(d)'s bytes per unit
+                 = algorithmic bytes per launch, / its average launch time (HIP events on the engine's own
+                 stream), against the 8 TB/s HBM peak. `traffic` = HBM bytes per launch from the rocprofv3
+                 PMC passes of THIS command cut to the same timed rounds (k_profile_mark dispatches around
+                 them; profiles/r03_pmc_summary.json; null when that summary was taken on another workload).
+                 `kernels` gives the same figures for the other kernels (the other checksum kernel, k_recv,
+                 k_resp, k_issue); `merge_kernel` repeats k_recv, the north-star merge kernel.
   cpu_baseline : the C oracle on the GPU box's host cores (rank 0, N=1 only), bounded sample.
 """
 import argparse
@@ -40,36 +41,102 @@ sys.path.insert(0, os.path.join(REPO, "ringpop-go_amd"))
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 VALU_PEAK_GINST = 256 * 4 * 2.4 / 2  # wave-instructions/ns: 1024 SIMDs, one wave64 VALU op per 2 cycles at 2.4 GHz
 KILL_ROUND = 10
-# kernel family (swimsim_kernel_times) -> kernel symbols in the rocprofv3 PMC summary
-# (template arguments are ignored: every instantiation of the named kernel counts)
-FAMILY_KERNELS = {"checksum": ["swimdev::k_checksum", "swimdev::k_checksum2", "swimdev::k_checksum3", "swimdev::k_checksum_n16",
-                               "swimdev::k_checksum_q16"],
-                  "recv_merge": ["swimdev::k_recv"], "issue": ["swimdev::k_issue"], "resp_merge": ["swimdev::k_resp"],
-                  "timers": ["swimdev::k_timers"]}
-FAMILY_SYMBOL = {"checksum": "k_checksum", "recv_merge": "k_recv", "resp_merge": "k_resp", "issue": "k_issue",
-                 "timers": "k_timers"}
-PMC_SUMMARY = os.path.join(REPO, "profiles", "r02_pmc_summary.json")
+MARK_BEGIN, MARK_END = 0x5717, 0x5718   # k_profile_mark ids around the timed rounds (tools/pmc_summary.py --window)
+# kernel family (swimsim_kernel_times) -> kernel symbol in rocprofv3 output (template arguments ignored)
+FAMILY_KERNEL = {"checksum_wide": "swimdev::k_checksum3", "checksum_narrow": "swimdev::k_checksum_q16",
+                 "recv_merge": "swimdev::k_recv", "resp_merge": "swimdev::k_resp", "issue": "swimdev::k_issue",
+                 "timers": "swimdev::k_timers"}
+PMC_SUMMARY = os.path.join(REPO, "profiles", "r03_pmc_summary.json")
 
 
-def pmc_family(family, workload):
-    """Per-launch PMC figures of the family's kernels, launch-weighted over the committed rocprofv3 --pmc
-    passes (FETCH_SIZE / WRITE_SIZE / SQ_INSTS_VALU..., separate runs; tools/pmc_summary.py), or None when the
-    summary is missing or was collected on a different workload than this run's."""
+def pmc_kernel(symbol, workload):
+    """Per-launch PMC figures of one kernel over the timed rounds only (rocprofv3 --pmc passes of this command, cut
+    between the k_profile_mark dispatches by tools/pmc_summary.py --window), or None when the committed summary was
+    taken on another workload or without the window cut."""
     try:
         with open(PMC_SUMMARY) as f:
             t = json.load(f)
-        if t.get("_workload") != workload:
+        if t.get("_workload") != workload or not t.get("_window"):
             return None
-        names = set(FAMILY_KERNELS.get(family, []))
-        ks = [v for k, v in t.items() if not k.startswith("_") and k.split("<")[0].strip() in names]
+        ks = [v for k, v in t.items() if not k.startswith("_") and k.split("<")[0].strip() == symbol]
     except (OSError, KeyError, ValueError):
         return None
     n = sum(k["launches"] for k in ks)
     if not n:
         return None
-    tot = lambda key: sum(k.get(key, 0.0) * k["launches"] for k in ks) / n
-    return {"traffic": round(tot("fetch_bytes_per_launch") + tot("write_bytes_per_launch"), 1),
-            "valu_insts": tot("sq_insts_valu_per_launch"), "lds_insts": tot("sq_insts_lds_per_launch")}
+    avg = lambda key: sum(k.get(key, 0.0) * k["launches"] for k in ks) / n
+    return {"launches": n, "fetch": avg("fetch_bytes_per_launch"), "write": avg("write_bytes_per_launch"),
+            "valu_insts": avg("sq_insts_valu_per_launch"), "lds_insts": avg("sq_insts_lds_per_launch"),
+            "source": os.path.relpath(PMC_SUMMARY, REPO)}
+
+
+def roofline_entry(fam, kt, units, n_members):
+    """One kernel against the HBM roofline: achieved = algorithmic bytes per launch (SURVEY.md §8(d) bytes per unit
+    x the units the launches processed, counted on the device over the timed rounds) / the average launch time
+    (HIP events on the engine's stream); frac = achieved / 8 TB/s. traffic = HBM bytes per launch from the PMC
+    passes of this command over the same rounds: FETCH_SIZE doubled (gfx950 tallies a 16-B-per-lane read's
+    128-B requests at 64 B, MI355X_MICROARCH.md §HBM; tools/fetch_calib.hip checks the factor per access pattern,
+    profiles/r03_fetch_calib.json) + WRITE_SIZE."""
+    k = kt.get(fam, {})
+    if not k.get("avg_ms") or not k.get("launches"):
+        return None
+    nl, sec = k["launches"], k["avg_ms"] * 1e-3
+    out = {"kernel": FAMILY_KERNEL[fam].split("::")[-1], "avg_launch_ms": round(k["avg_ms"], 4), "launches": nl}
+    if fam.startswith("checksum"):
+        rows = units["cs_rows_wide" if fam == "checksum_wide" else "cs_rows_narrow"]
+        per = 5.0 * n_members
+        out.update({"work_unit": "hashed row", "units_per_launch": round(rows / nl, 1),
+                    "bytes_per_unit": per, "bytes_per_unit_basis": "SURVEY.md §8(d): 5 B (status u8 + incarnation "
+                    "u32) per member per dirty row; the kernel reads a 4-B member word (e << 3 | status) per member",
+                    "alg_bytes_per_launch": round(rows / nl * per, 1),
+                    "alg_bytes_per_launch_4B": round(rows / nl * 4.0 * n_members, 1)})
+    elif fam in ("recv_merge", "resp_merge"):
+        pre = "recv" if fam == "recv_merge" else "resp"
+        merged, applied = units[pre + "_merged"], units[pre + "_applied"]
+        merge_b = 22.0 * merged + 23.0 * applied
+        if fam == "recv_merge":
+            side_b = 36.0 * units["recv_issued"] + 4.0 * units["bitmap_words_per_row"] * units["recv_calls"]
+            side = {"issue_as_receiver_bytes_per_launch": round(side_b / nl, 1),
+                    "issue_as_receiver_basis": "36 B per issued record (16-B cell gather + 16-B record write + 4-B "
+                    "counter write-back) + the presence bitmap (4 B per 32 members) per call"}
+        else:
+            side_b = 24.0 * units["resp_bumped"]
+            side = {"bump_bytes_per_launch": round(side_b / nl, 1),
+                    "bump_basis": "24 B per bumped entry (16-B record read + 4-B counter read and write)"}
+        out.update({"work_unit": "processed change", "units_per_launch": round(merged / nl, 1),
+                    "applied_per_launch": round(applied / nl, 1),
+                    "bytes_per_unit_basis": "SURVEY.md §8(d): 17 B change entry + 5 B row read per processed "
+                    "change; + 5 B row write + 9 B dissemination entry + 9 B timer per applied change",
+                    "alg_bytes_per_launch": round(merge_b / nl, 1), **side,
+                    "achieved_incl_side": round((merge_b + side_b) / nl / sec / 1e9, 2),
+                    "frac_incl_side": round((merge_b + side_b) / nl / sec / 1e9 / HBM_PEAK_GBPS, 4)})
+    elif fam == "issue":
+        out.update({"work_unit": "issued record", "units_per_launch": round(units["issued"] / nl, 1), "bytes_per_unit": 32.0,
+                    "alg_bytes_per_launch": round(units["issued"] / nl * 32.0, 1)})
+    else:
+        return out
+    alg = out["alg_bytes_per_launch"] / sec / 1e9
+    out.update({"achieved": round(alg, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(alg / HBM_PEAK_GBPS, 4)})
+    return out
+
+
+def add_pmc(entry, fam, workload):
+    if not entry:
+        return entry
+    p = pmc_kernel(FAMILY_KERNEL[fam], workload)
+    if not p:
+        entry.update({"traffic": None, "traffic_note": "no PMC summary of this workload's timed window"})
+        return entry
+    t = 2.0 * p["fetch"] + p["write"]
+    entry.update({"traffic": round(t, 1), "traffic_raw_fetch_plus_write": round(p["fetch"] + p["write"], 1),
+                  "traffic_over_alg": round(t / entry["alg_bytes_per_launch"], 3) if entry.get("alg_bytes_per_launch") else None,
+                  "pmc_launches": p["launches"], "pmc_source": p["source"]})
+    if fam.startswith("checksum") and p["valu_insts"]:
+        rate = p["valu_insts"] / (entry["avg_launch_ms"] * 1e6)
+        entry["valu"] = {"achieved": round(rate, 2), "peak": VALU_PEAK_GINST, "unit": "G wave-instr/s",
+                         "frac": round(rate / VALU_PEAK_GINST, 4), "valu_insts_per_launch": round(p["valu_insts"]),
+                         "lds_insts_per_launch": round(p["lds_insts"])}
+    return entry
 
 
 def ring_bench(n, replicas=100, nkeys=1 << 20):
@@ -137,13 +204,36 @@ def free_port():
         return s.getsockname()[1]
 
 
+def visible_gpu_count():
+    """GPUs this process may use, counted without initialising HIP (a parent that touched the GPU must not
+    re-launch under torch.distributed.run): the *_VISIBLE_DEVICES lists when set, else the KFD topology's GPU
+    nodes (nodes with SIMDs). None when neither is readable; each rank then checks LOCAL_RANK itself."""
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            return len([x for x in v.split(",") if x.strip() != ""])
+    root = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        count = 0
+        for node in os.listdir(root):
+            with open(os.path.join(root, node, "properties")) as f:
+                props = dict(l.split()[:2] for l in f if len(l.split()) >= 2)
+            count += int(props.get("simd_count", "0")) > 0
+        return count
+    except (OSError, ValueError):
+        return None
+
+
+def emit(obj):
+    """One JSON line in ONE write(2): ranks sharing a pipe never interleave their lines (< PIPE_BUF bytes)."""
+    os.write(1, (json.dumps(obj) + "\n").encode())
+
+
 def launch_ranks(args):
     """--gpus N without a launcher: start N ranks as a child torch.distributed.run, relay its status."""
     if not args.launch_check:
-        import torch  # device_count() does not initialise the GPU on this image
-
-        have = torch.cuda.device_count()
-        if have < args.gpus:
+        have = visible_gpu_count()
+        if have is not None and have < args.gpus:
             print(f"bench.py: --gpus {args.gpus} but only {have} GPU(s) visible", file=sys.stderr)
             return 2
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
@@ -173,7 +263,7 @@ def main():
     if ws != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws}")
     if args.launch_check:
-        print(json.dumps({"rank": rank, "world_size": ws, "local_rank": local}), flush=True)
+        emit({"rank": rank, "world_size": ws, "local_rank": local})
         return
 
     import torch
@@ -182,6 +272,8 @@ def main():
         raise SystemExit("bench.py needs an MI355X (no GPU visible)")
     if args.host_transport:
         local = 0
+    if local >= torch.cuda.device_count():
+        raise SystemExit(f"bench.py: rank {rank} needs GPU {local}, but {torch.cuda.device_count()} are visible")
     torch.cuda.set_device(local)
     if ws > 1:
         import torch.distributed as dist
@@ -227,6 +319,8 @@ def main():
     for r in range(args.warmup):
         eng.step(1, wl.events_for(r))
     eng.enable_timing(True)
+    if rank == 0:
+        eng.profile_mark(MARK_BEGIN)    # rocprofv3 counter passes are cut to the launches between the two marks
     barrier()
     t0 = time.perf_counter()
     ev = [e for e in wl.events if args.warmup <= e[0] < total_rounds]
@@ -238,7 +332,10 @@ def main():
 
         dt = sd.max_over_ranks(dt)
 
+    if rank == 0:
+        eng.profile_mark(MARK_END)
     kt = eng.kernel_times()
+    units = eng.kernel_units()
     counters = eng.counters()
     shard = eng.shard_info()
     eng.enable_timing(False)
@@ -246,28 +343,13 @@ def main():
         counters = sd.reduce_counters(counters)
     workload = {"members": n, "steps": args.steps, "warmup": args.warmup, "gpus": ws}
 
-    def family_roofline(f):
-        # algorithmic bytes per launch / HIP-event time of the same launches; PMC traffic of this command
-        k = kt.get(f, {})
-        if not k.get("avg_ms"):
-            return None
-        sec = k["avg_ms"] * 1e-3
-        per_launch = k["alg_bytes"] / max(1, k["launches"])
-        alg = per_launch / sec / 1e9
-        p = pmc_family(f, workload)
-        out = {"kernel": FAMILY_SYMBOL.get(f, f), "avg_launch_ms": round(k["avg_ms"], 4), "launches": k["launches"],
-               "alg_bytes_per_launch": round(per_launch, 1), "achieved": round(alg, 2),
-               "frac": round(alg / HBM_PEAK_GBPS, 4), "unit": "GB/s",
-               "traffic": p["traffic"] if p else None,
-               "traffic_over_alg": round(p["traffic"] / per_launch, 2) if p and per_launch > 0 else None}
-        return out
-
     if rank == 0:
         timed_first, timed_last = args.warmup, total_rounds - 1
         live_mr = live_member_rounds(wl, timed_first, timed_last)
         value = live_mr / dt
         dominant = max(kt.items(), key=lambda kv: kv[1]["avg_ms"] * kv[1]["launches"])[0]
-        dom = family_roofline(dominant)
+        entries = {f: add_pmc(roofline_entry(f, kt, units, n), f, workload) for f in FAMILY_KERNEL}
+        dom = entries.get(dominant) or {}
         in_window = timed_first <= KILL_ROUND <= timed_last
         faulty_from = KILL_ROUND + 25       # first suspicions at KILL_ROUND; their timers fire 25 rounds later
         line = {
@@ -291,21 +373,12 @@ def main():
                        "members": n, "rounds_timed": args.steps, "live_member_rounds": live_mr,
                        "parallelism": (f"observer-row shards x{ws} over " + ("host transport (diagnostic)" if args.host_transport
                                                                               else "RCCL")) if ws > 1 else "1 GPU"},
-            "roofline": {"bound": "hbm", **(dom or {}), "peak": HBM_PEAK_GBPS,
-                         "traffic_unit": "bytes per launch (FETCH_SIZE + WRITE_SIZE, " + os.path.basename(PMC_SUMMARY) + ")",
-                         "merge_kernel": family_roofline("recv_merge"),
-                         "merge": {f: family_roofline(f) for f in ("recv_merge", "resp_merge", "issue")}},
+            "roofline": {"bound": "hbm", **dom, "dominant_family": dominant,
+                         "kernels": {f: e for f, e in entries.items() if e and f != dominant},
+                         "merge_kernel": entries.get("recv_merge")},
             "kernel_ms": {k: round(v["avg_ms"] * v["launches"], 3) for k, v in kt.items()},
             "counters": counters,
         }
-        pmc = pmc_family(dominant, workload)
-        if dominant == "checksum" and pmc and pmc["valu_insts"] and kt[dominant]["avg_ms"] > 0:
-            # the checksum is integer-VALU work: its instruction rate against the chip's VALU issue peak
-            rate = pmc["valu_insts"] / (kt[dominant]["avg_ms"] * 1e6)
-            line["roofline"]["valu"] = {"achieved": round(rate, 2), "peak": VALU_PEAK_GINST, "unit": "G wave-instr/s",
-                                        "frac": round(rate / VALU_PEAK_GINST, 4),
-                                        "valu_insts_per_launch": round(pmc["valu_insts"]),
-                                        "lds_insts_per_launch": round(pmc["lds_insts"])}
         if ws > 1:
             line["exchange"] = {"bytes_rank0": shard["exchanged_bytes"], "exchanges_rank0": shard["exchanges"],
                                 "bytes_per_round_rank0": round(shard["exchanged_bytes"] / max(1, total_rounds), 1)}
@@ -313,7 +386,8 @@ def main():
             line["cpu_baseline"] = cpu_baseline(f"{n}:{args.warmup}:{args.steps}")
         if ws == 1 and not args.no_ring:
             line["hashring"] = ring_bench(n)
-        print(json.dumps(line), flush=True)
+        sys.stdout.flush()
+        emit(line)
     if ws > 1:
         import torch.distributed as dist
 

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SWIMSIM_ABI_VERSION 3
+#define SWIMSIM_ABI_VERSION 4
 
 enum {
     SWIMSIM_OK = 0,
@@ -164,11 +164,25 @@ int swimsim_converged(swimsim_t *h, int32_t *out);
  * between, coalesced per member: the ring's final membership depends only on each member's last change),
  * the checksum at the previous drain (OldChecksum), the current one (NewChecksum) and NumMembers. n = 0:
  * nothing applied, no event. Evictions are not events (RemoveMember emits none, memberlist.go:141-162).
- * At most 64 watched observers per handle. */
+ * At most 64 watched observers per handle.
+ * on = 1: the coalesced drain below. on = 2: also the per-Update stream (swimsim_applied_events). on = 0: off. */
 int swimsim_watch(swimsim_t *h, uint32_t observer, int32_t on);
 int swimsim_applied_changes(swimsim_t *h, uint32_t observer, int32_t *member, int32_t *status, int64_t *inc_ms,
                             int32_t *source, int64_t *source_inc_ms, size_t cap, size_t *n, uint32_t *old_checksum,
                             uint32_t *new_checksum, int32_t *num_members);
+/* The per-Update stream of an observer watched with on = 2, without coalescing: one event per Update that applied
+ * something (memberlist.go:366-384), in the order the node ran its Updates (docs/ROUND_SEMANTICS.md §4: events, each
+ * fired timer in (deadline, member) order, the inbox in sender order, the response, the ping-req relays, the
+ * reverse full syncs). Change i belongs to event event[i] (0 .. *nevents-1, ascending); the changes of one event
+ * are listed in member order (the reference lists a message's changes in Go map order, which is random). Ringpop's
+ * per-change statistics (ringpop.go:398-406) and its ring's insertion order are those of this stream.
+ * OldChecksum / NewChecksum / NumMembers are per DRAIN, not per event: the checksum at the previous drain of this
+ * stream, the current checksum and the current member count (the reference computes one checksum per Update,
+ * memberlist.go:367; this engine keeps the per-round ones). *n = total changes (also when > cap: only cap are
+ * written). SWIMSIM_ECAPACITY: more than 4*N changes since the last drain (the stream restarts empty). */
+int swimsim_applied_events(swimsim_t *h, uint32_t observer, int32_t *member, int32_t *status, int64_t *inc_ms,
+                           int32_t *source, int64_t *source_inc_ms, uint32_t *event, size_t cap, size_t *n,
+                           size_t *nevents, uint32_t *old_checksum, uint32_t *new_checksum, int32_t *num_members);
 
 /* NodeInterface.ProtocolStats (node.go:137-147, stats.go:81-104). Each round is one ProtocolPeriod of every
  * live node (gossip.go:178-188), so the Timing histogram is over rounds: the device wall time of each round
@@ -199,10 +213,16 @@ int swimsim_memory(swimsim_t *h, swimsim_memory_t *out);
 int swimsim_kernel_times(swimsim_t *h, const char **names, double *avg_ms, uint64_t *launches,
                          double *alg_bytes, size_t cap, size_t *n);
 int swimsim_enable_timing(swimsim_t *h, int32_t enable);
-/* time the checksum kernel alone on the first nrows rows (mode 0 full, 1 hasher only, 2 formatting
- * only; the last two are diagnostics and leave garbage checksums) — average ms per launch */
+/* the unit counts behind those byte figures since swimsim_enable_timing (rows hashed by each checksum kernel,
+ * changes processed / applied by each merge kernel, records issued, ...): names[i], values[i] */
+int swimsim_kernel_units(swimsim_t *h, const char **names, double *values, size_t cap, size_t *n);
+/* profiler window marker: one tiny kernel (k_profile_mark) on the engine's stream, after the side stream drained */
+int swimsim_profile_mark(swimsim_t *h, uint32_t id);
+/* time the checksum kernel alone on the first nrows rows — average ms per launch. mode 0: the production choice for
+ * nrows rows, 1: the wide kernel (k_checksum3), 2: the narrow kernel (k_checksum_q16); other modes (diagnostic
+ * variants) only in the diagnostics library tools/libswimsim_diag.so */
 int swimsim_bench_checksum(swimsim_t *h, uint32_t nrows, int32_t mode, int32_t reps, double *ms);
-/* diagnostics: the 32-bit words of every 20-byte block the checksum kernel hashes for row o (W = 19) */
+/* diagnostics library only: the 32-bit words of every 20-byte block the checksum kernel hashes for row o (W = 19) */
 int swimsim_debug_cs_stream(swimsim_t *h, uint32_t o, uint32_t *out, size_t cap_words);
 
 /* ---- shards: one cluster's observer rows split over G shards ----

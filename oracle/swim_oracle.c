@@ -108,6 +108,12 @@ typedef struct obs {
     uint32_t wcs_prev;    /* checksum at the last drain (the event's OldChecksum) */
     uint8_t *wdirty;      /* [n] */
     or_change *wlast;     /* [n] */
+    /* watched == 2: every applied change, one event per applying Update, in Update order */
+    or_change *wev;
+    int64_t *wev_seq;
+    size_t wev_n, wev_cap;
+    int64_t wseq;         /* applying Updates so far */
+    uint32_t wcs_ev_prev;
     omap tim;             /* stateTransitions.timers (state_transitions.go:49) */
     int64_t clock_off;
     uint32_t cs;          /* memberlist.members.checksum (memberlist.go:46) */
@@ -169,6 +175,7 @@ or_sim *or_create(const or_config *cfg) {
     s->st = (uint8_t *)malloc(nn);
     s->inc = (int64_t *)malloc(nn * sizeof(int64_t));
     memset(s->st, OR_UNKNOWN, nn);
+#pragma omp parallel for schedule(static)
     for (size_t i = 0; i < nn; i++) s->inc[i] = cfg->t0_ms;  /* never-known entries read e = 0 */
     s->o = (obs *)calloc(s->n, sizeof(obs));
     for (uint32_t i = 0; i < s->n; i++) {
@@ -214,6 +221,8 @@ void or_destroy(or_sim *s) {
         free(s->o[i].jobs);
         free(s->o[i].wdirty);
         free(s->o[i].wlast);
+        free(s->o[i].wev);
+        free(s->o[i].wev_seq);
     }
     free(s->o); free(s->st); free(s->inc); free(s->addr); free(s->addr_len);
     free(s->last_target);
@@ -352,6 +361,17 @@ static const char *STATUS_STR[5] = {"alive", "suspect", "faulty", "leave", "tomb
 
 static int cmp_cstr(const void *a, const void *b) { return strcmp(*(const char *const *)a, *(const char *const *)b); }
 
+/* %lld of v (Go's %v of an int64, memberlist.go:120) without snprintf's per-call overhead */
+static size_t fmt_i64(char *out, int64_t v) {
+    char tmp[24];
+    size_t k = 0, len = 0;
+    uint64_t u = v < 0 ? (uint64_t)0 - (uint64_t)v : (uint64_t)v;
+    do { tmp[k++] = (char)('0' + u % 10); u /= 10; } while (u);
+    if (v < 0) out[len++] = '-';
+    while (k) out[len++] = tmp[--k];
+    return len;
+}
+
 static void csbuf_reserve(size_t need) {
     if (tl_csbuf_cap >= need) return;
     tl_csbuf_cap = need * 2;
@@ -394,7 +414,7 @@ static size_t gen_checksum_string(or_sim *s, uint32_t o) {
             size_t sl = strlen(STATUS_STR[st]);
             memcpy(tl_csbuf + len, STATUS_STR[st], sl);
             len += sl;
-            len += (size_t)snprintf(tl_csbuf + len, 24, "%lld", (long long)INC(s, o, m));
+            len += fmt_i64(tl_csbuf + len, INC(s, o, m));
             tl_csbuf[len++] = ';';
         }
     }
@@ -601,6 +621,18 @@ int32_t or_update(or_sim *s, uint32_t j, const or_change *ch, int32_t n, or_chan
                 ob->wdirty[applied[i].member] = 1;
                 ob->wlast[applied[i].member] = applied[i];
             }
+        if (ob->watched == 2) {                           /* one event per applying Update */
+            if (ob->wev_n + (size_t)na > ob->wev_cap) {
+                ob->wev_cap = (ob->wev_n + (size_t)na) * 2;
+                ob->wev = (or_change *)realloc(ob->wev, sizeof(or_change) * ob->wev_cap);
+                ob->wev_seq = (int64_t *)realloc(ob->wev_seq, sizeof(int64_t) * ob->wev_cap);
+            }
+            for (int32_t i = 0; i < na; i++) {
+                ob->wev[ob->wev_n] = applied[i];
+                ob->wev_seq[ob->wev_n++] = ob->wseq;
+            }
+            ob->wseq++;
+        }
         handle_changes(s, j, applied, na);                /* memberlist.go:384 */
         CTR_ADD(s, OR_C_APPLIED, (uint64_t)na);
     }
@@ -1133,7 +1165,36 @@ void or_watch(or_sim *s, uint32_t o, int32_t on) {
         free(ob->wdirty); free(ob->wlast);
         ob->wdirty = NULL; ob->wlast = NULL;
     }
-    ob->watched = on ? 1 : 0;
+    if (on == 2 && ob->watched != 2) {                   /* the per-Update stream starts empty */
+        ob->wev_n = 0;
+        ob->wcs_ev_prev = or_checksum(s, o);
+    }
+    ob->watched = on == 2 ? 2 : on ? 1 : 0;
+}
+
+/* the per-Update stream (watched == 2): every applied change since the last drain, event_seq[i] = the index of its
+ * Update among this drain's applying Updates (0, 1, ...), changes of one Update in the order Update applied them;
+ * the checksum at the previous drain, the current one and NumMembers. Returns the number of changes. */
+int32_t or_drain_events(or_sim *s, uint32_t o, or_change *out, int32_t *event_seq, int32_t cap, uint32_t *old_cs,
+                        uint32_t *new_cs, int32_t *num_members) {
+    obs *ob = &s->o[o];
+    if (ob->watched != 2) return -1;
+    int32_t ev = -1;
+    for (size_t i = 0; i < ob->wev_n; i++) {
+        if (i == 0 || ob->wev_seq[i] != ob->wev_seq[i - 1]) ev++;
+        if ((int32_t)i < cap) {
+            out[i] = ob->wev[i];
+            event_seq[i] = ev;
+        }
+    }
+    const int32_t k = (int32_t)ob->wev_n;
+    ob->wev_n = 0;
+    const uint32_t cs = or_checksum(s, o);
+    if (old_cs) *old_cs = ob->wcs_ev_prev;
+    if (new_cs) *new_cs = cs;
+    if (num_members) *num_members = ob->nmem;
+    ob->wcs_ev_prev = cs;
+    return k;
 }
 
 /* every member with an applied change since the last drain (its last applied change), in member order,
@@ -1238,6 +1299,8 @@ static uint64_t round_of_deadline(const or_sim *s, int64_t dl) {
 }
 void or_digest(or_sim *s, uint64_t *rows, uint64_t *dis, uint64_t *tim) {
     uint64_t r = 0, d = 0, t = 0;
+    /* sums mod 2^64 are order-independent, so the OpenMP build's reduction equals the serial digest */
+#pragma omp parallel for schedule(dynamic, 64) reduction(+ : r, d, t)
     for (uint32_t o = 0; o < s->n; o++) {
         for (uint32_t m = 0; m < s->n; m++) r += mix4(o, m, ST(s, o, m), to_e(s, INC(s, o, m)));
         const omap *dm = &s->o[o].dis;

@@ -113,6 +113,10 @@ void or_digest(or_sim *s, uint64_t *rows, uint64_t *dis, uint64_t *tim);
 void or_watch(or_sim *s, uint32_t o, int32_t on);
 int32_t or_drain_applied(or_sim *s, uint32_t o, or_change *out, int32_t cap, uint32_t *old_cs, uint32_t *new_cs,
                          int32_t *num_members);
+/* per-Update stream of an observer watched with on = 2: every applied change since the last drain, event_seq[i] =
+ * index of its applying Update within the drain; old/new checksum and NumMembers as or_drain_applied */
+int32_t or_drain_events(or_sim *s, uint32_t o, or_change *out, int32_t *event_seq, int32_t cap, uint32_t *old_cs,
+                        uint32_t *new_cs, int32_t *num_members);
 
 /* --- unit-level primitives (for the reference KATs) --- */
 int32_t or_non_local_override(int64_t cur_inc, int32_t cur_st, int64_t ch_inc, int32_t ch_st);

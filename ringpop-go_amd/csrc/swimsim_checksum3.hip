@@ -218,13 +218,14 @@ __global__ void __launch_bounds__(128) k_checksum3(DS d, const uint32_t *list, c
         }
         if (t < nsteps) lds_barrier();
     }
+    const uint32_t nvalid = (uint32_t)__popcll(__ballot(valid));
+    if (lane == 0) ctr_add(d, C_X_CS_ROWS, (unsigned long long)nvalid);   // rows this launch hashed (measurement)
     if (valid) {
         fh.h = h; fh.g = g; fh.f = f;
         const uint32_t hv = ok ? fh.fin() : 0u;
         if (is_row) {
             d.cs[id] = hv;
             d.dirty[id] = 0;
-            ctr_add(d, C_X_CS_ROWS, 1ull);
         } else {
             d.dense_cs[id - d.NL] = hv;
         }

@@ -347,13 +347,14 @@ __global__ void __launch_bounds__(QGeo<IT>::THREADS) k_checksum_q16(DS d, const 
         if (QMODE != 7) lds_barrier();
     }
     const uint32_t g = (uint32_t)__shfl((int)X, (int)(lane & ~3u)), f = (uint32_t)__shfl((int)X, (int)(lane & ~3u) + 1);
+    const uint32_t nvalid = (uint32_t)__popcll(__ballot(role == 2 && valid));
+    if (lane == 0) ctr_add(d, C_X_CS_ROWS_N, (unsigned long long)nvalid);  // rows this launch hashed (measurement)
     if (role == 2 && valid) {
         fh.h = X; fh.g = g; fh.f = f;
         const uint32_t hv = ok ? fh.fin() : 0u;
         if (is_row) {
             d.cs[id] = hv;
             d.dirty[id] = 0;
-            ctr_add(d, C_X_CS_ROWS, 1ull);
         } else {
             d.dense_cs[id - d.NL] = hv;
         }

@@ -36,11 +36,13 @@ enum Counter {
     C_TIMERS_FIRED, C_MSG_CHANGES, C_HEAL_ATTEMPTS, C_HEAL_FAILURES, C_NCOUNTERS,
     // measurement-only counters (not part of the parity record)
     // (merges and applies of k_recv and k_resp are counted apart: C_X_MERGED + 5 / C_X_APPLIED + 5)
+    // (C_X_CS_ROWS / C_X_CS_ROWS_N: rows hashed by k_checksum3 / k_checksum_q16 launches, snapshots included)
     C_X_MERGED = C_NCOUNTERS, C_X_APPLIED, C_X_ISSUED, C_X_CS_ROWS, C_X_CS_DUP,
-    C_X_MERGED_R, C_X_APPLIED_R, C_X_RISSUED, C_X_RCALLS, C_X_BUMPED, C_NALL
+    C_X_MERGED_R, C_X_APPLIED_R, C_X_RISSUED, C_X_RCALLS, C_X_BUMPED, C_X_CS_ROWS_N, C_NALL
 };
 
 constexpr int CTR_SHARDS = 64, CTR_STRIDE = 32;   // d.ctr is [CTR_SHARDS][CTR_STRIDE] u64
+static_assert(C_NALL <= CTR_STRIDE, "counter block too small");
 constexpr uint32_t POOL_SHARDS = 64, POOL_CUR_STRIDE = 16;   // d.pool_cur is [POOL_SHARDS][POOL_CUR_STRIDE] u64
 
 enum ErrBits : uint32_t {
@@ -107,6 +109,16 @@ struct DS {
     uint32_t *wslot;          // [NL] watched row -> slot of wlog, SRC_NONE if unwatched; nullptr: no row watched
     uint4 *wlog;              // [slots][NP] per member, the last change applied since the last drain:
                               // {member word, source, source e, 1}; .w = 0: none
+    // per-Update stream of the watched rows whose slot bit is set in wev_mask (swimsim_watch on = 2): every applied
+    // change in apply order, {member, member word, source, source e}, tagged with its Update's sequence number
+    // (useq of the row when the Update began; all changes of one Update share it, memberlist.go:366-384)
+    uint64_t wev_mask;
+    uint4 *wev;               // [slots][wev_cap]
+    unsigned long long *wevt; // [slots][wev_cap] Update tag
+    uint32_t *wev_cnt;        // [slots] records appended since the last drain (may exceed wev_cap: overflow)
+    uint32_t wev_cap;
+    unsigned long long *useq; // [NL] Update sequence of each row (nullptr: no event stream on); +1 per applying
+                              // Update; phase T's timers take tags above it in (deadline, member) order
     // hot columns: compact copies of the row words and dissemination cells of the members that
     // sit in dissemination buffers, so that issue, merge and bump gather from a few KB per row instead of one
     // 64-B sector per member. hmw[ol][k] == mw[ol][hlist[k]] and hde[ol][k] == dent[ol][hlist[k]] for every

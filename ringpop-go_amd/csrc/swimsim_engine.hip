@@ -36,15 +36,16 @@ struct Timed {
     hipEvent_t a, b;
 };
 
-// F_CHECKSUM times exactly the FarmHash kernel dispatches (k_checksum / k_checksum_n16), one per
-// launch, so its average matches the profiler's per-dispatch average; F_CSPREP is the work around
+// F_CS_WIDE / F_CS_NARROW time exactly the FarmHash kernel dispatches (k_checksum3 / k_checksum_q16), one per
+// launch, so their averages match the profiler's per-dispatch averages; F_CSPREP is the work around
 // them (dirty lists, dedup, deferred-decision lists)
 // F_RECV times exactly the k_recv dispatches (phases D and Q2), so its launch count and average match
 // the profiler's; their deferred-decision epilogues are F_RECVFIN
-enum Fam { F_TIMERS, F_SELECT, F_ISSUE, F_SORT, F_RECV, F_RESP, F_PINGREQ, F_JOBS, F_CHECKSUM, F_CSPREP, F_EVENTS,
-           F_XCHG, F_RECVFIN, F_NFAM };
+enum Fam { F_TIMERS, F_SELECT, F_ISSUE, F_SORT, F_RECV, F_RESP, F_PINGREQ, F_JOBS, F_CS_WIDE, F_CS_NARROW, F_CSPREP,
+           F_EVENTS, F_XCHG, F_RECVFIN, F_NFAM };
 const char *kFamName[F_NFAM] = {"timers", "select", "issue", "sort", "recv_merge", "resp_merge", "pingreq",
-                                "rfs_jobs", "checksum", "checksum_prep", "events", "exchange", "recv_finish"};
+                                "rfs_jobs", "checksum_wide", "checksum_narrow", "checksum_prep", "events", "exchange",
+                                "recv_finish"};
 
 // ---------------------------------------------------------------------------------------------
 // shard transports: how parcels move between the shards of one cluster
@@ -133,10 +134,15 @@ struct LocalPort : Transport {
     }
 };
 
-// one process per GPU: RCCL point-to-point over xGMI, grouped so every pair moves concurrently
+// one process per GPU: RCCL point-to-point over xGMI, grouped so every pair moves concurrently.
+// Every collective of the port is ordered on ONE stream, the engine's main stream (swimsim_comm_attach sets st =
+// h->s, and data() is called with h->s): the size exchange, the segment exchange, the broadcasts and the pack /
+// unpack kernels around them run in issue order, so no RCCL call depends on RCCL serialising communicator
+// operations across streams. data() checks this and orders itself after st if a caller ever passes another stream.
 struct RcclPort : Transport {
     ncclComm_t comm = nullptr;
     hipStream_t st = nullptr;
+    hipEvent_t order = nullptr;
     uint64_t *dsz = nullptr;      // device staging for sizes / broadcasts
     size_t dsz_cap = 0;
     const char *name() const override { return "rccl"; }
@@ -144,6 +150,7 @@ struct RcclPort : Transport {
     ~RcclPort() override {
         if (comm) ncclCommDestroy(comm);
         if (dsz) hipFree(dsz);
+        if (order) hipEventDestroy(order);
     }
     int stage(size_t bytes) {
         if (bytes <= dsz_cap) return 0;
@@ -167,12 +174,19 @@ struct RcclPort : Transport {
     }
     int data(const uint8_t *sbuf, const uint64_t *soff, const uint64_t *sbytes, uint8_t *rbuf, const uint64_t *roff,
              const uint64_t *rbytes, hipStream_t s) override {
+        if (s != st) {                                             // keep one order with sizes() / bcast() on st
+            if (!order && hipEventCreateWithFlags(&order, hipEventDisableTiming) != hipSuccess) return SWIMSIM_EHIP;
+            if (hipEventRecord(order, st) != hipSuccess || hipStreamWaitEvent(s, order, 0) != hipSuccess) return SWIMSIM_EHIP;
+        }
         ncclGroupStart();
         for (uint32_t p = 0; p < G; p++) {
             if (sbytes[p]) ncclSend(sbuf + soff[p], sbytes[p], ncclUint8, (int)p, comm, s);
             if (rbytes[p]) ncclRecv(rbuf + roff[p], rbytes[p], ncclUint8, (int)p, comm, s);
         }
-        return ncclGroupEnd() == ncclSuccess ? 0 : SWIMSIM_EHIP;     // stream-ordered: the unpack follows on s
+        if (ncclGroupEnd() != ncclSuccess) return SWIMSIM_EHIP;    // stream-ordered: the unpack follows on s
+        if (s != st && (hipEventRecord(order, s) != hipSuccess || hipStreamWaitEvent(st, order, 0) != hipSuccess))
+            return SWIMSIM_EHIP;
+        return 0;
     }
     int bcast(void *buf, size_t bytes, uint32_t root) override {
         if (int rc = stage(bytes)) return rc;
@@ -309,6 +323,7 @@ struct swimsim {
     std::vector<uint32_t> wslot_h;                // [NL] slot or SRC_NONE
     std::vector<uint8_t> wused;                   // [kWatchCap]
     std::vector<uint32_t> wcs;                    // checksum at the last drain (OldChecksum), per slot
+    std::vector<uint32_t> wcs_ev;                 // the same for the per-Update stream's drains
     uint4 *wout = nullptr;
     uint32_t *winfo = nullptr;
     std::string err;
@@ -623,7 +638,7 @@ int shard_sum(swimsim *h, uint64_t v, uint64_t *out) {
 // distinct content: rows are grouped by fingerprint, compared word for word with their group's first
 // row, and equal rows copy its checksum (k_fp_*).
 // one FarmHash dispatch over the rows listed (count on the device; nrows = the count if the host
-// knows it, else ~0u), timed as F_CHECKSUM
+// knows it, else ~0u), timed as F_CS_WIDE / F_CS_NARROW
 // A main-stream launch of a known number of rows (at least 64) hashes them in row order: lists come out of atomic
 // compactions in arbitrary order, and a workgroup whose lanes stream rows spread over the 16 GB of row words (or
 // over the snapshot pool) touches as many distant pages per load, so address translation, not bandwidth or issue,
@@ -641,8 +656,10 @@ void hash_rows(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t m
                                               h->s) == hipSuccess)
             list = out;
     }
-    Scope sc(h, F_CHECKSUM, st);
-    launch_checksum(h->d, list, cnt, maxn, nrows, st ? st : h->s);
+    const uint32_t n = std::min(maxn, nrows);
+    const CsKind kind = cs_kind(n);
+    Scope sc(h, kind == CS_WIDE ? F_CS_WIDE : F_CS_NARROW, st);
+    launch_checksum_kind(h->d, list, cnt, n, kind, st ? st : h->s);
 }
 
 // hot columns: forget every hot member (raw row writes bypass the copies)
@@ -1301,8 +1318,6 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
         return bail(SWIMSIM_EHIP);
     }
     if (const char *v = getenv("SWIMSIM_CS_ASYNC")) h->cs_async = atoi(v) != 0;
-    if (const char *v = getenv("SWIMSIM_CS_KERNEL")) g_cs_kernel = atoi(v);
-    if (const char *v = getenv("SWIMSIM_CS_NARROW")) g_cs_narrow = atoi(v);
     if (const char *v = getenv("SWIMSIM_CS_NARROW_ROWS")) g_cs_narrow_rows = (uint32_t)strtoul(v, nullptr, 10);
     DS &d = h->d;
     d.N = h->N; d.NP = h->NP; d.NL = h->NL; d.lo = h->lo;
@@ -1828,15 +1843,26 @@ __global__ void k_iota(uint32_t *list, uint32_t *cnt, uint32_t n) {
     if (i < n) list[i] = i;
 }
 
+// mode 0: the production choice for nrows rows; 1: k_checksum3; 2: k_checksum_q16 (both production kernels).
+// Other modes (superseded kernels, diagnostic variants) exist only in the diagnostics library.
 int swimsim_bench_checksum(swimsim_t *h, uint32_t nrows, int32_t mode, int32_t reps, double *ms) {
     if (!h || !ms || nrows == 0 || nrows > h->NL || reps < 1) return SWIMSIM_EINVAL;
+#ifndef SWIMSIM_DIAG
+    if (mode < 0 || mode > 2) return h->fail(SWIMSIM_EINVAL, "checksum mode %d: diagnostics build only", mode);
+#endif
+    auto launch = [&]() {
+        if (mode <= 2) launch_checksum_kind(h->d, h->list, h->cnt, nrows, mode == 0 ? cs_kind(nrows) : (CsKind)mode, h->s);
+#ifdef SWIMSIM_DIAG
+        else launch_checksum_mode(h->d, h->list, h->cnt, nrows, mode, h->s);
+#endif
+    };
     hipLaunchKernelGGL(k_iota, dim3(blocks_for_threads(nrows)), dim3(256), 0, h->s, h->list, h->cnt, nrows);
     hipEvent_t a, b;
     HIPCHK(h, hipEventCreate(&a));
     HIPCHK(h, hipEventCreate(&b));
-    launch_checksum_mode(h->d, h->list, h->cnt, nrows, mode, h->s);   // warm-up
+    launch();                                                          // warm-up
     HIPCHK(h, hipEventRecord(a, h->s));
-    for (int i = 0; i < reps; i++) launch_checksum_mode(h->d, h->list, h->cnt, nrows, mode, h->s);
+    for (int i = 0; i < reps; i++) launch();
     HIPCHK(h, hipEventRecord(b, h->s));
     HIPCHK(h, hipEventSynchronize(b));
     float t = 0;
@@ -1849,6 +1875,9 @@ int swimsim_bench_checksum(swimsim_t *h, uint32_t nrows, int32_t mode, int32_t r
 
 int swimsim_debug_cs_stream(swimsim_t *h, uint32_t ol, uint32_t *out, size_t cap_words) {
     if (!h || !out || ol >= h->NL || cap_words == 0) return SWIMSIM_EINVAL;
+#ifndef SWIMSIM_DIAG
+    return h->fail(SWIMSIM_EINVAL, "swimsim_debug_cs_stream: diagnostics build only (tools/libswimsim_diag.so)");
+#else
     uint32_t *dev = nullptr;
     HIPCHK(h, hipMalloc(&dev, cap_words * 4));
     HIPCHK(h, hipMemsetAsync(dev, 0xEE, cap_words * 4, h->s));
@@ -1861,6 +1890,21 @@ int swimsim_debug_cs_stream(swimsim_t *h, uint32_t ol, uint32_t *out, size_t cap
     HIPCHK(h, hipStreamSynchronize(h->s));
     hipFree(dev);
     return check_err(h);
+#endif
+}
+
+// profiler window marker: one tiny dispatch on the engine's stream, so that rocprofv3 counter passes can be cut to
+// exactly the launches between two marks (tools/pmc_summary.py --window; bench.py marks its timed rounds)
+__global__ void k_profile_mark(uint32_t id, uint32_t *sink) {
+    if (threadIdx.x == 0 && id == 0xFFFFFFFFu) sink[0] = id;
+}
+
+int swimsim_profile_mark(swimsim_t *h, uint32_t id) {
+    if (!h) return SWIMSIM_EINVAL;
+    if (int rc = sync_side(h)) return rc;
+    hipLaunchKernelGGL(k_profile_mark, dim3(1), dim3(64), 0, h->s, id, h->scratch);
+    HIPCHK(h, hipStreamSynchronize(h->s));
+    return SWIMSIM_OK;
 }
 
 // ---- applied-change stream: MemberlistChangesAppliedEvent (swim/events.go:56-61) ----
@@ -1882,6 +1926,18 @@ int swimsim_watch(swimsim_t *h, uint32_t o, int32_t on) {
         h->wused.assign(kWatchCap, 0);
         h->wcs.assign(kWatchCap, 0);
     }
+    if (on == 2 && !h->d.useq) {                                   // the per-Update stream's buffers, on first use
+        int rc = 0;
+        h->d.wev_cap = std::max<uint32_t>(4u * h->NP, 4096u);
+        if ((rc = dalloc(h, &h->d.wev, (size_t)kWatchCap * h->d.wev_cap, "per-Update event log")) ||
+            (rc = dalloc(h, &h->d.wevt, (size_t)kWatchCap * h->d.wev_cap, "per-Update event tags")) ||
+            (rc = dalloc(h, &h->d.wev_cnt, kWatchCap, "per-Update event counts")) ||
+            (rc = dalloc(h, &h->d.useq, h->NL, "Update sequence")))
+            return rc;
+        HIPCHK(h, hipMemsetAsync(h->d.wev_cnt, 0, kWatchCap * 4, h->s));
+        HIPCHK(h, hipMemsetAsync(h->d.useq, 0, (size_t)h->NL * 8, h->s));
+        h->wcs_ev.assign(kWatchCap, 0);
+    }
     uint32_t slot = h->wslot_h[ol];
     if (on && slot == SRC_NONE) {
         for (slot = 0; slot < kWatchCap && h->wused[slot]; slot++) {}
@@ -1899,7 +1955,79 @@ int swimsim_watch(swimsim_t *h, uint32_t o, int32_t on) {
         HIPCHK(h, hipStreamSynchronize(h->s));
         h->wused[slot] = 0;
         h->wslot_h[ol] = SRC_NONE;
+        h->d.wev_mask &= ~(1ull << slot);
+        return SWIMSIM_OK;
     }
+    if (on == 2 && !((h->d.wev_mask >> slot) & 1ull)) {                // the per-Update stream starts empty now
+        if (int rc = checksum_dirty(h, 0)) return rc;
+        HIPCHK(h, hipMemsetAsync(h->d.wev_cnt + slot, 0, 4, h->s));
+        HIPCHK(h, hipMemcpyAsync(&h->wcs_ev[slot], h->d.cs + ol, 4, hipMemcpyDeviceToHost, h->s));
+        HIPCHK(h, hipStreamSynchronize(h->s));
+        h->d.wev_mask |= 1ull << slot;
+    } else if (on == 1) {
+        h->d.wev_mask &= ~(1ull << slot);
+    }
+    return SWIMSIM_OK;
+}
+
+// the per-Update stream of watched row o (swimsim_watch on = 2): every applied change since the last drain, one
+// event per applying Update (memberlist.go:366-384), events in the row's Update order, changes of an event in
+// member order
+int swimsim_applied_events(swimsim_t *h, uint32_t o, int32_t *member, int32_t *status, int64_t *inc_ms, int32_t *source,
+                           int64_t *source_inc_ms, uint32_t *event, size_t cap, size_t *n, size_t *nevents,
+                           uint32_t *old_checksum, uint32_t *new_checksum, int32_t *num_members) {
+    if (!h || !own(h, o)) return SWIMSIM_EINVAL;
+    const uint32_t ol = o - h->lo;
+    if (!h->d.wslot || h->wslot_h[ol] == SRC_NONE || !((h->d.wev_mask >> h->wslot_h[ol]) & 1ull))
+        return h->fail(SWIMSIM_EINVAL, "observer %u has no per-Update event stream (swimsim_watch on = 2)", o);
+    const uint32_t slot = h->wslot_h[ol];
+    if (int rc = checksum_dirty(h, 0)) return rc;
+    uint32_t cnt = 0, cs = 0;
+    HIPCHK(h, hipMemsetAsync(h->winfo, 0, 8, h->s));
+    hipLaunchKernelGGL(k_row_known, dim3(1), dim3(64), 0, h->s, h->d, ol, h->winfo);
+    HIPCHK(h, hipMemcpyAsync(&cnt, h->d.wev_cnt + slot, 4, hipMemcpyDeviceToHost, h->s));
+    HIPCHK(h, hipMemcpyAsync(&cs, h->d.cs + ol, 4, hipMemcpyDeviceToHost, h->s));
+    uint32_t known = 0;
+    HIPCHK(h, hipMemcpyAsync(&known, h->winfo, 4, hipMemcpyDeviceToHost, h->s));
+    HIPCHK(h, hipStreamSynchronize(h->s));
+    if (cnt > h->d.wev_cap) {
+        HIPCHK(h, hipMemsetAsync(h->d.wev_cnt + slot, 0, 4, h->s));
+        h->wcs_ev[slot] = cs;
+        return h->fail(SWIMSIM_ECAPACITY, "per-Update event log of observer %u overflowed (%u changes, capacity %u): "
+                       "drain more often", o, cnt, h->d.wev_cap);
+    }
+    std::vector<uint4> rec(cnt);
+    std::vector<unsigned long long> tag(cnt);
+    if (cnt) {
+        HIPCHK(h, hipMemcpyAsync(rec.data(), h->d.wev + (size_t)slot * h->d.wev_cap, (size_t)cnt * 16, hipMemcpyDeviceToHost, h->s));
+        HIPCHK(h, hipMemcpyAsync(tag.data(), h->d.wevt + (size_t)slot * h->d.wev_cap, (size_t)cnt * 8, hipMemcpyDeviceToHost, h->s));
+    }
+    HIPCHK(h, hipMemsetAsync(h->d.wev_cnt + slot, 0, 4, h->s));
+    HIPCHK(h, hipStreamSynchronize(h->s));
+    std::vector<uint32_t> ord(cnt);
+    for (uint32_t i = 0; i < cnt; i++) ord[i] = i;
+    std::sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) {
+        return tag[a] != tag[b] ? tag[a] < tag[b] : rec[a].x < rec[b].x;
+    });
+    size_t ev = 0;
+    for (uint32_t k = 0; k < cnt; k++) {
+        const uint32_t i = ord[k];
+        if (k && tag[i] != tag[ord[k - 1]]) ev++;
+        if (k >= cap) continue;
+        const uint4 v = rec[i];
+        if (member) member[k] = (int32_t)v.x;
+        if (status) status[k] = (int32_t)(v.y & 7u);
+        if (inc_ms) inc_ms[k] = from_e(h, v.y >> 3);
+        if (source) source[k] = v.z == SRC_NONE ? -1 : (int32_t)v.z;
+        if (source_inc_ms) source_inc_ms[k] = v.z == SRC_NONE ? 0 : from_e(h, v.w);
+        if (event) event[k] = (uint32_t)ev;
+    }
+    if (n) *n = cnt;
+    if (nevents) *nevents = cnt ? ev + 1 : 0;
+    if (old_checksum) *old_checksum = h->wcs_ev[slot];
+    if (new_checksum) *new_checksum = cs;
+    if (num_members) *num_members = (int32_t)known;
+    h->wcs_ev[slot] = cs;
     return SWIMSIM_OK;
 }
 
@@ -2030,8 +2158,11 @@ int swimsim_kernel_times(swimsim_t *h, const char **names, double *avg_ms, uint6
     // recv_merge (k_recv): its merges + IssueAsReceiver: 16 B entry gather + 16 B record write + 4 B counter
     // write-back per issued record, and the 4 B-per-32-members presence bitmap per call.
     // resp_merge (k_resp): its merges + bumpPiggybackCounters: 16 B record read + 4 B counter read and write.
-    const double merge_bytes = merged * 20.0 + applied * 22.0;
-    const double resp_bytes = delta(C_X_MERGED_R) * 20.0 + delta(C_X_APPLIED_R) * 22.0 + delta(C_X_BUMPED) * 24.0;
+    // merge = 17 B change entry + 5 B row read per processed change, + 5 B row write + 9 B
+    // dissemination entry + 9 B timer per applied change; checksum = 5 B (status + incarnation) per member per hashed
+    // row. IssueAsReceiver's bytes are beside them (swimsim_kernel_units has every count apart)
+    const double merge_bytes = merged * 22.0 + applied * 23.0;
+    const double resp_bytes = delta(C_X_MERGED_R) * 22.0 + delta(C_X_APPLIED_R) * 23.0 + delta(C_X_BUMPED) * 24.0;
     const double recv_issue_bytes = delta(C_X_RISSUED) * 36.0 + delta(C_X_RCALLS) * 4.0 * h->d.NBIT;
     for (int f = 0; f < F_NFAM && (size_t)f < cap; f++) {
         if (names) names[f] = kFamName[f];
@@ -2039,7 +2170,8 @@ int swimsim_kernel_times(swimsim_t *h, const char **names, double *avg_ms, uint6
         if (launches) launches[f] = h->fam_n[f];
         if (alg_bytes) {
             double b = 0;
-            if (f == F_CHECKSUM) b = csrows * 4.0 * h->N;      // member words of every hashed row
+            if (f == F_CS_WIDE) b = csrows * 5.0 * h->N;       // every hashed row, SURVEY.md §8(d) 5 B per member
+            if (f == F_CS_NARROW) b = delta(C_X_CS_ROWS_N) * 5.0 * h->N;
             if (f == F_CSPREP) b = csdups * 8.0 * h->N;        // duplicates verified word for word
             if (f == F_ISSUE) b = issued * 32.0;
             if (f == F_RECV) b = merge_bytes + recv_issue_bytes;   // k_recv merges (and the few other
@@ -2048,6 +2180,25 @@ int swimsim_kernel_times(swimsim_t *h, const char **names, double *avg_ms, uint6
         }
     }
     if (n) *n = F_NFAM;
+    return SWIMSIM_OK;
+}
+
+// unit counts behind swimsim_kernel_times' byte figures, since the last swimsim_enable_timing
+int swimsim_kernel_units(swimsim_t *h, const char **names, double *values, size_t cap, size_t *n) {
+    if (!h) return SWIMSIM_EINVAL;
+    uint64_t c[CTR_STRIDE];
+    if (int rc = read_counters(h, c)) return rc;
+    static const char *kn[] = {"cs_rows_wide", "cs_rows_narrow", "cs_dup_rows", "recv_merged", "recv_applied",
+                               "recv_issued", "recv_calls", "resp_merged", "resp_applied", "resp_bumped", "issued",
+                               "bitmap_words_per_row"};
+    const int ki[] = {C_X_CS_ROWS, C_X_CS_ROWS_N, C_X_CS_DUP, C_X_MERGED, C_X_APPLIED, C_X_RISSUED, C_X_RCALLS,
+                      C_X_MERGED_R, C_X_APPLIED_R, C_X_BUMPED, C_X_ISSUED, -1};
+    const size_t k = sizeof(ki) / sizeof(ki[0]);
+    for (size_t i = 0; i < k && i < cap; i++) {
+        if (names) names[i] = kn[i];
+        if (values) values[i] = ki[i] < 0 ? (double)h->d.NBIT : (double)(c[ki[i]] - h->fam_bytes_base[ki[i]]);
+    }
+    if (n) *n = k;
     return SWIMSIM_OK;
 }
 

@@ -7,8 +7,10 @@ namespace swimdev {
 // picks the latency (few rows) or the throughput variant
 void launch_checksum(const DS &d, const uint32_t *list, const uint32_t *count, uint32_t maxn, uint32_t nrows,
                      hipStream_t s);
+#ifdef SWIMSIM_DIAG   // diagnostics library only (tools/diag)
 void launch_checksum_dump(const DS &d, const uint32_t *list, const uint32_t *count, uint32_t *dbg, uint32_t cap,
                           hipStream_t s);
 void launch_checksum_mode(const DS &d, const uint32_t *list, const uint32_t *count, uint32_t maxn, int mode,
                           hipStream_t s);
+#endif
 }

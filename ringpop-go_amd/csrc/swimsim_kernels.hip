@@ -50,8 +50,15 @@ __device__ __forceinline__ bool reach(const DS &d, uint32_t a, uint32_t b) {
 struct MAcc {
     int dping, ddc, napp, nref, nproc, evict, dlen, maxlast, inval;
     unsigned long long dfp;   // row fingerprint delta
-    __device__ MAcc() : dping(0), ddc(0), napp(0), nref(0), nproc(0), evict(0), dlen(0), maxlast(-1), inval(0), dfp(0) {}
+    unsigned long long tag;   // Update tag of the per-Update event stream (d.useq of the row at the Update's start)
+    __device__ MAcc() : dping(0), ddc(0), napp(0), nref(0), nproc(0), evict(0), dlen(0), maxlast(-1), inval(0), dfp(0),
+                        tag(0) {}
 };
+
+// start of one Update on row ol: its changes carry the row's current sequence number (event stream only)
+__device__ __forceinline__ void acc_begin(const DS &d, uint32_t ol, MAcc &acc) {
+    if (d.useq) acc.tag = d.useq[ol];
+}
 
 // bytes of one member's checksum record addr ‖ status ‖ decimal(inc) ‖ ';' (memberlist.go:115-121);
 // tombstones and unknown members contribute nothing (memberlist.go:112-114)
@@ -114,7 +121,16 @@ __device__ __forceinline__ void merge_change_w(const DS &d, uint32_t ol, uint32_
     if (hk != SRC_NONE) d.hde[hx] = cell;
     if (d.wslot) {                                                 // watched row: MemberlistChangesAppliedEvent
         const uint32_t ws = d.wslot[ol];                           // (memberlist.go:378-383)
-        if (ws != SRC_NONE) d.wlog[(size_t)ws * d.NP + m] = make_uint4(nw_, nsrc, nsinc, 1u);
+        if (ws != SRC_NONE) {
+            d.wlog[(size_t)ws * d.NP + m] = make_uint4(nw_, nsrc, nsinc, 1u);
+            if ((d.wev_mask >> ws) & 1ull) {                       // per-Update stream: append in apply order
+                const uint32_t at = atomicAdd(d.wev_cnt + ws, 1u);
+                if (at < d.wev_cap) {
+                    d.wev[(size_t)ws * d.wev_cap + at] = make_uint4(m, nw_, nsrc, nsinc);
+                    d.wevt[(size_t)ws * d.wev_cap + at] = acc.tag;
+                }
+            }
+        }
     }
     if (m != o) {                                                  // no timers for the local member
         const uint8_t ts = d.tst[idx];
@@ -138,7 +154,8 @@ __device__ __forceinline__ void merge_change(const DS &d, uint32_t ol, uint32_t 
 }
 
 __device__ __forceinline__ void fold_row(const DS &d, uint32_t ol, int dping, int ddc, int napp, int nref, int evict,
-                                         int dlen, int maxlast, int inval, unsigned long long dfp) {
+                                         int dlen, int maxlast, int inval, unsigned long long dfp, bool next_update = true) {
+    if (napp && next_update && d.useq) d.useq[ol] += 1ull;          // the next Update of this row takes the next tag
     if (dfp) d.fp[ol] += dfp;
     if (dping) d.ping[ol] += dping;
     if (ddc) d.dcnt[ol] += ddc;
@@ -159,7 +176,7 @@ __device__ __forceinline__ int wmax(int v) {
     return v;
 }
 
-__device__ __forceinline__ void wave_finalize(const DS &d, uint32_t ol, const MAcc &acc, int cset = 0) {
+__device__ __forceinline__ void wave_finalize(const DS &d, uint32_t ol, const MAcc &acc, int cset = 0, bool next_update = true) {
     const int dping = wsum(acc.dping), ddc = wsum(acc.ddc), napp = wsum(acc.napp), nref = wsum(acc.nref);
     const int ev = wsum(acc.evict), np = wsum(acc.nproc), dl = wsum(acc.dlen), ml = wmax(acc.maxlast);
     const int inv = wmax(acc.inval);
@@ -167,7 +184,7 @@ __device__ __forceinline__ void wave_finalize(const DS &d, uint32_t ol, const MA
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) dfp += __shfl_xor(dfp, off, 64);
     if (lane_id() == 0) {
-        fold_row(d, ol, dping, ddc, napp, nref, ev, dl, ml, inv, dfp);
+        fold_row(d, ol, dping, ddc, napp, nref, ev, dl, ml, inv, dfp, next_update);
         if (np && cset < 2) ctr_add(d, cset ? C_X_MERGED_R : C_X_MERGED, (unsigned long long)np);
         if (napp && cset < 2) ctr_add(d, cset ? C_X_APPLIED_R : C_X_APPLIED, (unsigned long long)napp);
     }
@@ -208,6 +225,7 @@ __device__ __forceinline__ void wave_merge_dense(const DS &d, uint32_t ol, uint3
 __device__ void wave_merge_msg(const DS &d, uint32_t ol, uint32_t o, const MsgDesc &md, uint32_t now_e, uint32_t sched_r,
                                int cset = 0) {
     MAcc acc;
+    acc_begin(d, ol, acc);
     const uint32_t *rowp = d.mw + (size_t)ol * d.NP;
     const uint32_t *hrow = d.hmw + (size_t)ol * d.HP;
     if (md.kind == 0) {
@@ -590,6 +608,7 @@ __global__ void k_add_join_list(DS d, uint32_t ol, const uint4 *__restrict__ rec
     const uint32_t o = d.lo + ol;
     const uint32_t *rowp = d.mw + (size_t)ol * d.NP;
     MAcc acc;
+    acc_begin(d, ol, acc);
     for (uint32_t base = 0; base < n; base += 64 * MB) {
         uint4 c[MB];
         uint32_t cur[MB];
@@ -628,6 +647,7 @@ __global__ void k_add_join_list(DS d, uint32_t ol, const uint4 *__restrict__ rec
 // returns the number of applied changes (0/1)
 __device__ int thread_make_change(const DS &d, uint32_t ol, uint32_t o, uint32_t m, uint32_t e, uint32_t st, uint32_t r) {
     MAcc acc;
+    acc_begin(d, ol, acc);
     const uint32_t self_e = d.mw[(size_t)ol * d.NP + o] >> 3;   // MakeChange: SourceIncarnation = local inc
     merge_change(d, ol, o, m, st, e, o, self_e, r, r, acc);
     fold_row(d, ol, acc.dping, acc.ddc, acc.napp, acc.nref, 0, acc.dlen, acc.maxlast, acc.inval, acc.dfp);
@@ -674,6 +694,10 @@ __global__ void k_timers(DS d, uint32_t r) {
     if (!d.live[o] || d.tmin[ol] > r) return;
     const uint32_t self_e = d.mw[(size_t)ol * d.NP + o] >> 3;
     MAcc acc;
+    // every fired timer is its own one-change Update (MakeFaulty / MakeTombstone), in (deadline, member) order
+    // (clock.Mock fires in deadline order; equal deadlines by member, docs/ROUND_SEMANTICS.md): event tags above
+    // the row's sequence number, ordered by (deadline, member); the row's next Update then tags above them all
+    const unsigned long long tbase = d.useq ? d.useq[ol] : 0ull;
     uint32_t newmin = NO_DEADLINE;   // per-lane partial minimum, reduced at the end
     int fired = 0;
     for (uint32_t b0 = 0; b0 < d.NB; b0 += 64) {
@@ -694,6 +718,7 @@ __global__ void k_timers(DS d, uint32_t r) {
             if (state && !(ts & 0x80) && a.x <= r) {
                 d.tst[idx] = ts | 0x80;                             // fired; the entry stays
                 fired++;
+                acc.tag = tbase + ((0xFFFFull - min(r - a.x, 0xFFFFu)) << 24) + m;
                 if (state == ST_SUSPECT) merge_change(d, ol, o, m, ST_FAULTY, a.y, o, self_e, r, a.x, acc);   // MakeFaulty
                 else if (state == ST_FAULTY) merge_change(d, ol, o, m, ST_TOMB, a.y, o, self_e, r, a.x, acc); // MakeTombstone
                 else {                                              // Evict (memberlist.go:271-279)
@@ -721,8 +746,10 @@ __global__ void k_timers(DS d, uint32_t r) {
     if (lane_id() == 0) d.tmin[ol] = newmin;
     fired = wsum(fired);
     if (lane_id() == 0 && fired) ctr_add(d, C_TIMERS_FIRED, (unsigned long long)fired);
+    const int napp_t = wsum(acc.napp);
+    if (lane_id() == 0 && napp_t && d.useq) d.useq[ol] = tbase + (1ull << 40);
     __threadfence_block();
-    wave_finalize(d, ol, acc);
+    wave_finalize(d, ol, acc, 0, false);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1319,10 +1346,7 @@ __global__ void k_snap_dups(DS d, const uint32_t *vals, uint32_t n, const uint32
 
 __global__ void k_side_scatter(DS d, const uint2 *map, uint32_t n, uint32_t nhashed) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i == 0) {
-        ctr_add(d, C_X_CS_ROWS, (unsigned long long)nhashed);
-        ctr_add(d, C_X_CS_DUP, (unsigned long long)(n - nhashed));
-    }
+    if (i == 0) ctr_add(d, C_X_CS_DUP, (unsigned long long)(n - nhashed));   // (hashed rows: counted by the kernels)
     if (i >= n) return;
     const uint2 e = map[i];
     d.cs[e.x] = d.dense_cs[e.y];
@@ -1424,6 +1448,14 @@ __global__ void k_ping_with(DS d, uint32_t tol, uint32_t sender, const MsgDesc *
 // ---------------------------------------------------------------------------------------------
 // readback helpers
 // ---------------------------------------------------------------------------------------------
+// NumMembers of row ol (memberlist.go:174-179): out[0] = members known
+__global__ void k_row_known(DS d, uint32_t ol, uint32_t *out) {
+    int known = 0;
+    for (uint32_t m = lane_id(); m < d.N; m += 64) known += (d.mw[(size_t)ol * d.NP + m] & 7u) != ST_UNKNOWN;
+    known = wsum(known);
+    if (lane_id() == 0) out[0] = (uint32_t)known;
+}
+
 // drain the applied-change log of watched row ol (slot): out[i] = {member, member word, source, source e}
 // in member order, the flags cleared; info = {count, NumMembers}. One 1024-thread workgroup: each thread
 // takes a contiguous run of members, a block scan of the run counts places the records.

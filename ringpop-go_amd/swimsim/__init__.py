@@ -95,10 +95,12 @@ _lib = None
 
 
 def load_library(path: str = LIB_PATH):
-    """Load libswimsim.so. Raises loudly when it is absent: the product has no fallback."""
+    """Load libswimsim.so. Raises loudly when it is absent: the product has no fallback. SWIMSIM_LIBRARY selects
+    another build of the same ABI (tools/: the diagnostics library with the superseded checksum kernels)."""
     global _lib
     if _lib is not None:
         return _lib
+    path = os.environ.get("SWIMSIM_LIBRARY", path)
     if not os.path.exists(path):
         raise SwimsimError(f"{path} is missing: build it with `make -C ringpop-go_amd` (hipcc, gfx950)")
     L = C.CDLL(path)
@@ -136,6 +138,8 @@ def load_library(path: str = LIB_PATH):
         "swimsim_kernel_times": (C.c_int, [P, P, P, P, P, sz, C.POINTER(sz)]),
         "swimsim_enable_timing": (C.c_int, [P, i32]),
         "swimsim_bench_checksum": (C.c_int, [P, u32, i32, i32, C.POINTER(C.c_double)]),
+        "swimsim_kernel_units": (C.c_int, [P, P, P, sz, C.POINTER(sz)]),
+        "swimsim_profile_mark": (C.c_int, [P, u32]),
         "swimsim_debug_cs_stream": (C.c_int, [P, u32, P, sz]),
         "swimsim_group_create": (C.c_int, [C.POINTER(Config), u32, P, P]),
         "swimsim_group_step": (C.c_int, [P, u32, u32, C.POINTER(Event), sz]),
@@ -148,6 +152,8 @@ def load_library(path: str = LIB_PATH):
         "swimsim_watch": (C.c_int, [P, u32, i32]),
         "swimsim_applied_changes": (C.c_int, [P, u32, P, P, P, P, P, sz, C.POINTER(sz), C.POINTER(u32),
                                               C.POINTER(u32), C.POINTER(i32)]),
+        "swimsim_applied_events": (C.c_int, [P, u32, P, P, P, P, P, P, sz, C.POINTER(sz), C.POINTER(sz),
+                                             C.POINTER(u32), C.POINTER(u32), C.POINTER(i32)]),
         "swimsim_protocol_stats": (C.c_int, [P, C.POINTER(ProtocolStatsC)]),
         "swimsim_memory": (C.c_int, [P, C.POINTER(MemoryC)]),
     }
@@ -292,7 +298,25 @@ class Cluster:
 
     # ---- applied-change stream (MemberlistChangesAppliedEvent, swim/events.go:56-61) ----------
     def watch(self, o, on=True):
-        self._chk(load_library().swimsim_watch(self.h, o, int(on)))
+        """on: True = the coalesced drain (applied_changes); "events" = also the per-Update stream (applied_events);
+        False = off"""
+        self._chk(load_library().swimsim_watch(self.h, o, 2 if on == "events" else int(bool(on))))
+
+    def applied_events(self, o):
+        """drain the per-Update stream of observer o (watch(o, "events")): ([[(member, status, inc, source,
+        source_inc)] per applying Update, in the node's Update order; changes in member order], old checksum,
+        new checksum, NumMembers), the checksums and NumMembers per drain"""
+        cap = 4 * self.n + 4096
+        m = np.empty(cap, np.int32); st = np.empty(cap, np.int32); inc = np.empty(cap, np.int64)
+        s = np.empty(cap, np.int32); si = np.empty(cap, np.int64); ev = np.empty(cap, np.uint32)
+        n, ne, old, new, nm = C.c_size_t(), C.c_size_t(), C.c_uint32(), C.c_uint32(), C.c_int32()
+        self._chk(load_library().swimsim_applied_events(self.h, o, m.ctypes.data, st.ctypes.data, inc.ctypes.data,
+                                                        s.ctypes.data, si.ctypes.data, ev.ctypes.data, cap, C.byref(n),
+                                                        C.byref(ne), C.byref(old), C.byref(new), C.byref(nm)))
+        events = [[] for _ in range(ne.value)]
+        for i in range(n.value):
+            events[int(ev[i])].append((int(m[i]), int(st[i]), int(inc[i]), int(s[i]), int(si[i])))
+        return events, old.value, new.value, nm.value
 
     def applied_changes(self, o):
         """drain watched observer o: ([(member, status, inc, source, source_inc)] in member order, old checksum,
@@ -482,6 +506,20 @@ class Cluster:
         return {names[i].decode(): {"avg_ms": float(avg[i]), "launches": int(n_l[i]), "alg_bytes": float(byt[i])}
                 for i in range(n.value)}
 
+    def kernel_units(self):
+        """unit counts behind kernel_times' bytes since enable_timing: rows hashed per checksum kernel, changes
+        processed / applied per merge kernel, records issued, ..."""
+        cap = 32
+        names = (C.c_char_p * cap)()
+        vals = np.zeros(cap, np.float64)
+        n = C.c_size_t()
+        self._chk(load_library().swimsim_kernel_units(self.h, names, vals.ctypes.data, cap, C.byref(n)))
+        return {names[i].decode(): float(vals[i]) for i in range(n.value)}
+
+    def profile_mark(self, mark_id):
+        """one k_profile_mark dispatch: rocprofv3 counter passes are cut between two marks (tools/pmc_summary.py)"""
+        self._chk(load_library().swimsim_profile_mark(self.h, mark_id))
+
     def shard_info(self):
         g, r, lo, hi = C.c_uint32(), C.c_uint32(), C.c_uint32(), C.c_uint32()
         xb, xc = C.c_uint64(), C.c_uint64()
@@ -577,6 +615,9 @@ class ShardedCluster:
     def applied_changes(self, o):
         return self.owner(o).applied_changes(o)
 
+    def applied_events(self, o):
+        return self.owner(o).applied_events(o)
+
     def register_listener(self, o, listener):
         self.owner(o).register_listener(o, listener)
 
@@ -641,6 +682,20 @@ class ShardedCluster:
         cs = self.checksums()
         live = [o for o in range(self.n) if self.live[o]]
         return all(c.converged() for c in self.shards) and len(set(int(cs[o]) for o in live)) <= 1
+
+    def kernel_units(self):
+        """unit counts behind kernel_times' bytes since enable_timing: rows hashed per checksum kernel, changes
+        processed / applied per merge kernel, records issued, ..."""
+        cap = 32
+        names = (C.c_char_p * cap)()
+        vals = np.zeros(cap, np.float64)
+        n = C.c_size_t()
+        self._chk(load_library().swimsim_kernel_units(self.h, names, vals.ctypes.data, cap, C.byref(n)))
+        return {names[i].decode(): float(vals[i]) for i in range(n.value)}
+
+    def profile_mark(self, mark_id):
+        """one k_profile_mark dispatch: rocprofv3 counter passes are cut between two marks (tools/pmc_summary.py)"""
+        self._chk(load_library().swimsim_profile_mark(self.h, mark_id))
 
     def shard_info(self):
         return [c.shard_info() for c in self.shards]

@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU session script: each step under its own time limit; stop at the first failing step.
-# usage: run_gpu.sh [tests|smoke|bench|prof|pmc|all ...]   (several modes run in the order given)
+# usage: run_gpu.sh [tests|smoke|bench|prof|pmc|calib|all ...]   (several modes run in the order given)
 # BENCH_ARGS defaults to the driver's round-end command (--steps 20 --warmup 5); prof and pmc profile
 # exactly that command, so profiles/ figures and the bench line describe the same workload.
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -29,18 +29,29 @@ for mode in "$@"; do
     timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv \
       -- python3 bench.py $PROF_ARGS > gpurun_out/prof.log 2>&1
     rc=$?; echo "rocprof rc=$rc" >> gpurun_out/prof.log; [ $rc -eq 0 ] || exit $rc
+    python3 tools/prof_window.py $(ls gpurun_out/prof/*/run_kernel_trace.csv gpurun_out/prof/run_kernel_trace.csv 2>/dev/null | head -n 1) \
+      gpurun_out/prof_window_stats.csv || exit 1
     ;;&
   pmc|all)
-    timeout -k 10 -s KILL 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run \
-      --output-format csv -- python3 bench.py $PROF_ARGS > gpurun_out/pmc_fetch.log 2>&1
-    rc=$?; echo "pmc fetch rc=$rc" >> gpurun_out/pmc_fetch.log; [ $rc -eq 0 ] || exit $rc
-    timeout -k 10 -s KILL 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run \
-      --output-format csv -- python3 bench.py $PROF_ARGS > gpurun_out/pmc_write.log 2>&1
-    rc=$?; echo "pmc write rc=$rc" >> gpurun_out/pmc_write.log; [ $rc -eq 0 ] || exit $rc
-    timeout -k 10 -s KILL 400 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVES GRBM_GUI_ACTIVE --kernel-trace \
-      -d gpurun_out/pmc_valu -o run --output-format csv -- python3 bench.py $PROF_ARGS > gpurun_out/pmc_valu.log 2>&1
-    rc=$?; echo "pmc valu rc=$rc" >> gpurun_out/pmc_valu.log; [ $rc -eq 0 ] || exit $rc
-    python3 tools/pmc_summary.py --workload $WL gpurun_out/pmc_summary.json gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc_valu
+    # separate passes (a pass holds at most 8 SQ / 4 TCC counters), each cut to the timed rounds (--window)
+    i=0
+    for pass in "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVES GRBM_GUI_ACTIVE" \
+                "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS" \
+                "TCC_HIT_sum TCC_MISS_sum"; do
+      i=$((i+1))
+      timeout -k 10 -s KILL 400 rocprofv3 --pmc $pass --kernel-trace -d gpurun_out/pmc_$i -o run \
+        --output-format csv -- python3 bench.py $PROF_ARGS > gpurun_out/pmc_$i.log 2>&1
+      rc=$?; echo "pmc pass $i ($pass) rc=$rc" >> gpurun_out/pmc_$i.log; [ $rc -eq 0 ] || exit $rc
+    done
+    dirs=""
+    for k in $(seq 1 $i); do dirs="$dirs $(dirname $(ls gpurun_out/pmc_$k/*/run_counter_collection.csv gpurun_out/pmc_$k/run_counter_collection.csv 2>/dev/null | head -n 1))"; done
+    python3 tools/pmc_summary.py --workload $WL --window gpurun_out/pmc_summary.json $dirs || exit 1
+    ;;&
+  calib|all)
+    timeout -k 10 -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/calib_fetch -o run --output-format csv \
+      -- tools/fetch_calib > gpurun_out/calib.json 2> gpurun_out/calib.err || exit 1
+    timeout -k 10 -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/calib_write -o run --output-format csv \
+      -- tools/fetch_calib > /dev/null 2>> gpurun_out/calib.err || exit 1
     ;;
   bench2)
     timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \

@@ -6,6 +6,9 @@
                        node has changes and all live checksums are equal) (configs[3])
   config5_n4096.json   4,096 members, 10 % of them Reincarnate every 20 rounds, 100 rounds (configs[4] at the
                        largest size the oracle runs in minutes)
+  config3_n65536.json  bench.py's own workload: 65,536 members, 655 killed at round 10 (Philox seed 11), rounds
+                       0-44: steady state, the kill, the suspect wave and the first faulty timers (r >= 35)
+                       (configs[2]; dense oracle rows ~39 GB, generated in the 62-GB build container)
 
 Each per-round record holds: the round, sha256 of the checksum vector (uint32 little-endian, observer order),
 sha256 of the phase-S ping targets (int32 little-endian), the three canonical state digests (member rows,
@@ -15,7 +18,7 @@ The oracle is oracle/swim_oracle.c built with OpenMP over observers (oracle/buil
 tests/test_oracle_kats.py::test_openmp_oracle_equals_single_thread pins that build to the single-threaded one.
 TEST INFRASTRUCTURE ONLY: tests/test_parity_at_size.py compares the MI355X engine with these files on the GPU.
 
-usage: python tests/golden/make_size_fixtures.py {config2|config4|config5} [threads]"""
+usage: python tests/golden/make_size_fixtures.py {config2|config4|config5|config3} [threads]"""
 import hashlib
 import json
 import os
@@ -39,6 +42,7 @@ CONFIGS = {
     "config2": (lambda: W.config2(n=4096, rounds=200), False, "config2_n4096.json"),
     "config4": (lambda: W.config4(n=16384, rounds=260), True, "config4_n16384.json"),
     "config5": (lambda: W.config5(n=4096, rounds=100), False, "config5_n4096.json"),
+    "config3": (lambda: W.config3(n=65536, rounds=45, kill_round=10), False, "config3_n65536.json"),
 }
 
 

@@ -94,6 +94,8 @@ def lib():
             "or_watch": (None, [P, u32, i32]),
             "or_drain_applied": (i32, [P, u32, C.POINTER(OrChange), i32, C.POINTER(u32), C.POINTER(u32),
                                        C.POINTER(i32)]),
+            "or_drain_events": (i32, [P, u32, C.POINTER(OrChange), P, i32, C.POINTER(u32), C.POINTER(u32),
+                                      C.POINTER(i32)]),
             "or_non_local_override": (i32, [i64, i32, i64, i32]),
             "or_local_override": (i32, [i32, i64, i64, i32]),
             "or_update": (i32, [P, u32, C.POINTER(OrChange), i32, C.POINTER(OrChange), i32]),
@@ -312,7 +314,26 @@ class OracleSim:
 
     # --- applied-change stream (MemberlistChangesAppliedEvent, swim/events.go:56-61) ---
     def watch(self, o, on=True):
-        lib().or_watch(self.h, o, int(on))
+        """on: True = coalesced drains; "events" = also the per-Update stream; False = off"""
+        lib().or_watch(self.h, o, 2 if on == "events" else int(bool(on)))
+
+    def drain_events(self, o):
+        """per-Update stream of observer o: ([[change, ...] per applying Update in Update order], old checksum,
+        new checksum, NumMembers); changes as (member, status, inc, source, source_inc) in apply order"""
+        cap = 4 * self.n + 4096
+        out = (OrChange * cap)()
+        seq = np.empty(cap, np.int32)
+        a, b, c = C.c_uint32(), C.c_uint32(), C.c_int32()
+        k = lib().or_drain_events(self.h, o, out, seq.ctypes.data, cap, C.byref(a), C.byref(b), C.byref(c))
+        if k < 0:
+            raise ValueError(f"observer {o} has no per-Update stream")
+        ch = _unpack(out, min(k, cap))
+        events = []
+        for i, x in enumerate(ch):
+            if int(seq[i]) == len(events):
+                events.append([])
+            events[-1].append(x)
+        return events, a.value, b.value, c.value
 
     def drain_applied(self, o):
         """(changes, old checksum, new checksum, NumMembers) since the last drain of watched observer o;

@@ -8,12 +8,27 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def json_objects(text):
+    """every JSON object in text, also when two ranks' lines ever share one line of the pipe"""
+    dec, objs, i = json.JSONDecoder(), [], 0
+    while True:
+        i = text.find("{", i)
+        if i < 0:
+            return objs
+        obj, i = dec.raw_decode(text, i)
+        objs.append(obj)
+
+
+def test_json_objects_parses_merged_lines():
+    assert json_objects('noise\n{"rank": 0}{"rank": 1}\n\n{"rank": 2}\n') == [{"rank": 0}, {"rank": 1}, {"rank": 2}]
+
+
 def test_gpus2_spawns_two_ranks():
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--launch-check"],
                          capture_output=True, text=True, timeout=300, env=env, cwd=REPO)
     assert out.returncode == 0, out.stderr[-2000:]
-    lines = [json.loads(l) for l in out.stdout.splitlines() if l.startswith("{")]
+    lines = json_objects(out.stdout)
     assert sorted(l["rank"] for l in lines) == [0, 1]
     assert all(l["world_size"] == 2 for l in lines)
 

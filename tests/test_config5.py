@@ -51,3 +51,38 @@ def test_memory_budget_accounting():
     assert m["dissemination"] >= n * np_ * 8 and m["timers"] >= n * np_ * 9
     assert m["total"] >= m["row_words"] + m["dissemination"] + m["timers"] + m["message_pool"] + m["dense_snapshots"]
     assert m["dense_cap"] >= 64
+
+
+def test_config5_shard_allocates_on_one_mi355x():
+    """One shard of BASELINE.json config 5 at its stated size: N = 262,144 members over 8 GPUs, so this GPU holds
+    observer rows [0, 32,768) (the canonical split) with every dense cell, the message pool and the snapshot slots
+    of DESIGN.md §2. The reference keeps the disseminator and timers as maps (disseminator.go:47,
+    state_transitions.go:52); here they are dense cells, and this checks on hardware that the budget fits with at
+    least 10 % headroom, and that a 262,144-member row's checksum (a 10 MB string) equals Fingerprint32 of the
+    reference's string rebuilt from the row (memberlist.go:106-128)."""
+    import torch
+
+    from oracle_ffi import fingerprint32
+
+    total = torch.cuda.get_device_properties(0).total_memory
+    if total < 280e9:
+        pytest.skip(f"needs a 288 GB MI355X ({total / 1e9:.0f} GB visible)")
+    n, shard = 262144, (0, 32768)
+    eng = swimsim.Cluster(n, observer_range=shard)
+    try:
+        m = eng.memory()
+        np_ = n
+        rows = shard[1] - shard[0]
+        assert m["row_words"] == rows * np_ * 4
+        assert m["dissemination"] >= rows * np_ * 8 and m["timers"] >= rows * np_ * 9
+        assert m["total"] <= 0.90 * total, f"{m['total'] / 1e9:.1f} GB of {total / 1e9:.1f} GB: < 10 % headroom"
+        assert m["message_pool"] >= 2 * rows * 26214 * 16 // 2   # one burst's requests + responses (DESIGN.md §2)
+        cs = eng.checksums()
+        for o in (0, rows - 1):
+            st, inc = eng.row(o)
+            assert (st == swimsim.ALIVE).all()
+            s = "".join(f"{swimsim.address_of(k)}alive{swimsim.T0_MS};" for k in range(n))
+            assert int(cs[o]) == fingerprint32(s.encode()), f"observer {o}"
+        print(f"config5 shard {shard} of N={n}: {m}")
+    finally:
+        eng.close()

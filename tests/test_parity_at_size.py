@@ -7,8 +7,10 @@
   oracle fixtures (tests/golden/make_size_fixtures.py): every round, the sha256 of the checksum vector and of the
   phase-S targets, the three canonical state digests (rows, dissemination buffers, timer tables) and the protocol
   counters must be equal.
-* config 3 at 65,536 members through the suspect AND faulty waves: the oracle would take hours there, so parity
-  is checked through size-independent properties every 5 rounds: each sampled observer's checksum equals
+* config 3 at 65,536 members, bench.py's exact workload (kill at round 10), rounds 0-44 against a committed
+  fixture of the OpenMP oracle, every round as above.
+* config 3 at 65,536 members through the suspect AND faulty waves (75 rounds, kill at round 2): beyond the fixture,
+  parity is checked through size-independent properties every 5 rounds: each sampled observer's checksum equals
   Fingerprint32 of the reference's checksum string (memberlist.go:106-128) rebuilt on the host from the engine's
   own row, and the killed members go alive -> suspect -> faulty in every sampled live row on the reference's
   timeouts (suspect 5 s = 25 rounds, state_transitions.go:90-117).
@@ -73,6 +75,16 @@ def test_config4_full_size_to_convergence_vs_oracle_fixture():
     c, last = compare_with_fixture(wl, load_fixture("config4_n16384.json"))
     assert last["converged"], "the fixture ends at convergence"
     assert c["heal_attempts"] > 0 and c["timers_fired"] > 0
+
+
+def test_config3_n65536_bench_workload_vs_oracle_fixture():
+    """bench.py's own workload at its own size, every round against the OpenMP oracle (north star: bit-exact
+    per-round parity at 16-64k members): 65,536 members, 655 killed at round 10, rounds 0-44 (steady state, the
+    kill, the suspect wave, the first faulty timers at r >= 35)."""
+    wl = W.config3(n=65536, rounds=45, kill_round=10)
+    c, last = compare_with_fixture(wl, load_fixture("config3_n65536.json"))
+    assert last["round"] == 44
+    assert c["suspect_decl"] > 0 and c["timers_fired"] > 0 and c["pingreqs"] > 0
 
 
 def test_config5_bursts_n4096_vs_oracle_fixture():

@@ -1,7 +1,9 @@
 """Per-kernel, per-launch PMC figures from rocprofv3 --pmc passes of bench.py (one directory per pass).
 
-usage: python tools/pmc_summary.py [--workload MEMBERS:STEPS:WARMUP:GPUS] <out.json> <pass_dir> [<pass_dir> ...]
+usage: python tools/pmc_summary.py [--workload MEMBERS:STEPS:WARMUP:GPUS] [--window] <out.json> <pass_dir> [<pass_dir> ...]
 --workload records the bench.py command the passes profiled (bench.py uses the summary only for that workload).
+--window keeps only the dispatches between the first and the last k_profile_mark dispatch of each pass (bench.py
+marks its timed rounds), so the per-launch figures cover exactly the launches its HIP-event timings cover.
 Every counter of every pass is averaged per launch of each kernel. FETCH_SIZE and WRITE_SIZE are in
 KiB (TCC_EA0_RDREQ/WRREQ-derived) and are reported as bytes. MI355X_MICROARCH.md §HBM: on gfx950
 FETCH_SIZE reports half the bytes of a wide coalesced 16-B/lane streaming read (doubled here as
@@ -14,8 +16,17 @@ import json
 import sys
 
 
-def load(path, agg):
-    for x in csv.DictReader(open(f"{path}/run_counter_collection.csv")):
+def load(path, agg, window):
+    rows = list(csv.DictReader(open(f"{path}/run_counter_collection.csv")))
+    lo, hi = -1, float("inf")
+    if window:
+        marks = sorted(int(x["Dispatch_Id"]) for x in rows if "k_profile_mark" in x["Kernel_Name"])
+        if len(marks) < 2:
+            raise SystemExit(f"{path}: --window needs two k_profile_mark dispatches, found {len(marks)}")
+        lo, hi = marks[0], marks[-1]
+    for x in rows:
+        if not lo < int(x["Dispatch_Id"]) < hi:
+            continue
         k = x["Kernel_Name"].split("(")[0].replace("void ", "").strip()
         c = x["Counter_Name"]
         agg[k][c][0].add(x["Dispatch_Id"])
@@ -29,10 +40,14 @@ def main():
         m, st, w, g = (int(x) for x in argv[1].split(":"))
         workload = {"members": m, "steps": st, "warmup": w, "gpus": g}
         argv = argv[2:]
+    window = False
+    if argv and argv[0] == "--window":
+        window = True
+        argv = argv[1:]
     agg = collections.defaultdict(lambda: collections.defaultdict(lambda: [set(), 0.0]))
     for p in argv[1:]:
-        load(p, agg)
-    out = {"_workload": workload}
+        load(p, agg, window)
+    out = {"_workload": workload, "_window": "between k_profile_mark dispatches (bench.py timed rounds)" if window else None}
     for k in sorted(agg):
         e = {}
         for c, (ids, v) in agg[k].items():
