@@ -188,11 +188,11 @@ def live_member_rounds(wl, first, last):
     return total
 
 
-def cpu_baseline(gpu_window, seconds_budget=25.0):
+def cpu_baseline(gpu_window, seconds_budget=60.0):
     """The CPU oracle on a bounded sample of the same protocol (tools/cpu_baseline.py does the timing in a
     child process so that OpenMP threads do not share this process with the HIP runtime)."""
     out = subprocess.run([sys.executable, os.path.join(REPO, "tools", "cpu_baseline.py"), "--budget",
-                          str(seconds_budget), "--window", gpu_window], capture_output=True, text=True, timeout=600)
+                          str(seconds_budget), "--window", gpu_window], capture_output=True, text=True, timeout=1200)
     if out.returncode != 0:
         return {"error": out.stderr[-400:]}
     return json.loads(out.stdout.strip().splitlines()[-1])

@@ -134,6 +134,7 @@ constexpr int cs_no(int W, int maxtail) { return (3 + W + maxtail + 3) / 4; }
 
 #include "swimsim_checksum3.hip"
 #include "swimsim_checksum4.hip"
+#include "swimsim_checksum5.hip"
 #ifdef SWIMSIM_DIAG
 #include "swimsim_checksum_diag.hip"           // tools/diag (diagnostics library only)
 #endif

@@ -306,7 +306,6 @@ __global__ void __launch_bounds__(256) k_checksum(DS d, const uint32_t *list, co
 constexpr int CN_IT = 8;                        // records per row per step
 constexpr int CN_RING = 250;                    // ring words per row (50 blocks): 3 steps of 8 records
 constexpr int CN_NBLK = CN_RING / 5;
-constexpr int CN_MIR = 20;
 constexpr int CN_MBLK = 4;
 constexpr int CN_SINK = CS_PRE + CN_RING + CN_MIR;
 constexpr int CN_STRIDE = CN_SINK + 13;         // landing area + ring + mirror + sink; odd
@@ -836,7 +835,9 @@ void launch_checksum_mode(const DS &d, const uint32_t *list, const uint32_t *cou
     const uint32_t grid = (maxn + CS_ROWS - 1) / CS_ROWS;
     if (grid == 0 || d.W != 19) return;
     const uint32_t ngrid = (maxn + CN_ROWS - 1) / CN_ROWS;
-    if (mode == 30) launch_csq_w<19, 8>(d, list, count, ngrid, s);
+    if (mode == 50) launch_cs5_w<19, 1>(d, list, count, grid, s);
+    else if (mode == 51) launch_cs5_w<19, 2>(d, list, count, grid, s);
+    else if (mode == 30) launch_csq_w<19, 8>(d, list, count, ngrid, s);
     else if (mode == 31) launch_csq_w<19, 8, 1>(d, list, count, ngrid, s);
     else if (mode == 32) launch_csq_w<19, 8, 2>(d, list, count, ngrid, s);
     else if (mode == 33) launch_csq_w<19, 16>(d, list, count, ngrid, s);
