@@ -131,6 +131,8 @@ struct DS {
     uint32_t *hotnew;         // [NBIT] members that got a new dissemination entry while not hot
     uint32_t *hot_cnt;        // {slots in use, slots filled}
     uint32_t HP;              // hot slots per row
+    int32_t *nhe;             // [NL] dissemination entries of members WITHOUT a hot slot; 0: every buffered member of
+                              // the row is hot, so issue walks the hot slots instead of the presence bitmap
 };
 
 // hot slot of member m, SRC_NONE when m has none (or hot columns are off)

@@ -668,6 +668,7 @@ void hot_reset(swimsim *h) {
     hipMemsetAsync(h->d.hidx, 0xFF, (size_t)h->N * 4, h->s);
     hipMemsetAsync(h->d.hotnew, 0, (size_t)h->d.NBIT * 4, h->s);
     hipMemsetAsync(h->d.hot_cnt, 0, 8, h->s);
+    hipLaunchKernelGGL(k_nhe_reset, dim3(blocks_for_threads(h->NL)), dim3(256), 0, h->s, h->d);   // every entry is cold
 }
 
 // hot columns, start of phase I: members that got a first dissemination entry since the last call take free
@@ -1341,8 +1342,9 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
         (rc = dalloc(h, &d.live, h->N, "live")) || (rc = dalloc(h, &d.part, h->N, "part")) ||
         (rc = dalloc(h, &d.ctr, (size_t)CTR_SHARDS * CTR_STRIDE, "counters")) || (rc = dalloc(h, &d.err, 4, "err")) ||
         (rc = dalloc(h, &d.clen, h->NL, "clen")) || (rc = dalloc(h, &d.clast, h->NL, "clast")) ||
-        (rc = dalloc(h, &d.cpslot, h->NL, "cpslot")))
+        (rc = dalloc(h, &d.cpslot, h->NL, "cpslot")) || (rc = dalloc(h, &d.nhe, h->NL, "cold entry counts")))
         return bail(rc);
+    hipMemset(d.nhe, 0, (size_t)h->NL * 4);
     hipMemset(d.cpslot, 0xFF, (size_t)h->NL * 4);
     {
         // hot columns: 2,048 slots per row (1.6 GB at 65,536 rows); SWIMSIM_HOT_SLOTS=0 turns

@@ -49,10 +49,11 @@ __device__ __forceinline__ bool reach(const DS &d, uint32_t a, uint32_t b) {
 // ---------------------------------------------------------------------------------------------
 struct MAcc {
     int dping, ddc, napp, nref, nproc, evict, dlen, maxlast, inval;
+    int dnh;                  // entries created for members without a hot slot (d.nhe)
     unsigned long long dfp;   // row fingerprint delta
     unsigned long long tag;   // Update tag of the per-Update event stream (d.useq of the row at the Update's start)
-    __device__ MAcc() : dping(0), ddc(0), napp(0), nref(0), nproc(0), evict(0), dlen(0), maxlast(-1), inval(0), dfp(0),
-                        tag(0) {}
+    __device__ MAcc() : dping(0), ddc(0), napp(0), nref(0), nproc(0), evict(0), dlen(0), maxlast(-1), inval(0), dnh(0),
+                        dfp(0), tag(0) {}
 };
 
 // start of one Update on row ol: its changes carry the row's current sequence number (event stream only)
@@ -110,6 +111,7 @@ __device__ __forceinline__ void merge_change_w(const DS &d, uint32_t ol, uint32_
     if (de_p(d.dent[idx].x) == DP_NONE) {
         acc.ddc++;
         atomicOr(&d.dbit[(size_t)ol * d.NBIT + (m >> 5)], 1u << (m & 31));
+        if (hk == SRC_NONE) acc.dnh++;
         if (hk == SRC_NONE && d.hidx) {                           // a candidate for the next round's hot columns
             uint32_t *hw = d.hotnew + (m >> 5);
             if (!(__hip_atomic_load(hw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & (1u << (m & 31))))
@@ -154,8 +156,10 @@ __device__ __forceinline__ void merge_change(const DS &d, uint32_t ol, uint32_t 
 }
 
 __device__ __forceinline__ void fold_row(const DS &d, uint32_t ol, int dping, int ddc, int napp, int nref, int evict,
-                                         int dlen, int maxlast, int inval, unsigned long long dfp, bool next_update = true) {
+                                         int dlen, int maxlast, int inval, unsigned long long dfp, bool next_update = true,
+                                         int dnh = 0) {
     if (napp && next_update && d.useq) d.useq[ol] += 1ull;          // the next Update of this row takes the next tag
+    if (dnh) d.nhe[ol] += dnh;
     if (dfp) d.fp[ol] += dfp;
     if (dping) d.ping[ol] += dping;
     if (ddc) d.dcnt[ol] += ddc;
@@ -179,12 +183,12 @@ __device__ __forceinline__ int wmax(int v) {
 __device__ __forceinline__ void wave_finalize(const DS &d, uint32_t ol, const MAcc &acc, int cset = 0, bool next_update = true) {
     const int dping = wsum(acc.dping), ddc = wsum(acc.ddc), napp = wsum(acc.napp), nref = wsum(acc.nref);
     const int ev = wsum(acc.evict), np = wsum(acc.nproc), dl = wsum(acc.dlen), ml = wmax(acc.maxlast);
-    const int inv = wmax(acc.inval);
+    const int inv = wmax(acc.inval), dnh = wsum(acc.dnh);
     unsigned long long dfp = acc.dfp;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) dfp += __shfl_xor(dfp, off, 64);
     if (lane_id() == 0) {
-        fold_row(d, ol, dping, ddc, napp, nref, ev, dl, ml, inv, dfp, next_update);
+        fold_row(d, ol, dping, ddc, napp, nref, ev, dl, ml, inv, dfp, next_update, dnh);
         if (np && cset < 2) ctr_add(d, cset ? C_X_MERGED_R : C_X_MERGED, (unsigned long long)np);
         if (napp && cset < 2) ctr_add(d, cset ? C_X_APPLIED_R : C_X_APPLIED, (unsigned long long)napp);
     }
@@ -263,7 +267,7 @@ __device__ void wave_bump(const DS &d, uint32_t ol, const MsgDesc &md) {
     const int maxp = d.maxp[ol];
     uint32_t *dx = (uint32_t *)(d.dent + (size_t)ol * d.NP);       // word 0 of each entry, stride 2
     uint32_t *hx = (uint32_t *)(d.hde + (size_t)ol * d.HP);        // the same in the hot columns
-    int del = 0;
+    int del = 0, delnh = 0;
     for (uint32_t base = 0; base < md.len; base += 64 * MB) {
         uint32_t m[MB], x[MB], hk[MB];
 #pragma unroll
@@ -285,6 +289,7 @@ __device__ void wave_bump(const DS &d, uint32_t ol, const MsgDesc &md) {
                 nx = x[u] | 0xFF000000u;
                 atomicAnd(&d.dbit[(size_t)ol * d.NBIT + (m[u] >> 5)], ~(1u << (m[u] & 31)));
                 del++;
+                delnh += hk[u] == SRC_NONE;
             } else {
                 nx = x[u] + (1u << 24);
             }
@@ -293,7 +298,9 @@ __device__ void wave_bump(const DS &d, uint32_t ol, const MsgDesc &md) {
         }
     }
     del = wsum(del);
+    delnh = wsum(delnh);
     if (lane_id() == 0 && del) d.dcnt[ol] -= del;
+    if (lane_id() == 0 && delnh) d.nhe[ol] -= delnh;
     __threadfence_block();
 }
 
@@ -347,7 +354,55 @@ __device__ uint32_t wave_issue_t(const DS &d, uint32_t ol, uint32_t sender, uint
     const size_t rb = (size_t)ol * d.NP, hb = (size_t)ol * d.HP;
     uint32_t *bits = d.dbit + (size_t)ol * d.NBIT;
     uint32_t pos = 0;
-    int del = 0;
+    int del = 0, delnh = 0;
+    if (d.hidx && d.nhe[ol] == 0) {
+        // every buffered member of this row has a hot slot: walk the row's slots in use (a few KB,
+        // contiguous) instead of the presence bitmap (N/8 bytes) and the gathers it leads to. Records come out in
+        // slot order; the order of a message does not matter (its changes are distinct members).
+        const uint32_t nslots = d.hot_cnt[0];
+        for (uint32_t base = 0; base < nslots; base += 64 * MB) {
+            uint2 ce[MB];
+            uint32_t wv[MB], m[MB];
+#pragma unroll
+            for (int u = 0; u < MB; u++) {
+                const uint32_t k = base + u * 64 + lane_id();
+                ce[u] = k < nslots ? d.hde[hb + k] : make_uint2(DE_NONE, 0);
+                wv[u] = k < nslots ? d.hmw[hb + k] : 0u;
+                m[u] = k < nslots ? d.hlist[k] : 0u;
+            }
+            bool keep[MB];
+            uint32_t nk = 0;
+#pragma unroll
+            for (int u = 0; u < MB; u++) {
+                const uint32_t src = de_src(ce[u].x);
+                keep[u] = de_p(ce[u].x) != DP_NONE && !(RECV && src == sender && ce[u].y == sinc);   // filterChangesFromSender
+                nk += keep[u] ? 1u : 0u;
+            }
+            uint32_t tot;
+            uint32_t at = pos + wscan_excl(nk, tot);
+#pragma unroll
+            for (int u = 0; u < MB; u++) {
+                if (!keep[u]) continue;
+                const uint32_t st = (wv[u] & 7u) == ST_UNKNOWN ? ST_TOMB : (wv[u] & 7u);   // evicted: (tombstone, inc)
+                if (at < cnt) d.pool[off + at] = make_uint4(m[u] | (st << 24), wv[u] >> 3, de_src(ce[u].x), ce[u].y);
+                at++;
+                if (RECV) {                                                   // bump
+                    const uint32_t k = base + u * 64 + lane_id();
+                    uint32_t nx;
+                    if ((int)(de_p(ce[u].x) + 1) >= maxp) {
+                        nx = ce[u].x | 0xFF000000u;
+                        atomicAnd(bits + (m[u] >> 5), ~(1u << (m[u] & 31)));
+                        del++;
+                    } else {
+                        nx = ce[u].x + (1u << 24);
+                    }
+                    d.dent[rb + m[u]].x = nx;
+                    d.hde[hb + k].x = nx;
+                }
+            }
+            pos += tot;
+        }
+    } else
     for (uint32_t q0 = 0; q0 < d.NBIT; q0 += 256) {
         const uint32_t q = q0 + lane_id() * 4;
         unsigned long long lo = 0, hi = 0;                       // the lane's 128 presence bits
@@ -416,6 +471,7 @@ __device__ uint32_t wave_issue_t(const DS &d, uint32_t ol, uint32_t sender, uint
                         const uint32_t l = m[k] - mbase;
                         if (l < 64) dlo |= 1ull << l; else dhi |= 1ull << (l - 64);
                         del++;
+                        delnh += hk[k] == SRC_NONE;
                     } else {
                         nx = ce[k].x + (1u << 24);
                     }
@@ -434,7 +490,9 @@ __device__ uint32_t wave_issue_t(const DS &d, uint32_t ol, uint32_t sender, uint
     }
     if (RECV) {
         del = wsum(del);
+        delnh = wsum(delnh);
         if (lane_id() == 0 && del) d.dcnt[ol] -= del;
+        if (lane_id() == 0 && delnh) d.nhe[ol] -= delnh;
     } else if (pos != cnt && lane_id() == 0) {
         atomicOr(d.err, E_COUNT);
     }
@@ -512,6 +570,7 @@ __global__ void k_init_rows(DS d, int mode, uint32_t e0) {
         d.ping[ol] = p;
         d.maxp[ol] = mode == 0 ? (int32_t)d.pfactor * digits10(p) : (int32_t)d.pfactor;
         d.dcnt[ol] = 0;
+        d.nhe[ol] = 0;
         d.dirty[ol] = 1;
         d.cs[ol] = 0;
         d.it_idx[ol] = -1;
@@ -543,6 +602,7 @@ __global__ void k_recount(DS d, uint32_t ol) {
     for (int off = 32; off > 0; off >>= 1) fp += __shfl_xor(fp, off, 64);
     if (lane_id() == 0) {
         d.ping[ol] = p; d.dcnt[ol] = c; d.dirty[ol] = 1; d.clen[ol] = (uint32_t)len; d.clast[ol] = last; d.fp[ol] = fp;
+        d.nhe[ol] = c;                                             // raw writes drop every hot slot (hot_reset)
     }
 }
 
@@ -551,7 +611,16 @@ __global__ void k_clear_changes(DS d, uint32_t ol) {
     if (d.hidx)
         for (uint32_t k = threadIdx.x; k < d.HP; k += blockDim.x) d.hde[(size_t)ol * d.HP + k].x = DE_NONE;
     for (uint32_t b = threadIdx.x; b < d.NBIT; b += blockDim.x) d.dbit[(size_t)ol * d.NBIT + b] = 0;
-    if (threadIdx.x == 0) d.dcnt[ol] = 0;
+    if (threadIdx.x == 0) {
+        d.dcnt[ol] = 0;
+        d.nhe[ol] = 0;
+    }
+}
+
+// hot columns were dropped (hot_reset): every entry of every row belongs to a member without a slot
+__global__ void k_nhe_reset(DS d) {
+    const uint32_t ol = blockIdx.x * blockDim.x + threadIdx.x;
+    if (ol < d.NL) d.nhe[ol] = d.dcnt[ol];
 }
 
 // hot columns, start of phase I: members that got a first dissemination entry while not hot take free slots
@@ -589,10 +658,17 @@ __global__ void k_hot_fill(DS d) {
     if (ol >= d.NL) return;
     const uint32_t k0 = d.hot_cnt[1], k1 = d.hot_cnt[0];
     const size_t rb = (size_t)ol * d.NP, hb = (size_t)ol * d.HP;
+    int nowhot = 0;                                                // the row's entries whose member just got a slot
     for (uint32_t k = k0 + lane_id(); k < k1; k += 64) {
         const uint32_t m = d.hlist[k];
+        const uint2 cell = d.dent[rb + m];
         d.hmw[hb + k] = d.mw[rb + m];
-        d.hde[hb + k] = d.dent[rb + m];
+        d.hde[hb + k] = cell;
+        nowhot += de_p(cell.x) != DP_NONE;
+    }
+    if (k1 > k0) {
+        nowhot = wsum(nowhot);
+        if (lane_id() == 0 && nowhot) d.nhe[ol] -= nowhot;
     }
 }
 
@@ -630,6 +706,7 @@ __global__ void k_add_join_list(DS d, uint32_t ol, const uint4 *__restrict__ rec
                 d.dent[idx].x = DE_NONE;
                 const uint32_t hk = hot_slot(d, m);
                 if (hk != SRC_NONE) d.hde[(size_t)ol * d.HP + hk].x = DE_NONE;
+                else acc.dnh--;
                 atomicAnd(&d.dbit[(size_t)ol * d.NBIT + (m >> 5)], ~(1u << (m & 31)));
                 acc.ddc--;
             }
@@ -650,7 +727,7 @@ __device__ int thread_make_change(const DS &d, uint32_t ol, uint32_t o, uint32_t
     acc_begin(d, ol, acc);
     const uint32_t self_e = d.mw[(size_t)ol * d.NP + o] >> 3;   // MakeChange: SourceIncarnation = local inc
     merge_change(d, ol, o, m, st, e, o, self_e, r, r, acc);
-    fold_row(d, ol, acc.dping, acc.ddc, acc.napp, acc.nref, 0, acc.dlen, acc.maxlast, acc.inval, acc.dfp);
+    fold_row(d, ol, acc.dping, acc.ddc, acc.napp, acc.nref, 0, acc.dlen, acc.maxlast, acc.inval, acc.dfp, true, acc.dnh);
     return acc.napp;
 }
 
