@@ -188,7 +188,12 @@ int swimsim_applied_events(swimsim_t *h, uint32_t observer, int32_t *member, int
  * live node (gossip.go:178-188), so the Timing histogram is over rounds: the device wall time of each round
  * (HIP events on the engine's stream), in ns. ProtocolRate = max(2 x median, MinProtocolPeriod)
  * (AdjustProtocolRate, gossip.go:110-115). ServerRate = pings and ping-reqs handled per node per simulated
- * second (ping_handler.go:37, ping_request_handler.go:45); ClientRate is never marked by the reference (0). */
+ * second (ping_handler.go:37, ping_request_handler.go:45); ClientRate is never marked by the reference (0).
+ * Deviation (documented, not pinnable): the reference's Timing is metrics.NewHistogram(NewUniformSample(10))
+ * (gossip.go:65), so its Min/Max/Sum/Mean/Variance/percentiles come from a 10-element random reservoir (Count is
+ * the total), and AdjustProtocolRate takes that reservoir's median; its rates are go-metrics Meter.Rate1() (a
+ * one-minute EWMA). Here every statistic is over every round (up to 2^20) and rates are means over the run. The
+ * reservoir is filled from Go's global math/rand, so no restatement could match it sample for sample. */
 typedef struct swimsim_protocol_stats {
     int64_t count;
     double min_ns, max_ns, sum_ns, mean_ns, variance, stddev_ns, median_ns, p75_ns, p95_ns, p99_ns, p999_ns;

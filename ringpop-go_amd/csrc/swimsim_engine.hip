@@ -1390,6 +1390,10 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
     const uint64_t want_records = cfg->message_pool_bytes
                                       ? cfg->message_pool_bytes / 16
                                       : std::min<uint64_t>(std::max<uint64_t>(4ull * h->NL * h->N, 1ull << 20), pool_bound);
+    if (want_records < (uint64_t)POOL_SHARDS * h->N) {              // every sub-pool holds the longest message
+        h->err = "message_pool_bytes below 64 sub-pools x N records x 16 bytes";
+        return bail(SWIMSIM_EINVAL);
+    }
     d.pool_cap = want_records;
     if ((rc = dalloc(h, &d.pool, want_records, "message pool")) || (rc = dalloc(h, &d.pool_cur, POOL_SHARDS * POOL_CUR_STRIDE, "pool cursors")))
         return bail(rc);

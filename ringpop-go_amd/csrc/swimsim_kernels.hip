@@ -307,17 +307,24 @@ __device__ void wave_bump(const DS &d, uint32_t ol, const MsgDesc &md) {
 // The message pool is split into POOL_SHARDS sub-pools with a cursor each (own 128-B line): one returning
 // atomic per issuing wave on a single word saturates at ~88 per us (MI355X_MICROARCH.md row "dequeue"), which
 // serialised the 65,536 issues of a cascade round. A wave starts at the sub-pool of its wave id and moves on
-// to the next one only when its records do not fit, so the pool fails only when every sub-pool is full.
+// to the next one only when its records do not fit, so the pool fails only when every sub-pool is full. A
+// sub-pool's cursor only moves when the records fit (compare-and-swap), so a failed attempt strands no space;
+// swimsim_create requires every sub-pool to hold N records, the longest message.
 __device__ __forceinline__ unsigned long long pool_alloc(const DS &d, uint32_t n) {
     unsigned long long off = 0;
     if (lane_id() == 0 && n) {
         const unsigned long long sub = d.pool_cap / POOL_SHARDS;
         off = ~0ull;
-        for (uint32_t t = 0, s = wave_gid() % POOL_SHARDS; t < POOL_SHARDS; t++, s = (s + 1) % POOL_SHARDS) {
-            const unsigned long long old = atomicAdd(d.pool_cur + (size_t)s * POOL_CUR_STRIDE, (unsigned long long)n);
-            if (old + n <= sub) {
-                off = s * sub + old;
-                break;
+        for (uint32_t t = 0, s = wave_gid() % POOL_SHARDS; t < POOL_SHARDS && off == ~0ull; t++, s = (s + 1) % POOL_SHARDS) {
+            unsigned long long *cur = d.pool_cur + (size_t)s * POOL_CUR_STRIDE;
+            unsigned long long old = __hip_atomic_load(cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            while (old + n <= sub) {
+                const unsigned long long seen = atomicCAS(cur, old, old + n);
+                if (seen == old) {
+                    off = s * sub + old;
+                    break;
+                }
+                old = seen;
             }
         }
         if (off == ~0ull) atomicOr(d.err, E_POOL);

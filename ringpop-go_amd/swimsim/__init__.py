@@ -279,16 +279,17 @@ class Cluster:
 
     def _emit(self):
         """deliver MemberlistChangesAppliedEvent to the listeners of watched observers (node.emit, node.go:266-270):
-        one event per observer with changes applied since the previous delivery"""
+        one event per Update that applied something, in the node's Update order (the per-Update stream). Old/New
+        checksums are per drain: the first event of a drain carries the checksum at the previous drain, every event
+        the current one as NewChecksum (and as OldChecksum after the first)"""
         for o, ls in self._listeners.items():
             if not ls:
                 continue
-            changes, old, new, nm = self.applied_changes(o)
-            if not changes:
-                continue
-            evt = MemberlistChangesAppliedEvent(self._wire_changes(changes), old, new, nm)
-            for l in ls:
-                (l.HandleEvent if hasattr(l, "HandleEvent") else l)(evt)
+            events, old, new, nm = self.applied_events(o)
+            for i, changes in enumerate(events):
+                evt = MemberlistChangesAppliedEvent(self._wire_changes(changes), old if i == 0 else new, new, nm)
+                for l in ls:
+                    (l.HandleEvent if hasattr(l, "HandleEvent") else l)(evt)
 
     @staticmethod
     def _wire_changes(changes):
@@ -335,7 +336,7 @@ class Cluster:
     def register_listener(self, o, listener):
         """NodeInterface.RegisterListener (node.go:146) for simulated node o"""
         if o not in self._listeners:
-            self.watch(o)
+            self.watch(o, "events")
             self._listeners[o] = []
         self._listeners[o].append(listener)
 

@@ -86,3 +86,14 @@ def test_config5_shard_allocates_on_one_mi355x():
         print(f"config5 shard {shard} of N={n}: {m}")
     finally:
         eng.close()
+
+
+def test_message_pool_must_hold_the_longest_message_per_sub_pool():
+    """pool_alloc's 64 sub-pools each take a whole message; a message has up to N records (no per-message cap,
+    SURVEY.md §0.2), so a caller-set pool below 64 x N records is refused at create time"""
+    n = 1024
+    with pytest.raises(swimsim.SwimsimError):
+        swimsim.Cluster(n, message_pool_bytes=64 * n * 16 - 16)
+    eng = swimsim.Cluster(n, message_pool_bytes=64 * n * 16)
+    eng.step(3)
+    eng.close()
