@@ -47,6 +47,25 @@ FAMILY_KERNEL = {"checksum_wide": "swimdev::k_checksum3", "checksum_narrow": "sw
                  "recv_merge": "swimdev::k_recv", "resp_merge": "swimdev::k_resp", "issue": "swimdev::k_issue",
                  "timers": "swimdev::k_timers"}
 PMC_SUMMARY = os.path.join(REPO, "profiles", "r03_pmc_summary.json")
+FETCH_CALIB = os.path.join(REPO, "profiles", "r03_fetch_calib.json")
+
+
+def fetch_factor(fam):
+    """HBM bytes per FETCH_SIZE byte for the kernel's dominant read pattern, measured by tools/fetch_calib.hip
+    (profiles/r03_fetch_calib.json): the checksum kernels stream each lane's own row 16 B at a time
+    (k_rowstream16); the merge and issue kernels gather one 4-B or 8-B word per 64-B sector, which FETCH_SIZE
+    counts in full (64 B per sector, factor 1; their coalesced record streams are then undercounted by half, so
+    the doubled figure is kept as the upper bound)."""
+    try:
+        with open(FETCH_CALIB) as f:
+            c = json.load(f)
+    except (OSError, ValueError):
+        c = {}
+    if fam.startswith("checksum"):
+        r = c.get("k_rowstream16", {}).get("fetch_over_read") or c.get("k_stream16", {}).get("fetch_over_read") or 0.5
+        return 1.0 / r, "k_rowstream16" if "k_rowstream16" in c else "k_stream16"
+    r = c.get("k_gather<unsigned int>", {}).get("fetch_per_sector")
+    return (64.0 / r if r else 1.0), "k_gather<unsigned int>"
 
 
 def pmc_kernel(symbol, workload):
@@ -127,8 +146,11 @@ def add_pmc(entry, fam, workload):
     if not p:
         entry.update({"traffic": None, "traffic_note": "no PMC summary of this workload's timed window"})
         return entry
-    t = 2.0 * p["fetch"] + p["write"]
-    entry.update({"traffic": round(t, 1), "traffic_raw_fetch_plus_write": round(p["fetch"] + p["write"], 1),
+    ff, pattern = fetch_factor(fam)
+    t = ff * p["fetch"] + p["write"]
+    entry.update({"traffic": round(t, 1), "traffic_fetch_factor": round(ff, 3), "traffic_fetch_pattern": pattern,
+                  "traffic_raw_fetch_plus_write": round(p["fetch"] + p["write"], 1),
+                  "traffic_upper_2x_fetch_plus_write": round(2.0 * p["fetch"] + p["write"], 1),
                   "traffic_over_alg": round(t / entry["alg_bytes_per_launch"], 3) if entry.get("alg_bytes_per_launch") else None,
                   "pmc_launches": p["launches"], "pmc_source": p["source"]})
     if fam.startswith("checksum") and p["valu_insts"]:
