@@ -134,14 +134,18 @@ constexpr int cs_no(int W, int maxtail) { return (3 + W + maxtail + 3) / 4; }
 
 #include "swimsim_checksum3.hip"
 #include "swimsim_checksum4.hip"
-#include "swimsim_checksum5.hip"
-#ifdef SWIMSIM_DIAG
-#include "swimsim_checksum_diag.hip"           // tools/diag (diagnostics library only)
+#ifdef SWIMSIM_DIAG                            // tools/diag (diagnostics library only): the 3-wave and
+#include "swimsim_checksum5.hip"               // fast-path experiments and every superseded kernel
+#include "swimsim_checksum6.hip"
+#include "swimsim_checksum_diag.hip"
 #endif
 
 // up to CS_NARROW_ROWS rows (measured crossover) the launch is latency-bound: k_checksum_q16 (16 rows per
 // workgroup; 16 records per step up to 4,096 rows, 8 above); above, the 64-row throughput kernel k_checksum3
-constexpr uint32_t CS_NARROW_ROWS = 12288;
+constexpr uint32_t CS_NARROW_ROWS = 8192;
+// phase-C launches of at most CS_ASYNC_ROWS rows (after dedup) run on the side stream, overlapping the next round
+// (swimsim_engine.hip checksum_dirty); the kernel is still chosen by row count
+constexpr uint32_t CS_ASYNC_ROWS = 12288;
 static uint32_t g_csq16_groups = 256;                  // q16 row groups up to which 16 records per step are used
 static uint32_t g_cs_narrow_rows = CS_NARROW_ROWS;     // SWIMSIM_CS_NARROW_ROWS (tests: 0 = wide kernel only)
 

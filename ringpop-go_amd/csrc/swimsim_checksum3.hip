@@ -47,16 +47,17 @@ __global__ void __launch_bounds__(128) k_checksum3(DS d, const uint32_t *list, c
         // SIMD arbitrates VALU issue between its two waves by priority, then age: raised, it takes its issue slots
         // ahead of the co-resident hasher wave (17.8 -> 14.6 ms at 65,536 rows, 17.1 -> 13.6 ms at 32,768)
         if (MODE != 7) __builtin_amdgcn_s_setprio(2);             // (MODE 7: diagnostics without it)
-        const uint32_t ecap1 = d.ecap - 1;
+        const uint32_t wmax = d.ecap * 8u - 1u;                     // last member word of the record table
         uint32_t pos = 0, hc = 0;                                  // bytes formatted; the stream's last 4 bytes
         uint4 cur[4], pre[4];                                      // row words: this super step, the next
         uint4 TA[4][C2_IT], TB[4][C2_IT];                          // record tails of steps u .. u+2 (slot u & 3)
+        // rtail is d.rtail8, indexed by the member word: 32-byte entries, 32-bit byte offsets
         const char *rtb = (const char *)rtail;
         auto tails = [&](uint4 q4, uint4 (&ta)[C2_IT], uint4 (&tb)[C2_IT]) {
             const uint32_t ws[4] = {q4.x, q4.y, q4.z, q4.w};
 #pragma unroll
-            for (int k = 0; k < C2_IT; k++) {                    // 32-byte entries, 32-bit byte offsets
-                const uint32_t off = ((min(ws[k] >> 3, ecap1) << 2) + (ws[k] & 3u)) << 5;
+            for (int k = 0; k < C2_IT; k++) {
+                const uint32_t off = min(ws[k], wmax) << 5;
                 ta[k] = *(const uint4 *)(rtb + off);
                 tb[k] = *(const uint4 *)(rtb + off + 16u);
             }
@@ -130,7 +131,7 @@ __global__ void __launch_bounds__(128) k_checksum3(DS d, const uint32_t *list, c
 #pragma unroll
                 for (int k = 0; k < C2_IT; k++) {
                     const uint32_t m = mb + k;
-                    const uint32_t L = ((ws[k] & 7u) < 4u && (FULL || m < N)) ? (tb[k].z >> 24) : 0u;
+                    const uint32_t L = (FULL || m < N) ? (tb[k].z >> 24) : 0u;   // 0: tombstone / unknown
                     const uint32_t sh = pos & 3u;
                     // sh * 0x01010101 as a byte broadcast (one full-rate v_perm, not a multiply)
                     const uint32_t sel = 0x07060504u - __builtin_amdgcn_perm(0u, sh, 0u);
@@ -194,26 +195,34 @@ __global__ void __launch_bounds__(128) k_checksum3(DS d, const uint32_t *list, c
             for (int j = 0; j < NB; j++)
 #pragma unroll
                 for (int i = 0; i < 5; i++) v[j][i] = MODE == 4 ? (t * 977u + j * 31u + i) ^ lane : OB[(5 * j + i) * C2_ROWS];
-            // blocks every lane has (a uniform count: no predication) first, then the predicated rest
+            // blocks every lane has (a uniform count: no predication) first, then the predicated rest. The three
+            // cases are separate code paths: with one loop and a run-time jall the compiler if-converts every block's
+            // update into v_cndmask selects (21 per step of 8 blocks, about 5 % of the hasher's VALU cycles)
             const uint32_t nb = lim > done ? lim - done : 0u;
             const uint32_t jall = (MODE == 3 || MODE == 4) ? NB : __all(nb >= NB) ? NB : __all(nb >= NB - 1) ? NB - 1 : 0u;
+            auto blocks = [&](auto JALL) {
+                constexpr uint32_t JA = decltype(JALL)::value;
 #pragma unroll
-            for (int j = 0; j < NB; j++) {
-                const uint32_t a = v[j][0], b = v[j][1], c = v[j][2], dd = v[j][3], e = v[j][4];
-                const uint32_t hn = fh_fold(h + a, fh_m(dd), e);
-                uint32_t gn = fh_fold(g + b, fh_m(c), a);
-                uint32_t fn = fh_fold(f + c, fh_m(b + e * FH_C1), dd);
-                fn += gn;
-                gn += fn;
-                if ((uint32_t)j < jall) {
-                    h = hn; g = gn; f = fn;
-                } else {
-                    const bool act = (uint32_t)j < nb;
-                    h = act ? hn : h;
-                    g = act ? gn : g;
-                    f = act ? fn : f;
+                for (int j = 0; j < NB; j++) {
+                    const uint32_t a = v[j][0], b = v[j][1], c = v[j][2], dd = v[j][3], e = v[j][4];
+                    const uint32_t hn = fh_fold(h + a, fh_m(dd), e);
+                    uint32_t gn = fh_fold(g + b, fh_m(c), a);
+                    uint32_t fn = fh_fold(f + c, fh_m(b + e * FH_C1), dd);
+                    fn += gn;
+                    gn += fn;
+                    if ((uint32_t)j < JA) {
+                        h = hn; g = gn; f = fn;
+                    } else {
+                        const bool act = (uint32_t)j < nb;
+                        h = act ? hn : h;
+                        g = act ? gn : g;
+                        f = act ? fn : f;
+                    }
                 }
-            }
+            };
+            if (jall == NB) blocks(std::integral_constant<uint32_t, NB>{});
+            else if (jall == NB - 1) blocks(std::integral_constant<uint32_t, NB - 1>{});
+            else blocks(std::integral_constant<uint32_t, 0>{});
             done = be;
         }
         if (t < nsteps) lds_barrier();
@@ -237,10 +246,10 @@ void launch_cs3_w(const DS &d, const uint32_t *list, const uint32_t *count, uint
     if (W == 19 && d.max_tail <= 21 && d.min_tail >= 19) {     // 13-digit incarnations: records of 38..40 bytes
         constexpr int NO = cs_no(W, 21);
         hipLaunchKernelGGL((k_checksum3<W, NO, c2_nb(W + 21), c2_bw(W + 21, NO), MODE>), dim3(grid), dim3(128), 0, s, d, list,
-                           count, d.addrw, (const uint4 *)d.rtail);
+                           count, d.addrw, (const uint4 *)d.rtail8);
     } else {                                                   // any tail of up to 24 bytes
         constexpr int NO = cs_no(W, 24);
         hipLaunchKernelGGL((k_checksum3<W, NO, c2_nb(W + 24), c2_bw(W + 24, NO)>), dim3(grid), dim3(128), 0, s, d, list,
-                           count, d.addrw, (const uint4 *)d.rtail);
+                           count, d.addrw, (const uint4 *)d.rtail8);
     }
 }

@@ -41,8 +41,8 @@ enum Counter {
     C_X_MERGED_R, C_X_APPLIED_R, C_X_RISSUED, C_X_RCALLS, C_X_BUMPED, C_X_CS_ROWS_N, C_NALL
 };
 
-constexpr int CTR_SHARDS = 64, CTR_STRIDE = 32;   // d.ctr is [CTR_SHARDS][CTR_STRIDE] u64
-static_assert(C_NALL <= CTR_STRIDE, "counter block too small");
+constexpr int CTR_SHARDS = 64, CTR_STRIDE = 40;   // d.ctr is [CTR_SHARDS][CTR_STRIDE] u64
+static_assert(C_NALL + 4 <= CTR_STRIDE, "counter block too small (4 diagnostic slots follow C_NALL)");
 constexpr uint32_t POOL_SHARDS = 64, POOL_CUR_STRIDE = 16;   // d.pool_cur is [POOL_SHARDS][POOL_CUR_STRIDE] u64
 
 enum ErrBits : uint32_t {
@@ -81,6 +81,8 @@ struct DS {
                             // address bytes zeroed (tail pre-shifted by W%4 bytes); byte 27 (word 6's
                             // high byte, never a record byte) = record length; word 7 = the record's
                             // last 4 bytes
+    const uint32_t *rtail8; // [ecap*8][8]: rtail indexed by the member word itself (e << 3 | status), the
+                            // entries of statuses 4..7 all zero (record length 0: not in the string)
     unsigned long long *ctr;
     uint32_t *err;
     uint4 *pool;

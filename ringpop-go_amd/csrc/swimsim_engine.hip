@@ -314,7 +314,7 @@ struct swimsim {
     std::vector<hipEvent_t> evpool;
     double fam_ms[F_NFAM] = {0};
     uint64_t fam_n[F_NFAM] = {0};
-    uint64_t fam_bytes_base[C_NALL] = {0};
+    uint64_t fam_bytes_base[CTR_STRIDE] = {0};
     // ProtocolStats (swim/stats.go:81-104): device wall time of every round, from consecutive round-start
     // events on the main stream (the last round ends at the step's closing event)
     std::vector<hipEvent_t> round_ev;
@@ -454,13 +454,21 @@ int build_tail_table(swimsim *h, uint32_t ecap) {
         rt[i * 8 + 6] |= L << 24;
     }
     (void)q;
-    uint32_t *dev = nullptr, *rdev = nullptr;
+    // the same indexed by the member word: the wide formatter's table offset is one shift and a clamp, and a
+    // tombstone / unknown member reads record length 0 instead of testing its status
+    std::vector<uint32_t> rt8((size_t)ecap * 8 * 8, 0u);
+    for (size_t e = 0; e < ecap; e++)
+        for (int s = 0; s < 4; s++) memcpy(&rt8[(e * 8 + s) * 8], &rt[(e * 4 + s) * 8], 32);
+    uint32_t *dev = nullptr, *rdev = nullptr, *r8dev = nullptr;
     if (int rc = dalloc(h, &dev, t.size(), "tail table")) return rc;
     if (int rc = dalloc(h, &rdev, rt.size(), "record tail table")) return rc;
+    if (int rc = dalloc(h, &r8dev, rt8.size(), "record tail table by member word")) return rc;
     HIPCHK(h, hipMemcpy(dev, t.data(), t.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(h, hipMemcpy(rdev, rt.data(), rt.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemcpy(r8dev, rt8.data(), rt8.size() * 4, hipMemcpyHostToDevice));
     h->d.tailw = dev;
     h->d.rtail = rdev;
+    h->d.rtail8 = r8dev;
     // digit-count thresholds of t0 + e*period over the table (the checksum record length formula)
     {
         uint32_t d0 = t[6] - 6, nthr = 0;   // "alive" + ';' around the digits of e = 0
@@ -1408,7 +1416,7 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
             d.dense_cap = (uint32_t)std::max<unsigned long>(64, std::min<unsigned long>(d.dense_cap, strtoul(v, nullptr, 10)));
         // side-stream checksum snapshots (latency-bound phase C launches only), up to 1/8 of the free HBM
         const uint64_t snap_mem = (uint64_t)(freeb / 8) / (4ull * h->NP);
-        uint64_t async_rows = CS_NARROW_ROWS;
+        uint64_t async_rows = CS_ASYNC_ROWS;
         if (const char *v = getenv("SWIMSIM_CS_ASYNC_ROWS")) async_rows = strtoull(v, nullptr, 10);
         h->snap_cap = h->cs_async ? (uint32_t)std::min<uint64_t>(std::min<uint64_t>(async_rows, h->NL), snap_mem) : 0u;
     }
@@ -2142,7 +2150,7 @@ int swimsim_enable_timing(swimsim_t *h, int32_t enable) {
     for (int f = 0; f < F_NFAM; f++) { h->fam_ms[f] = 0; h->fam_n[f] = 0; }
     uint64_t c[CTR_STRIDE];
     if (int rc = read_counters(h, c)) return rc;
-    for (int i = 0; i < C_NALL; i++) h->fam_bytes_base[i] = c[i];
+    for (int i = 0; i < CTR_STRIDE; i++) h->fam_bytes_base[i] = c[i];
     return SWIMSIM_OK;
 }
 
@@ -2196,9 +2204,9 @@ int swimsim_kernel_units(swimsim_t *h, const char **names, double *values, size_
     if (int rc = read_counters(h, c)) return rc;
     static const char *kn[] = {"cs_rows_wide", "cs_rows_narrow", "cs_dup_rows", "recv_merged", "recv_applied",
                                "recv_issued", "recv_calls", "resp_merged", "resp_applied", "resp_bumped", "issued",
-                               "bitmap_words_per_row"};
+                               "bitmap_words_per_row", "diag_stamp0", "diag_stamp1", "diag_stamp2", "diag_stamp3"};
     const int ki[] = {C_X_CS_ROWS, C_X_CS_ROWS_N, C_X_CS_DUP, C_X_MERGED, C_X_APPLIED, C_X_RISSUED, C_X_RCALLS,
-                      C_X_MERGED_R, C_X_APPLIED_R, C_X_BUMPED, C_X_ISSUED, -1};
+                      C_X_MERGED_R, C_X_APPLIED_R, C_X_BUMPED, C_X_ISSUED, -1, C_NALL, C_NALL + 1, C_NALL + 2, C_NALL + 3};
     const size_t k = sizeof(ki) / sizeof(ki[0]);
     for (size_t i = 0; i < k && i < cap; i++) {
         if (names) names[i] = kn[i];

@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU session script: each step under its own time limit; stop at the first failing step.
-# usage: run_gpu.sh [tests|smoke|bench|prof|pmc|calib|all ...]   (several modes run in the order given)
+# usage: run_gpu.sh [tests|smoke|bench|prof|pmc|calib|curve|all ...]   (several modes run in the order given)
 # BENCH_ARGS defaults to the driver's round-end command (--steps 20 --warmup 5); prof and pmc profile
 # exactly that command, so profiles/ figures and the bench line describe the same workload.
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -58,6 +58,12 @@ for mode in "$@"; do
       --master-port 29511 bench.py --gpus 2 --members 2048 --steps 30 --warmup 10 --host-transport \
       > gpurun_out/bench2.json 2> gpurun_out/bench2.err
     rc=$?; echo "bench2 rc=$rc" >> gpurun_out/bench2.err; [ $rc -eq 0 ] || exit $rc
+    ;;
+  curve)
+    # rows-vs-ms of the production checksum kernels on real cascade rows (config 3 at 65,536, round 18), parity-checked
+    timeout -k 10 300 python -u tools/cs_bench_real.py 65536 18 0,1,2 2 2048,4096,6144,8192,10240,12288,16384,24576,32768,49152,65536 \
+      > gpurun_out/curve.json 2> gpurun_out/curve.err
+    rc=$?; echo "curve rc=$rc" >> gpurun_out/curve.err; [ $rc -eq 0 ] || exit $rc
     ;;
   csbench)
     timeout -k 10 300 python -u tools/cs_bench.py 65536 64,1024,16384,65536 2 ${CS_MODES:-0,1,2} > gpurun_out/csbench.json 2> gpurun_out/csbench.err

@@ -835,7 +835,11 @@ void launch_checksum_mode(const DS &d, const uint32_t *list, const uint32_t *cou
     const uint32_t grid = (maxn + CS_ROWS - 1) / CS_ROWS;
     if (grid == 0 || d.W != 19) return;
     const uint32_t ngrid = (maxn + CN_ROWS - 1) / CN_ROWS;
-    if (mode == 50) launch_cs5_w<19, 1>(d, list, count, grid, s);
+    if (mode == 62) launch_cs6_w<19, 1, 1>(d, list, count, grid, s);
+    else if (mode == 63) launch_cs6_w<19, 2, 1>(d, list, count, grid, s);
+    else if (mode == 60) launch_cs6_w<19, 1>(d, list, count, grid, s);
+    else if (mode == 61) launch_cs6_w<19, 2>(d, list, count, grid, s);
+    else if (mode == 50) launch_cs5_w<19, 1>(d, list, count, grid, s);
     else if (mode == 51) launch_cs5_w<19, 2>(d, list, count, grid, s);
     else if (mode == 30) launch_csq_w<19, 8>(d, list, count, ngrid, s);
     else if (mode == 31) launch_csq_w<19, 8, 1>(d, list, count, ngrid, s);
