@@ -115,12 +115,13 @@ def roofline_entry(fam, kt, units, n_members):
         merge_b = 22.0 * merged + 23.0 * applied
         if fam == "recv_merge":
             side_b = 36.0 * units["recv_issued"] + 4.0 * units["bitmap_words_per_row"] * units["recv_calls"]
-            side = {"issue_as_receiver_bytes_per_launch": round(side_b / nl, 1),
+            side = {"issued_per_launch": round(units["recv_issued"] / nl, 1), "calls_per_launch": round(units["recv_calls"] / nl, 1),
+                    "issue_as_receiver_bytes_per_launch": round(side_b / nl, 1),
                     "issue_as_receiver_basis": "36 B per issued record (16-B cell gather + 16-B record write + 4-B "
                     "counter write-back) + the presence bitmap (4 B per 32 members) per call"}
         else:
             side_b = 24.0 * units["resp_bumped"]
-            side = {"bump_bytes_per_launch": round(side_b / nl, 1),
+            side = {"bumped_per_launch": round(units["resp_bumped"] / nl, 1), "bump_bytes_per_launch": round(side_b / nl, 1),
                     "bump_basis": "24 B per bumped entry (16-B record read + 4-B counter read and write)"}
         out.update({"work_unit": "processed change", "units_per_launch": round(merged / nl, 1),
                     "applied_per_launch": round(applied / nl, 1),

@@ -123,9 +123,11 @@ struct DS {
                               // Update; phase T's timers take tags above it in (deadline, member) order
     // hot columns: compact copies of the row words and dissemination cells of the members that
     // sit in dissemination buffers, so that issue, merge and bump gather from a few KB per row instead of one
-    // 64-B sector per member. hmw[ol][k] == mw[ol][hlist[k]] and hde[ol][k] == dent[ol][hlist[k]] for every
-    // slot k < hot_cnt[0]: every write of a hot member's word or cell goes to both copies, so reads may use
-    // either. hidx = nullptr: off.
+    // 64-B sector per member. hmw[ol][k] == mw[ol][hlist[k]] for every slot k < hot_cnt[0] (every write of a hot
+    // member's word goes to both copies: snapshots and checksums stream the dense words). hde[ol][k] IS the
+    // dissemination cell of member hlist[k]: merges, bumps and evictions of a hot member write only the slot, and
+    // dent[ol][hlist[k]] is stale until k_hot_flush writes the slots back (before hot_reset drops them and
+    // before a host read-back of dent). hidx = nullptr: off.
     uint32_t *hidx;           // [N] member -> hot slot, SRC_NONE if not hot
     uint32_t *hlist;          // [HP] slot -> member
     uint32_t *hmw;            // [NL][HP]

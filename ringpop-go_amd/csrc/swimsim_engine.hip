@@ -670,9 +670,18 @@ void hash_rows(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t m
     launch_checksum_kind(h->d, list, cnt, n, kind, st ? st : h->s);
 }
 
-// hot columns: forget every hot member (raw row writes bypass the copies)
-void hot_reset(swimsim *h) {
+// the hot slots' cells back into dent for rows [ol0, ol0 + n) (DS::hde: the slot is the cell of a hot member)
+void hot_flush(swimsim *h, uint32_t ol0, uint32_t n) {
+    if (!h->d.hidx || n == 0) return;
+    hipLaunchKernelGGL(k_hot_flush, dim3(blocks_for_waves(n)), dim3(SWIM_WAVE_BLOCK), 0, h->s, h->d, ol0, n);
+}
+
+// hot columns: forget every hot member (raw row writes bypass the copies). flush: the rows' cells are live
+// (set_member / set_row), so the slots are written back to dent first; init and allocation overwrite or have
+// no cells.
+void hot_reset(swimsim *h, bool flush) {
     if (!h->d.hidx) return;
+    if (flush) hot_flush(h, 0, h->NL);
     hipMemsetAsync(h->d.hidx, 0xFF, (size_t)h->N * 4, h->s);
     hipMemsetAsync(h->d.hotnew, 0, (size_t)h->d.NBIT * 4, h->s);
     hipMemsetAsync(h->d.hot_cnt, 0, 8, h->s);
@@ -1369,7 +1378,7 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
                 (rc = dalloc(h, &d.hotnew, d.NBIT, "hot candidates")) || (rc = dalloc(h, &d.hot_cnt, 2, "hot count")))
                 return bail(rc);
             d.HP = hp;
-            hot_reset(h);
+            hot_reset(h, false);
         }
     }
     // address words
@@ -1522,7 +1531,7 @@ int swimsim_destroy(swimsim_t *h) {
 }
 
 static int init_rows(swimsim_t *h, int mode) {
-    hot_reset(h);
+    hot_reset(h, false);
     hipLaunchKernelGGL(k_init_rows, dim3(blocks_for_waves(h->NL)), dim3(SWIM_WAVE_BLOCK), 0, h->s, h->d, mode, 0u);
     if (int rc = checksum_dirty(h, 0)) return rc;
     return check_err(h);
@@ -1539,7 +1548,7 @@ int swimsim_set_member(swimsim_t *h, uint32_t o, uint32_t m, int32_t status, int
     if (status != SWIMSIM_UNKNOWN)
         if (int rc = to_e(h, inc_ms, &e)) return rc;
     const uint32_t w = (e << 3) | (uint32_t)status;
-    hot_reset(h);
+    hot_reset(h, true);
     HIPCHK(h, hipMemcpyAsync(h->d.mw + (size_t)(o - h->lo) * h->NP + m, &w, 4, hipMemcpyHostToDevice, h->s));
     hipLaunchKernelGGL(k_recount, dim3(1), dim3(64), 0, h->s, h->d, o - h->lo);
     HIPCHK(h, hipStreamSynchronize(h->s));
@@ -1557,7 +1566,7 @@ int swimsim_set_row(swimsim_t *h, uint32_t o, const uint8_t *status, const int64
         if (int rc = to_e(h, inc_ms[m], &e)) return rc;
         row[m] = (e << 3) | (uint32_t)s;
     }
-    hot_reset(h);
+    hot_reset(h, true);
     HIPCHK(h, hipMemcpyAsync(h->d.mw + (size_t)(o - h->lo) * h->NP, row.data(), (size_t)h->N * 4,
                              hipMemcpyHostToDevice, h->s));
     hipLaunchKernelGGL(k_recount, dim3(1), dim3(64), 0, h->s, h->d, o - h->lo);
@@ -1749,6 +1758,7 @@ int swimsim_changes(swimsim_t *h, uint32_t o, int32_t *member, int32_t *p, int32
     if (!h || !own(h, o)) return SWIMSIM_EINVAL;
     const size_t base = (size_t)(o - h->lo) * h->NP;
     std::vector<uint2> ent(h->NP);
+    hot_flush(h, o - h->lo, 1);                                     // hot members' cells live in their slots
     HIPCHK(h, hipMemcpyAsync(ent.data(), h->d.dent + base, h->NP * 8, hipMemcpyDeviceToHost, h->s));
     HIPCHK(h, hipStreamSynchronize(h->s));
     size_t k = 0;

@@ -108,7 +108,7 @@ __device__ __forceinline__ void merge_change_w(const DS &d, uint32_t ol, uint32_
     acc.dfp += fpmix(m, (ne << 3) | nst) - fpmix(m, cur);
     if (m != o) acc.dping += (int)is_pingable(nst) - (int)is_pingable(cur_st);
     // RecordChange (disseminator.go:223-227): entry = {p 0, source, source incarnation}
-    if (de_p(d.dent[idx].x) == DP_NONE) {
+    if (de_p(hk != SRC_NONE ? d.hde[hx].x : d.dent[idx].x) == DP_NONE) {   // hot: the slot's cell is the entry
         acc.ddc++;
         atomicOr(&d.dbit[(size_t)ol * d.NBIT + (m >> 5)], 1u << (m & 31));
         if (hk == SRC_NONE) acc.dnh++;
@@ -119,8 +119,8 @@ __device__ __forceinline__ void merge_change_w(const DS &d, uint32_t ol, uint32_
         }
     }
     const uint2 cell = make_uint2(de_x(nsrc, 0), nsinc);
-    d.dent[idx] = cell;
     if (hk != SRC_NONE) d.hde[hx] = cell;
+    else d.dent[idx] = cell;
     if (d.wslot) {                                                 // watched row: MemberlistChangesAppliedEvent
         const uint32_t ws = d.wslot[ol];                           // (memberlist.go:378-383)
         if (ws != SRC_NONE) {
@@ -293,8 +293,8 @@ __device__ void wave_bump(const DS &d, uint32_t ol, const MsgDesc &md) {
             } else {
                 nx = x[u] + (1u << 24);
             }
-            dx[(size_t)m[u] * 2] = nx;
             if (hk[u] != SRC_NONE) hx[(size_t)hk[u] * 2] = nx;
+            else dx[(size_t)m[u] * 2] = nx;
         }
     }
     del = wsum(del);
@@ -403,7 +403,6 @@ __device__ uint32_t wave_issue_t(const DS &d, uint32_t ol, uint32_t sender, uint
                     } else {
                         nx = ce[u].x + (1u << 24);
                     }
-                    d.dent[rb + m[u]].x = nx;
                     d.hde[hb + k].x = nx;
                 }
             }
@@ -482,8 +481,8 @@ __device__ uint32_t wave_issue_t(const DS &d, uint32_t ol, uint32_t sender, uint
                     } else {
                         nx = ce[k].x + (1u << 24);
                     }
-                    d.dent[rb + m[k]].x = nx;
                     if (hk[k] != SRC_NONE) d.hde[hb + hk[k]].x = nx;
+                    else d.dent[rb + m[k]].x = nx;
                 }
             }
             pos += tot;
@@ -677,6 +676,17 @@ __global__ void k_hot_fill(DS d) {
         nowhot = wsum(nowhot);
         if (lane_id() == 0 && nowhot) d.nhe[ol] -= nowhot;
     }
+}
+
+// write the hot columns' cells back to the dense cells of rows [ol0, ol0 + nrows), one wave per row: for a hot
+// member the slot's cell is the entry (the dense cell is not written while the member holds a slot), so the
+// dense array is current only after this (before the slots are dropped, and before a host read-back of a row)
+__global__ void k_hot_flush(DS d, uint32_t ol0, uint32_t nrows) {
+    const uint32_t i = wave_gid();
+    if (i >= nrows) return;
+    const uint32_t ol = ol0 + i, k1 = d.hot_cnt[0];
+    const size_t rb = (size_t)ol * d.NP, hb = (size_t)ol * d.HP;
+    for (uint32_t k = lane_id(); k < k1; k += 64) d.dent[rb + d.hlist[k]] = d.hde[hb + k];
 }
 
 // memberlist.AddJoinList (memberlist.go:398-406) on observer row ol, one wave: Update of the join list
@@ -1587,7 +1597,8 @@ __global__ void k_digest(DS d, unsigned long long *out, uint32_t period_div) {
         const size_t idx = (size_t)ol * d.NP + m;
         const uint32_t w = d.mw[idx];
         r += mix4(o, m, w & 7u, w >> 3);
-        const uint2 ce = d.dent[idx];
+        const uint32_t hk = hot_slot(d, m);
+        const uint2 ce = hk != SRC_NONE ? d.hde[(size_t)ol * d.HP + hk] : d.dent[idx];
         const uint32_t p = de_p(ce.x);
         if (p != DP_NONE) {
             const uint2 a = make_uint2(de_src(ce.x), ce.y);

@@ -1,6 +1,7 @@
 """Hot columns: per-row compact copies of the row words and dissemination cells of the members that sit
 in dissemination buffers, read by issue, merge and bump instead of one scattered sector per member. They are copies,
-so no result may depend on them: these tests run workloads with the columns off (SWIMSIM_HOT_SLOTS=0), with a few
+so no result may depend on them (the slot is a hot member's dissemination cell, written back to the dense
+array before the slots are dropped or a row is read back): these tests run workloads with the columns off (SWIMSIM_HOT_SLOTS=0), with a few
 slots that overflow (members beyond them stay on the dense path) and with the default, and require every round to
 match the oracle or the column-free engine bit for bit."""
 import os
@@ -46,6 +47,9 @@ def test_cascade_same_with_and_without_hot_columns():
             assert (on.checksums() == off.checksums()).all(), f"round {r}: checksums differ"
             assert on.digest() == off.digest(), f"round {r}: state digests differ"
             assert on.counters() == off.counters(), f"round {r}: counters differ"
+            if r % 5 == 4:                                   # host read-back of the cells (hot slots flushed first)
+                for o in (0, 1, 777, wl.n - 1):
+                    assert on.changes(o) == off.changes(o), f"round {r}: row {o} dissemination cells"
         assert on.counters()["timers_fired"] > 0
     finally:
         on.close()
