@@ -776,6 +776,9 @@ int checksum_dirty(swimsim *h, int mode, bool async = false) {
 // values are the same either way; only where the work happens changes. mode: k_list's 1 (phase I senders) or
 // 2 (phase Q1 senders).
 int bound_lazy_snapshots(swimsim *h, int mode) {
+    // at most one lazy snapshot per owned row: with half the pool at least NL they always fit, and the count (a
+    // host round trip that drains the stream) is not needed
+    if (h->NL <= h->d.dense_cap / 2) return 0;
     HIPCHK(h, hipMemsetAsync(h->cnt, 0, 4, h->s));
     hipLaunchKernelGGL(k_list, dim3(blocks_for_threads(h->NL)), dim3(256), 0, h->s, h->d, mode, h->tgt, h->failed,
                        h->list, h->cnt);
@@ -1105,11 +1108,14 @@ int step_one(swimsim *h, const swimsim_event *ev, size_t nev) {
         HIPCHK(h, hipMemcpyAsync(&hi[5], h->npairs, 4, hipMemcpyDeviceToHost, h->s));
     }
     // ---- D: deliver in waves ----
-    HIPCHK(h, hipMemcpyAsync(hi + 4, h->info + 2, 4, hipMemcpyDeviceToHost, h->s));
-    HIPCHK(h, hipStreamSynchronize(h->s));
-    if (sharded) ninbox = std::min(hi[5], h->keycap);
-    const uint32_t nfailed = hi[4];
+    // (the failed-ping count info[2] reaches the host with sort_inbox's copy of info[0..3]; a sharded inbox size
+    // needs its own round trip first)
+    if (sharded) {
+        HIPCHK(h, hipStreamSynchronize(h->s));
+        ninbox = std::min(hi[5], h->keycap);
+    }
     if (int rc = sort_inbox(h, ninbox, hi)) return rc;
+    const uint32_t nfailed = hi[2];
     if (int rc = run_waves(h, 0, hi[0], hi[1])) return rc;
     if (sharded) {                                                   // responses to senders on other shards
         hipLaunchKernelGGL(k_x_resp, dim3(blocks_for_threads(ninbox)), dim3(256), 0, h->s, h->d, h->keys, ninbox, 0,
