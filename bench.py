@@ -116,6 +116,7 @@ def roofline_entry(fam, kt, units, n_members):
         if fam == "recv_merge":
             side_b = 36.0 * units["recv_issued"] + 4.0 * units["bitmap_words_per_row"] * units["recv_calls"]
             side = {"issued_per_launch": round(units["recv_issued"] / nl, 1), "calls_per_launch": round(units["recv_calls"] / nl, 1),
+                    "hot_slots_at_end": units.get("hot_slots"),
                     "issue_as_receiver_bytes_per_launch": round(side_b / nl, 1),
                     "issue_as_receiver_basis": "36 B per issued record (16-B cell gather + 16-B record write + 4-B "
                     "counter write-back) + the presence bitmap (4 B per 32 members) per call"}

@@ -219,7 +219,8 @@ int swimsim_kernel_times(swimsim_t *h, const char **names, double *avg_ms, uint6
                          double *alg_bytes, size_t cap, size_t *n);
 int swimsim_enable_timing(swimsim_t *h, int32_t enable);
 /* the unit counts behind those byte figures since swimsim_enable_timing (rows hashed by each checksum kernel,
- * changes processed / applied by each merge kernel, records issued, ...): names[i], values[i] */
+ * changes processed / applied by each merge kernel, records issued, ...): names[i], values[i]; "hot_slots" is
+ * the number of hot-column slots in use now (not a count since the reset) */
 int swimsim_kernel_units(swimsim_t *h, const char **names, double *values, size_t cap, size_t *n);
 /* profiler window marker: one tiny kernel (k_profile_mark) on the engine's stream, after the side stream drained */
 int swimsim_profile_mark(swimsim_t *h, uint32_t id);

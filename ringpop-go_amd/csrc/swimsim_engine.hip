@@ -2220,13 +2220,21 @@ int swimsim_kernel_units(swimsim_t *h, const char **names, double *values, size_
     if (int rc = read_counters(h, c)) return rc;
     static const char *kn[] = {"cs_rows_wide", "cs_rows_narrow", "cs_dup_rows", "recv_merged", "recv_applied",
                                "recv_issued", "recv_calls", "resp_merged", "resp_applied", "resp_bumped", "issued",
-                               "bitmap_words_per_row", "diag_stamp0", "diag_stamp1", "diag_stamp2", "diag_stamp3"};
+                               "bitmap_words_per_row", "diag_stamp0", "diag_stamp1", "diag_stamp2", "diag_stamp3",
+                               "hot_slots"};
     const int ki[] = {C_X_CS_ROWS, C_X_CS_ROWS_N, C_X_CS_DUP, C_X_MERGED, C_X_APPLIED, C_X_RISSUED, C_X_RCALLS,
-                      C_X_MERGED_R, C_X_APPLIED_R, C_X_BUMPED, C_X_ISSUED, -1, C_NALL, C_NALL + 1, C_NALL + 2, C_NALL + 3};
+                      C_X_MERGED_R, C_X_APPLIED_R, C_X_BUMPED, C_X_ISSUED, -1, C_NALL, C_NALL + 1, C_NALL + 2, C_NALL + 3,
+                      -2};
+    uint32_t hot = 0;                                              // hot slots in use now (not a delta)
+    if (h->d.hot_cnt) {
+        HIPCHK(h, hipMemcpyAsync(&hot, h->d.hot_cnt, 4, hipMemcpyDeviceToHost, h->s));
+        HIPCHK(h, hipStreamSynchronize(h->s));
+    }
     const size_t k = sizeof(ki) / sizeof(ki[0]);
     for (size_t i = 0; i < k && i < cap; i++) {
         if (names) names[i] = kn[i];
-        if (values) values[i] = ki[i] < 0 ? (double)h->d.NBIT : (double)(c[ki[i]] - h->fam_bytes_base[ki[i]]);
+        if (values)
+            values[i] = ki[i] == -1 ? (double)h->d.NBIT : ki[i] == -2 ? (double)hot : (double)(c[ki[i]] - h->fam_bytes_base[ki[i]]);
     }
     if (n) *n = k;
     return SWIMSIM_OK;

@@ -40,6 +40,25 @@ void run(int grid, int threads, int ldsw_kind) {
             c[(v >> 4) & 3]++;
             wave_simd[w][(v >> 4) & 3]++;
         }
+    // role composition of every SIMD: how many wave-0s and wave-1s (formatter / hasher of k_checksum3) share it
+    std::map<uint64_t, std::vector<int>> simd_roles;        // (cu key, simd) -> waves per role
+    for (int b = 0; b < grid; b++)
+        for (int w = 0; w < threads / 64; w++) {
+            const uint32_t v = h[2 * (b * 16 + w)], x = h[2 * (b * 16 + w) + 1] & 15;
+            const uint64_t key = ((uint64_t)x << 40) | ((uint64_t)((v >> 4) & 3) << 32) | (((v >> 13) & 7) << 8) |
+                                 (((v >> 12) & 1) << 4) | ((v >> 8) & 15);
+            auto &c = simd_roles[key];
+            if (c.empty()) c.assign(threads / 64, 0);
+            c[w]++;
+        }
+    std::map<std::vector<int>, int> rhist;
+    for (auto &kv : simd_roles) rhist[kv.second]++;
+    printf("   waves of each role per SIMD (wave 0, wave 1, ...) -> SIMDs:\n");
+    for (auto &kv : rhist) {
+        printf("     [");
+        for (size_t i = 0; i < kv.first.size(); i++) printf("%s%d", i ? " " : "", kv.first[i]);
+        printf("] x %d\n", kv.second);
+    }
     std::map<std::vector<int>, int> hist;
     for (auto &kv : cu) hist[kv.second]++;
     printf("grid %d x %d threads (LDS %s): %zu CUs used; waves per SIMD pattern -> CUs:\n", grid, threads,
@@ -55,6 +74,7 @@ void run(int grid, int threads, int ldsw_kind) {
 
 int main() {
     run(1024, 128, 0);
+    run(512, 128, 0);
     run(1024, 128, 1);
     run(768, 320, 0);
     run(4096, 64, 1);
