@@ -225,9 +225,15 @@ int swimsim_kernel_units(swimsim_t *h, const char **names, double *values, size_
 /* profiler window marker: one tiny kernel (k_profile_mark) on the engine's stream, after the side stream drained */
 int swimsim_profile_mark(swimsim_t *h, uint32_t id);
 /* time the checksum kernel alone on the first nrows rows — average ms per launch. mode 0: the production choice for
- * nrows rows, 1: the wide kernel (k_checksum3), 2: the narrow kernel (k_checksum_q16); other modes (diagnostic
+ * nrows rows, 1: the wide kernel (k_checksum3), 2: the narrow kernel (k_checksum_q16), 3: the reference-row path
+ * (reference row, k_csd_scan, k_cs_delta and the fallback launch for the rows it leaves); other modes (diagnostic
  * variants) only in the diagnostics library tools/libswimsim_diag.so */
 int swimsim_bench_checksum(swimsim_t *h, uint32_t nrows, int32_t mode, int32_t reps, double *ms);
+/* the reference-row checksum path so far (swimsim_checksum_delta.hip; SWIMSIM_CS_DELTA = 0 off, 1 wide launches,
+ * 2 every launch of >= 1024 rows): its launches, the rows it left to the production kernels and, per reason (7
+ * entries: short string, entry capacity, workgroup window, entry batch, exception slots, jump slots, window miss),
+ * how many of those rows had it */
+int swimsim_checksum_path_stats(swimsim_t *h, uint64_t *delta_launches, uint64_t *fallback_rows, uint64_t *reasons);
 /* diagnostics library only: the 32-bit words of every 20-byte block the checksum kernel hashes for row o (W = 19) */
 int swimsim_debug_cs_stream(swimsim_t *h, uint32_t o, uint32_t *out, size_t cap_words);
 

@@ -17,6 +17,14 @@
 
 #include <type_traits>
 
+// address widths the checksum kernels are instantiated for (W = 13..20 bytes; a development build with
+// -DSWIMSIM_DEV_W19 compiles W = 19 only, the workloads' width, in a third of the time)
+#ifdef SWIMSIM_DEV_W19
+#define CS_W_CASES(X) X(19)
+#else
+#define CS_W_CASES(X) X(13) X(14) X(15) X(16) X(17) X(18) X(19) X(20)
+#endif
+
 constexpr int CS_ROWS = 64;                     // rows per workgroup of the wide kernel
 constexpr int CS_PRE = 12;                      // spill area in front of a row's ring (narrow kernel)
 constexpr int CS_RW = 11;                       // record words of the prologue record (<= 44 bytes)
@@ -134,6 +142,7 @@ constexpr int cs_no(int W, int maxtail) { return (3 + W + maxtail + 3) / 4; }
 
 #include "swimsim_checksum3.hip"
 #include "swimsim_checksum4.hip"
+#include "swimsim_checksum_delta.hip"
 #ifdef SWIMSIM_DIAG                            // tools/diag (diagnostics library only): the 3-wave and
 #include "swimsim_checksum5.hip"               // fast-path experiments and every superseded kernel
 #include "swimsim_checksum6.hip"
@@ -160,7 +169,7 @@ void launch_checksum_kind(const DS &d, const uint32_t *list, const uint32_t *cou
         const uint32_t grid = (n + CS_ROWS - 1) / CS_ROWS;
         switch (d.W) {
 #define CS_CASE(Wv) case Wv: launch_cs3_w<Wv>(d, list, count, grid, s); break;
-            CS_CASE(13) CS_CASE(14) CS_CASE(15) CS_CASE(16) CS_CASE(17) CS_CASE(18) CS_CASE(19) CS_CASE(20)
+            CS_W_CASES(CS_CASE)
 #undef CS_CASE
         default: break;
         }
@@ -172,7 +181,7 @@ void launch_checksum_kind(const DS &d, const uint32_t *list, const uint32_t *cou
         if (ngrid <= g_csq16_groups) launch_csq_w<Wv, 16>(d, list, count, ngrid, s);        \
         else launch_csq_w<Wv, 8>(d, list, count, ngrid, s);                                 \
         break;
-            CS_CASE(13) CS_CASE(14) CS_CASE(15) CS_CASE(16) CS_CASE(17) CS_CASE(18) CS_CASE(19) CS_CASE(20)
+            CS_W_CASES(CS_CASE)
 #undef CS_CASE
         default: break;
         }

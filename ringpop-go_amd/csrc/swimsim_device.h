@@ -36,9 +36,10 @@ enum Counter {
     C_TIMERS_FIRED, C_MSG_CHANGES, C_HEAL_ATTEMPTS, C_HEAL_FAILURES, C_NCOUNTERS,
     // measurement-only counters (not part of the parity record)
     // (merges and applies of k_recv and k_resp are counted apart: C_X_MERGED + 5 / C_X_APPLIED + 5)
-    // (C_X_CS_ROWS / C_X_CS_ROWS_N: rows hashed by k_checksum3 / k_checksum_q16 launches, snapshots included)
+    // (C_X_CS_ROWS / C_X_CS_ROWS_N: rows hashed by k_checksum3 or k_cs_delta / k_checksum_q16 launches, snapshots
+    // included; C_X_CSD_SCANNED: rows k_csd_scan read)
     C_X_MERGED = C_NCOUNTERS, C_X_APPLIED, C_X_ISSUED, C_X_CS_ROWS, C_X_CS_DUP,
-    C_X_MERGED_R, C_X_APPLIED_R, C_X_RISSUED, C_X_RCALLS, C_X_BUMPED, C_X_CS_ROWS_N, C_NALL
+    C_X_MERGED_R, C_X_APPLIED_R, C_X_RISSUED, C_X_RCALLS, C_X_BUMPED, C_X_CS_ROWS_N, C_X_CSD_SCANNED, C_NALL
 };
 
 constexpr int CTR_SHARDS = 64, CTR_STRIDE = 40;   // d.ctr is [CTR_SHARDS][CTR_STRIDE] u64

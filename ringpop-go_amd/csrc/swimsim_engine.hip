@@ -41,11 +41,13 @@ struct Timed {
 // them (dirty lists, dedup, deferred-decision lists)
 // F_RECV times exactly the k_recv dispatches (phases D and Q2), so its launch count and average match
 // the profiler's; their deferred-decision epilogues are F_RECVFIN
+// With the reference-row path on, F_CS_WIDE times the k_cs_delta dispatches and F_CSD_SCAN the work before them
+// (reference row, reference string, k_csd_scan); rows it leaves to the production kernels are timed as they are.
 enum Fam { F_TIMERS, F_SELECT, F_ISSUE, F_SORT, F_RECV, F_RESP, F_PINGREQ, F_JOBS, F_CS_WIDE, F_CS_NARROW, F_CSPREP,
-           F_EVENTS, F_XCHG, F_RECVFIN, F_NFAM };
+           F_EVENTS, F_XCHG, F_RECVFIN, F_CSD_SCAN, F_NFAM };
 const char *kFamName[F_NFAM] = {"timers", "select", "issue", "sort", "recv_merge", "resp_merge", "pingreq",
                                 "rfs_jobs", "checksum_wide", "checksum_narrow", "checksum_prep", "events", "exchange",
-                                "recv_finish"};
+                                "recv_finish", "checksum_delta_scan"};
 
 // ---------------------------------------------------------------------------------------------
 // shard transports: how parcels move between the shards of one cluster
@@ -326,6 +328,17 @@ struct swimsim {
     std::vector<uint32_t> wcs_ev;                 // the same for the per-Update stream's drains
     uint4 *wout = nullptr;
     uint32_t *winfo = nullptr;
+    // reference-row checksum path (swimsim_checksum_delta.hip), allocated at its first launch
+    int csd_mode = 0;                             // SWIMSIM_CS_DELTA: 0 off, 1 wide launches, 2 every launch >= 1024 rows
+    bool csd_ready = false, csd_failed = false;
+    uint32_t csd_rows = 0;                        // rows a launch may hold
+    uint32_t *csd_B = nullptr, *csd_Lb = nullptr, *csd_OB = nullptr, *csd_SBw = nullptr, *csd_fb = nullptr,
+             *csd_fbcnt = nullptr;
+    size_t csd_sbw_words = 0;
+    uint4 *csd_ent = nullptr;
+    CsdRow *csd_rinfo = nullptr;
+    uint32_t csd_ecap = 1024;
+    uint64_t csd_launches = 0, csd_fallback_rows = 0, csd_reasons[CSD_NFLAGS] = {0};
     std::string err;
 
     int fail(int code, const char *fmt, ...) {
@@ -645,6 +658,90 @@ int shard_sum(swimsim *h, uint64_t v, uint64_t *out) {
 // checksums of the dirty rows selected by mode (k_list). Mode 0 (all dirty rows) hashes one row per
 // distinct content: rows are grouped by fingerprint, compared word for word with their group's first
 // row, and equal rows copy its checksum (k_fp_*).
+// the reference-row path (swimsim_checksum_delta.hip) for launches of n rows (n known on the host)
+bool csd_wanted(swimsim *h, uint32_t n, CsKind kind) {
+    if (h->csd_mode == 0 || h->csd_failed || n < CSD_MIN_ROWS || h->N < 1024) return false;
+    return kind == CS_WIDE || h->csd_mode == 2;
+}
+
+int csd_alloc(swimsim *h) {
+    if (h->csd_ready) return 0;
+    h->csd_rows = h->NL;
+    h->csd_sbw_words = ((size_t)h->N * (h->W + 32) + 256) / 4;
+    int rc = 0;
+    if ((rc = dalloc(h, &h->csd_B, (size_t)h->NP, "csd reference row")) ||
+        (rc = dalloc(h, &h->csd_Lb, (size_t)h->N + 1, "csd reference lengths")) ||
+        (rc = dalloc(h, &h->csd_OB, (size_t)h->N + 1, "csd reference offsets")) ||
+        (rc = dalloc(h, &h->csd_SBw, h->csd_sbw_words, "csd reference string")) ||
+        (rc = dalloc(h, &h->csd_fb, (size_t)h->csd_rows, "csd fallback list")) ||
+        (rc = dalloc(h, &h->csd_fbcnt, 1 + CSD_NFLAGS, "csd fallback count")) ||
+        (rc = dalloc(h, &h->csd_rinfo, (size_t)h->csd_rows, "csd row info")) ||
+        (rc = dalloc(h, &h->csd_ent, (size_t)h->csd_rows * h->csd_ecap * 2, "csd exception entries"))) {
+        h->csd_failed = true;                                      // the production kernels stay in charge
+        h->err.clear();
+        return rc;
+    }
+    size_t need = 0;
+    hipcub::DeviceScan::ExclusiveSum(nullptr, need, h->csd_Lb, h->csd_OB, (int)h->N + 1, h->s);
+    if (need > h->cub_bytes) {
+        void *p = nullptr;
+        if (hipMalloc(&p, need) != hipSuccess) { h->csd_failed = true; return SWIMSIM_ENOMEM; }
+        h->allocs.push_back(p);
+        h->alloc_bytes += need;
+        h->cub_tmp = p;
+        h->cub_bytes = need;
+    }
+    h->csd_ready = true;
+    return 0;
+}
+
+// hash the n listed rows (count on the device) by the reference-row path. Returns 0 when every row is hashed, 1 when
+// the path is unavailable (the caller hashes them), < 0 on a HIP error (h->err set)
+int csd_hash(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t n) {
+    if (n > h->NL) return 1;
+    if (csd_alloc(h)) return 1;
+    CsdArgs a{};
+    a.B = h->csd_B;
+    a.OB = h->csd_OB;
+    a.SBw = h->csd_SBw;
+    a.sbw_words = (uint32_t)h->csd_sbw_words;
+    a.ent = h->csd_ent;
+    a.rinfo = h->csd_rinfo;
+    a.ecap = h->csd_ecap;
+    a.fb_list = h->csd_fb;
+    a.fb_cnt = h->csd_fbcnt;
+    {
+        Scope sc(h, F_CSD_SCAN);
+        hipLaunchKernelGGL(k_csd_ref, dim3((h->N + 256) / 256), dim3(256), 0, h->s, h->d, list, n, h->csd_B, h->csd_Lb);
+        size_t bytes = h->cub_bytes;
+        HIPCHK(h, hipcub::DeviceScan::ExclusiveSum(h->cub_tmp, bytes, h->csd_Lb, h->csd_OB, (int)h->N + 1, h->s));
+        HIPCHK(h, hipMemsetAsync(h->csd_SBw, 0, h->csd_sbw_words * 4, h->s));
+        launch_csd(h->d, list, n, cnt, a, h->s, 0);
+        launch_csd(h->d, list, n, cnt, a, h->s, 1);
+        HIPCHK(h, hipMemsetAsync(h->csd_fbcnt, 0, 4 * (1 + CSD_NFLAGS), h->s));
+        hipLaunchKernelGGL(k_ctr_add, dim3(1), dim3(1), 0, h->s, h->d, (int)C_X_CSD_SCANNED, (unsigned long long)n);
+    }
+    {
+        Scope sc(h, F_CS_WIDE);
+        launch_csd(h->d, list, n, cnt, a, h->s, 2);
+    }
+    h->csd_launches++;
+    // rows the path left (flags): hashed by the production kernels
+    uint32_t hf[1 + CSD_NFLAGS];
+    HIPCHK(h, hipMemcpyAsync(h->hinfo + 16, h->csd_fbcnt, 4 * (1 + CSD_NFLAGS), hipMemcpyDeviceToHost, h->s));
+    HIPCHK(h, hipStreamSynchronize(h->s));
+    memcpy(hf, h->hinfo + 16, sizeof hf);
+    const uint32_t nf = hf[0];
+    if (nf) {
+        h->csd_fallback_rows += nf;
+        for (uint32_t b = 0; b < CSD_NFLAGS; b++) h->csd_reasons[b] += hf[1 + b];
+        const CsKind k2 = cs_kind(nf);
+        Scope sc(h, k2 == CS_WIDE ? F_CS_WIDE : F_CS_NARROW);
+        launch_checksum_kind(h->d, h->csd_fb, h->csd_fbcnt, nf, k2, h->s);
+    }
+    return 0;
+}
+
 // one FarmHash dispatch over the rows listed (count on the device; nrows = the count if the host
 // knows it, else ~0u), timed as F_CS_WIDE / F_CS_NARROW
 // A main-stream launch of a known number of rows (at least 64) hashes them in row order: lists come out of atomic
@@ -666,6 +763,10 @@ void hash_rows(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t m
     }
     const uint32_t n = std::min(maxn, nrows);
     const CsKind kind = cs_kind(n);
+    if (!st && nrows != ~0u && csd_wanted(h, n, kind)) {
+        const int rc = csd_hash(h, list, cnt, n);
+        if (rc <= 0) return;                                       // done (or failed loudly: h->err)
+    }
     Scope sc(h, kind == CS_WIDE ? F_CS_WIDE : F_CS_NARROW, st);
     launch_checksum_kind(h->d, list, cnt, n, kind, st ? st : h->s);
 }
@@ -1343,6 +1444,7 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
     }
     if (const char *v = getenv("SWIMSIM_CS_ASYNC")) h->cs_async = atoi(v) != 0;
     if (const char *v = getenv("SWIMSIM_CS_NARROW_ROWS")) g_cs_narrow_rows = (uint32_t)strtoul(v, nullptr, 10);
+    if (const char *v = getenv("SWIMSIM_CS_DELTA")) h->csd_mode = atoi(v);
     DS &d = h->d;
     d.N = h->N; d.NP = h->NP; d.NL = h->NL; d.lo = h->lo;
     d.NB = h->NP / 64;
@@ -1499,7 +1601,7 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
         h->shard_lo = {0, h->N};
         d.G = 1; d.rank = 0; d.shard_lo = sl;
     }
-    if (hipHostMalloc((void **)&h->hinfo, 64, 0) != hipSuccess) return bail(SWIMSIM_ENOMEM);
+    if (hipHostMalloc((void **)&h->hinfo, 128, 0) != hipSuccess) return bail(SWIMSIM_ENOMEM);
     hipMemset(d.ctr, 0, (size_t)CTR_SHARDS * CTR_STRIDE * 8);
     hipMemset(d.err, 0, 4);
     hipMemset(h->need, 0, h->N);
@@ -1878,10 +1980,13 @@ __global__ void k_iota(uint32_t *list, uint32_t *cnt, uint32_t n) {
 int swimsim_bench_checksum(swimsim_t *h, uint32_t nrows, int32_t mode, int32_t reps, double *ms) {
     if (!h || !ms || nrows == 0 || nrows > h->NL || reps < 1) return SWIMSIM_EINVAL;
 #ifndef SWIMSIM_DIAG
-    if (mode < 0 || mode > 2) return h->fail(SWIMSIM_EINVAL, "checksum mode %d: diagnostics build only", mode);
+    if (mode < 0 || mode > 3) return h->fail(SWIMSIM_EINVAL, "checksum mode %d: diagnostics build only", mode);
 #endif
+    // mode 3: the reference-row path (swimsim_checksum_delta.hip), its preparation and any fallback launch included
+    if (mode == 3 && (csd_alloc(h) || nrows > h->NL)) return h->fail(SWIMSIM_EINVAL, "reference-row path unavailable");
     auto launch = [&]() {
-        if (mode <= 2) launch_checksum_kind(h->d, h->list, h->cnt, nrows, mode == 0 ? cs_kind(nrows) : (CsKind)mode, h->s);
+        if (mode == 3) (void)csd_hash(h, h->list, h->cnt, nrows);
+        else if (mode <= 2) launch_checksum_kind(h->d, h->list, h->cnt, nrows, mode == 0 ? cs_kind(nrows) : (CsKind)mode, h->s);
 #ifdef SWIMSIM_DIAG
         else launch_checksum_mode(h->d, h->list, h->cnt, nrows, mode, h->s);
 #endif
@@ -2203,6 +2308,7 @@ int swimsim_kernel_times(swimsim_t *h, const char **names, double *avg_ms, uint6
             if (f == F_CS_WIDE) b = csrows * 5.0 * h->N;       // every hashed row, SURVEY.md §8(d) 5 B per member
             if (f == F_CS_NARROW) b = delta(C_X_CS_ROWS_N) * 5.0 * h->N;
             if (f == F_CSPREP) b = csdups * 8.0 * h->N;        // duplicates verified word for word
+            if (f == F_CSD_SCAN) b = delta(C_X_CSD_SCANNED) * 4.0 * h->N;   // every listed row read once
             if (f == F_ISSUE) b = issued * 32.0;
             if (f == F_RECV) b = merge_bytes + recv_issue_bytes;   // k_recv merges (and the few other
             if (f == F_RESP) b = resp_bytes;                        // merges) + its issue; k_resp
@@ -2379,6 +2485,15 @@ int swimsim_debug_exchange(swimsim_t *h, const uint8_t *send, const uint64_t *sb
     hipFree(ds);
     hipFree(dr);
     return rc ? h->fail(rc, "debug exchange: data (%s)", h->xp->name()) : SWIMSIM_OK;
+}
+
+int swimsim_checksum_path_stats(swimsim_t *h, uint64_t *delta_launches, uint64_t *fallback_rows, uint64_t *reasons) {
+    if (!h) return SWIMSIM_EINVAL;
+    if (delta_launches) *delta_launches = h->csd_launches;
+    if (fallback_rows) *fallback_rows = h->csd_fallback_rows;
+    if (reasons)
+        for (uint32_t b = 0; b < CSD_NFLAGS; b++) reasons[b] = h->csd_reasons[b];
+    return SWIMSIM_OK;
 }
 
 int swimsim_shard_info(swimsim_t *h, uint32_t *nshards, uint32_t *rank, uint32_t *lo, uint32_t *hi,

@@ -138,6 +138,7 @@ def load_library(path: str = LIB_PATH):
         "swimsim_kernel_times": (C.c_int, [P, P, P, P, P, sz, C.POINTER(sz)]),
         "swimsim_enable_timing": (C.c_int, [P, i32]),
         "swimsim_bench_checksum": (C.c_int, [P, u32, i32, i32, C.POINTER(C.c_double)]),
+        "swimsim_checksum_path_stats": (C.c_int, [P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), _U64P]),
         "swimsim_kernel_units": (C.c_int, [P, P, P, sz, C.POINTER(sz)]),
         "swimsim_profile_mark": (C.c_int, [P, u32]),
         "swimsim_debug_cs_stream": (C.c_int, [P, u32, P, sz]),
@@ -528,6 +529,16 @@ class Cluster:
                                                     C.byref(xb), C.byref(xc)))
         return {"shards": g.value, "rank": r.value, "lo": lo.value, "hi": hi.value, "exchanged_bytes": xb.value,
                 "exchanges": xc.value}
+
+    CSD_REASONS = ("short", "entry_cap", "window_plan", "entry_batch", "exception_slots", "jump_slots", "window_miss")
+
+    def checksum_path_stats(self):
+        dl, fb = C.c_uint64(), C.c_uint64()
+        rs = np.zeros(len(self.CSD_REASONS), np.uint64)
+        self._chk(load_library().swimsim_checksum_path_stats(self.h, C.byref(dl), C.byref(fb),
+                                                             rs.ctypes.data_as(_U64P)))
+        return {"delta_launches": dl.value, "fallback_rows": fb.value,
+                "reasons": {k: int(v) for k, v in zip(self.CSD_REASONS, rs)}}
 
     def debug_cs_stream(self, o, nwords):
         """the words of every 20-byte block the checksum kernel hashes for observer o (diagnostics)"""
