@@ -30,21 +30,24 @@
 // (a', b', c' = the next block's first words, zero after the last block, so that X ends as the state itself).
 
 constexpr int CSD_SB = 32;            // blocks per super step
+constexpr int CSD_PF = 4;             // blocks the chain waves' LDS reads run ahead
 constexpr int CSD_ROWS = 256;         // rows per workgroup
-constexpr int CSD_HW = 4;             // hasher waves (waves 0..3); helper waves 4..7 serve the same rows
-constexpr int CSD_THREADS = 512;
-constexpr int CSD_PWENT = 1280;       // premixed S_B blocks per window buffer (phases x positions)
+constexpr int CSD_HW = 4;             // row groups of 64: h-chain waves 0..3, g/f-chain waves 4..7, helper waves 8..11
+constexpr int CSD_THREADS = 768;
+constexpr int CSD_RING = 2240;        // premixed S_B blocks in the window ring (phases x (ring + mirror) positions)
 // exception slots per helper wave per buffer: differing members are column-correlated (the members whose state is
 // in flux differ in many rows at once), so a super step can hold a run of 3-4 exception blocks in every row
-constexpr int CSD_EXW = 384;
+constexpr int CSD_EXW = 320;
 constexpr int CSD_NJ = 6;             // jumps per row per super step (block 0, then a start and an end per run)
 constexpr int CSD_E = 8;              // exception entries a helper lane holds in registers
 constexpr uint32_t CSD_NOJ = 0xFFFFu; // unused jump slot
 constexpr uint32_t CSD_JB = 128;      // jump word: block i << 16 | (target - 3 i + CSD_JB), target in uint2 units
+constexpr int CSD_JWMAX = 160;        // window positions at most (the workgroup's shifts spread < 2,500 bytes)
+constexpr int CSD_SBST = 5 * CSD_SB + 16;      // staged S_B words per super step (its SB new positions)
 constexpr uint32_t CSD_C = 0xe6546b64u;
 constexpr uint32_t CSD_MIN_ROWS = 1024; // launches of fewer rows keep the production kernels
-// LDS of k_cs_delta in uint2 units: two window buffers, then 2 x 4 exception regions
-constexpr int CSD_EXB = 2 * CSD_PWENT * 3;
+// LDS of k_cs_delta in uint2 units: the window ring, then 2 x 4 exception regions
+constexpr int CSD_EXB = CSD_RING * 3;
 constexpr int CSD_LDS2 = CSD_EXB + 2 * CSD_HW * CSD_EXW * 3;
 
 // per listed row: what k_csd_scan found (32 B)
@@ -68,6 +71,9 @@ struct CsdArgs {
     CsdRow *rinfo;            // [rows]
     uint32_t ecap;
     uint32_t *fb_list, *fb_cnt; // rows left to the production kernels; fb_cnt[1 + b]: rows with flag bit b
+    uint32_t dmode;           // diagnostics (swimsim_bench_checksum modes 31..46 = dmode + 30, garbage checksums): 1 helpers
+                              // alone, 2 chains alone, 3 helpers without the exception work; bit 8: no barrier between
+                              // super steps; 0 in production
 };
 
 __device__ __forceinline__ const uint32_t *csd_row(const DS &d, uint32_t id) {
@@ -198,9 +204,9 @@ __global__ void __launch_bounds__(256) k_csd_scan(DS d, const uint32_t *list, ui
     // CSD_SU chunks of 64 members per pass, their loads in flight together (a row is one 256-KB stream). Chunks with
     // differing members are staged in LDS, and the pass's diffs are walked by a loop that is not unrolled; runs wait
     // in LDS for their entries, generated (one lane per run) between passes.
-    constexpr uint32_t CSD_SU = 16, RUNCAP = 256, RUNFLUSH = 128;
+    constexpr uint32_t CSD_SU = 8, RUNCAP = 128, RUNFLUSH = 64;
     __shared__ uint32_t runs[4][RUNCAP][6];                         // {klo, khi, m0, o0, s_after, first entry}
-    __shared__ uint32_t stw[4][CSD_SU][64], stb[4][CSD_SU][64];     // staged row / reference words of a pass
+    __shared__ uint32_t stw[4][CSD_SU][64];                         // staged row words of a pass
     __shared__ uint64_t stm[4][CSD_SU];                             // their diff masks
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
     const uint32_t i = blockIdx.x * 4 + wv;
@@ -285,10 +291,7 @@ __global__ void __launch_bounds__(256) k_csd_scan(DS d, const uint32_t *list, ui
 #pragma unroll
         for (uint32_t k = 0; k < CSD_SU; k++) {
             const uint64_t mk = __ballot(c00 + 64 * k + lane < N && !csd_same(wv_[k], bv_[k]));
-            if (mk) {
-                stw[wv][k][lane] = wv_[k];
-                stb[wv][k][lane] = bv_[k];
-            }
+            if (mk) stw[wv][k][lane] = wv_[k];
             if (lane == 0) stm[wv][k] = mk;
             any |= mk ? 1u : 0u;
         }
@@ -299,7 +302,8 @@ __global__ void __launch_bounds__(256) k_csd_scan(DS d, const uint32_t *list, ui
             while (mask && !flags) {                                // the chunk's differing members, in order
                 const uint32_t l = (uint32_t)__builtin_ctzll(mask);
                 mask &= mask - 1;
-                diff(c00 + 64 * k + l, stw[wv][k][l], stb[wv][k][l]);
+                const uint32_t mm = c00 + 64 * k + l;
+                diff(mm, stw[wv][k][l], a.B[mm]);
             }
         }
         wsync();
@@ -334,20 +338,65 @@ __device__ __forceinline__ uint32_t csd_alignbyte(uint32_t hi, uint32_t lo, uint
     return __builtin_amdgcn_alignbyte(hi, lo, sh);
 }
 
+// one block of the coupled g and f lanes in carried-sum form, the two lanes' instructions interleaved (a wave issues in
+// order: each of a pair's dependent successors then waits one instruction less)
+__device__ __forceinline__ void csd_gf_step(uint32_t &Xg, uint32_t &Xf, uint32_t mg, uint32_t dd, uint32_t mf, uint32_t pf) {
+    uint32_t tg, tf;
+    asm volatile("v_xor_b32 %2, %0, %4\n\t"
+                 "v_xor_b32 %3, %1, %6\n\t"
+                 "v_alignbit_b32 %2, %2, %2, 19\n\t"
+                 "v_alignbit_b32 %3, %3, %3, 19\n\t"
+                 "v_lshl_add_u32 %2, %2, 2, %2\n\t"
+                 "v_lshl_add_u32 %3, %3, 2, %3\n\t"
+                 "v_add3_u32 %1, %3, %2, %7\n\t"
+                 "v_add3_u32 %0, %2, %1, %5"
+                 : "+v"(Xg), "+v"(Xf), "=&v"(tg), "=&v"(tf)
+                 : "v"(mg), "v"(dd), "v"(mf), "v"(pf));
+}
+// one block of the h lane: Xh' = 5 ror(Xh ^ Mh, 19) + KH
+__device__ __forceinline__ void csd_h_step(uint32_t &Xh, uint32_t mh, uint32_t kh) {
+    asm volatile("v_xor_b32 %0, %0, %1\n\t"
+                 "v_alignbit_b32 %0, %0, %0, 19\n\t"
+                 "v_lshl_add_u32 %0, %0, 2, %0\n\t"
+                 "v_add_u32 %0, %0, %2"
+                 : "+v"(Xh)
+                 : "v"(mh), "v"(kh));
+}
+
 template <int W>
 __global__ void __launch_bounds__(CSD_THREADS) k_cs_delta(DS d, const uint32_t *list, const uint32_t *count, CsdArgs a) {
-    __shared__ uint2 L2[CSD_LDS2];                       // window buffers, then exception regions (24-B entries)
-    __shared__ uint32_t jl[2][CSD_ROWS][CSD_NJ];         // per row: jump words (CSD_JB); block CSD_NOJ: unused
-    __shared__ uint32_t uni[2][CSD_HW];                  // per hasher wave: blocks where some lane jumps
+    __shared__ uint2 L2[CSD_LDS2];                       // window ring, then exception regions (24-B entries)
+    __shared__ __attribute__((aligned(8))) uint32_t jl[2][CSD_ROWS][CSD_NJ];   // per row: jump words (CSD_JB);
+                                                                                // block CSD_NOJ: unused
+    __shared__ uint32_t uni[2][CSD_HW];                  // per row group of 64: blocks where some lane jumps
+    __shared__ uint32_t xcnt[2][CSD_HW];                 // exception slots taken, per helper wave and buffer
     __shared__ uint32_t rflag[CSD_ROWS];
+    __shared__ uint32_t xh[CSD_ROWS];                    // the h lanes' results, for the g/f waves' finalisation
     __shared__ int32_t plan[4];
     __shared__ uint32_t phs[20];
+    __shared__ uint32_t sbst[2][CSD_SBST];               // S_B words of the window's new positions, staged ahead
+    __shared__ uint32_t simd_n[4];
     const uint32_t cnt = *count;
     const uint32_t g0 = blockIdx.x * CSD_ROWS;
     if (g0 >= cnt) return;                                          // uniform per workgroup
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
-    const bool hasher = wave < (uint32_t)CSD_HW;
-    const uint32_t hw = wave & 3u;
+    // roles by SIMD: every SIMD should run one h-chain wave, one g/f-chain wave and one helper wave of the same 64
+    // rows (two chain waves of one role on a SIMD would share its integer VALU issue, ~2.6 cycles an instruction,
+    // and take twice as long). The hardware's placement of a workgroup's waves is read from HW_ID; if it is not
+    // three waves per SIMD, the roles follow the wave index.
+    uint32_t hwid;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+    const uint32_t simd = (hwid >> 4) & 3u;
+    if (threadIdx.x < 4) simd_n[threadIdx.x] = 0u;
+    __syncthreads();
+    uint32_t slot = 0;
+    if (lane == 0) slot = atomicAdd(&simd_n[simd], 1u);
+    slot = __builtin_amdgcn_readfirstlane(slot);
+    __syncthreads();
+    const bool even = simd_n[0] == 3u && simd_n[1] == 3u && simd_n[2] == 3u && simd_n[3] == 3u;
+    const uint32_t role = even ? slot : wave >> 2;                  // 0: h chains, 1: g/f chains, 2: helpers
+    const uint32_t hw = even ? simd : wave & 3u;
+    if (!even && threadIdx.x == 0) ctr_add(d, C_NALL, 1ull);       // diagnostics: uneven placements
     const uint32_t r = hw * 64 + lane;                              // this lane's row
     const uint32_t gi = g0 + r;
     const bool valid = gi < cnt;
@@ -362,7 +411,7 @@ __global__ void __launch_bounds__(CSD_THREADS) k_cs_delta(DS d, const uint32_t *
     // ---- plan: the workgroup's shift range and phases
     if (threadIdx.x == 0) { plan[0] = 0x7FFFFFFF; plan[1] = -0x7FFFFFFF - 1; plan[2] = 0; plan[3] = 0; }
     __syncthreads();
-    if (hasher) {
+    if (role == 0) {
         rflag[r] = live ? 0u : (ri.flags ? ri.flags : CSD_F_SHORT);
         if (live) {
             atomicMin(&plan[0], ri.smin);
@@ -377,19 +426,24 @@ __global__ void __launch_bounds__(CSD_THREADS) k_cs_delta(DS d, const uint32_t *
     const uint32_t maxit = (uint32_t)plan[3];
     if (phm == 0) { phm = 1; smin = 0; smax = 0; }
     const int32_t cmax = -csd_floordiv20(-smax), fmin = csd_floordiv20(smin);
-    const int32_t joff = -cmax - 1;                                 // window of super step t: S_B blocks from t SB + joff
+    // window of super step t: S_B blocks (20-byte positions) jlo0 + t SB + [0, JW), kept in a ring of R positions per
+    // phase (+ a mirror of the first CSD_SB so that a row's 32 consecutive positions never wrap)
+    const int32_t jlo0 = -cmax - 1;
     const uint32_t JW = (uint32_t)(CSD_SB + cmax - fmin + 2);
+    const uint32_t R = JW + CSD_SB, RS = R + CSD_SB;
     const uint32_t nph = (uint32_t)__popc(phm);
-    const bool feasible = nph * JW <= (uint32_t)CSD_PWENT;
+    const bool feasible = nph * RS <= (uint32_t)CSD_RING && JW <= (uint32_t)CSD_JWMAX;
     const uint32_t T = feasible ? (maxit + CSD_SB - 1) / CSD_SB : 0u;
     if (threadIdx.x < 20 && ((phm >> threadIdx.x) & 1u)) phs[__popc(phm & ((1u << threadIdx.x) - 1u))] = threadIdx.x;
-    if (!feasible && hasher) rflag[r] |= CSD_F_PLAN;
+    if (!feasible && role == 0) rflag[r] |= CSD_F_PLAN;
     __syncthreads();
+    // uint2 index of the ring slot holding position p (relative to jlo0) of phase slot ps
+    // uint2 index of ring slot `slot` (< R) of phase slot ps
+    auto ring_at = [&](uint32_t ps, uint32_t slot) -> uint32_t { return 3u * (ps * RS + slot); };
 
-    if (!hasher) {
+    if (role == 2) {
         // ================================= helpers =================================
         const uint32_t th = r;                                      // 0..255
-        const uint32_t lenB = a.OB[d.N];
         const uint4 *ent = a.ent + (size_t)(valid ? gi : g0) * a.ecap * 2;
         const uint32_t ecnt = live ? ri.ecnt : 0u;
         int32_t s = 0;
@@ -412,64 +466,97 @@ __global__ void __launch_bounds__(CSD_THREADS) k_cs_delta(DS d, const uint32_t *
             }
         };
         load_batch();
-        // window entries q = th + 256 u of every super step; their S_B words are loaded one super step ahead (a
-        // global load takes longer than a super step's 32 blocks of chain)
-        constexpr int QL = (CSD_PWENT + 255) / 256;
-        const uint32_t nent = nph * JW;
-        uint32_t xs[QL][9];
-        auto entry_off = [&](uint32_t tp, uint32_t q) -> int32_t {
-            const uint32_t slot = q / JW, jr = q - slot * JW;
-            return 20 * ((int32_t)(tp * CSD_SB) + joff + (int32_t)jr) + (int32_t)phs[slot];
-        };
-        auto load_win = [&](uint32_t tp) {
+        // premixed S_B block of phase slot ps into ring slot `slot` from words x[0..8] (shifted by sh bytes)
+        auto put = [&](uint32_t ps, uint32_t slot, const uint32_t (&x)[9], uint32_t sh) {
+            uint32_t w8[8], v[6];
 #pragma unroll
-            for (int u = 0; u < QL; u++) {
-                const uint32_t q = th + 256u * u;
-                const int32_t off = q < nent ? entry_off(tp, q) : -1;
-                const bool in = off >= 0 && (uint32_t)off + 32u <= lenB;
-                const uint32_t wi = in ? (uint32_t)off >> 2 : 0u;
-#pragma unroll
-                for (int k = 0; k < 9; k++) xs[u][k] = in ? a.SBw[wi + k] : 0u;
+            for (int k = 0; k < 8; k++) w8[k] = csd_alignbyte(x[k + 1], x[k], sh);
+            csd_premix(w8[0], w8[1], w8[2], w8[3], w8[4], w8[5], w8[6], w8[7], v);
+            const uint32_t at = ring_at(ps, slot);
+            L2[at] = make_uint2(v[0], v[1]);
+            L2[at + 1] = make_uint2(v[2], v[3]);
+            L2[at + 2] = make_uint2(v[4], v[5]);
+            if (slot < (uint32_t)CSD_SB) {                          // the mirror behind the ring's end
+                const uint32_t mi = at + 3u * R;
+                L2[mi] = make_uint2(v[0], v[1]);
+                L2[mi + 1] = make_uint2(v[2], v[3]);
+                L2[mi + 2] = make_uint2(v[4], v[5]);
             }
         };
-        load_win(0);
+        // window 0 (positions 0 .. JW - 1), from global memory once
+        for (uint32_t q = th; q < nph * JW; q += 256u) {
+            const uint32_t ps = q / JW, p = q - ps * JW;
+            const int32_t off = 20 * (jlo0 + (int32_t)p) + (int32_t)phs[ps];
+            uint32_t x[9];
+            const int32_t wi = off >= 0 ? off >> 2 : -1;
+#pragma unroll
+            for (int k = 0; k < 9; k++) x[k] = (wi >= 0 && (uint32_t)(wi + k) < a.sbw_words) ? a.SBw[wi + k] : 0u;
+            put(ps, p, x, off >= 0 ? (uint32_t)off & 3u : 0u);
+        }
+        // the SB new positions of super step tp >= 1 are JW + (tp - 1) SB .. JW + tp SB - 1; their S_B words (from byte
+        // 20 (jlo0 + JW + (tp - 1) SB) on) are loaded into registers two super steps ahead and staged in LDS one ahead
+        constexpr int SL = (CSD_SBST + 255) / 256;
+        uint32_t sw[SL];
+        auto load_sb = [&](uint32_t tp) {
+            const int32_t wb = 5 * (jlo0 + (int32_t)JW + (int32_t)((tp - 1) * CSD_SB));
+#pragma unroll
+            for (int u = 0; u < SL; u++) {
+                const int32_t w = wb + (int32_t)(th + 256u * u);
+                sw[u] = (th + 256u * u < (uint32_t)CSD_SBST && w >= 0 && (uint32_t)w < a.sbw_words) ? a.SBw[w] : 0u;
+            }
+        };
+        auto store_sb = [&](uint32_t tp) {
+#pragma unroll
+            for (int u = 0; u < SL; u++)
+                if (th + 256u * u < (uint32_t)CSD_SBST) sbst[tp & 1u][th + 256u * u] = sw[u];
+        };
+        load_sb(1);
+        store_sb(1);
+        load_sb(2);
+        lds_barrier();
+        // ring slots of positions tp SB (the super step's first block at shift 0's window start) and JW + (tp - 1) SB
+        // (its first new position), advanced by SB per super step instead of taken modulo R
+        uint32_t ws = 0, nbs = JW;
         auto prepare = [&](uint32_t tp) {
             const uint32_t bp = tp & 1u;
-            const int32_t jlo = (int32_t)(tp * CSD_SB) + joff;
-            uint2 *pw = L2 + bp * CSD_PWENT * 3;
-            // (a) S_B's premixed blocks at every phase in use, positions jlo .. jlo + JW - 1
+            // (a) the window's SB new positions at every phase in use
+            if (tp >= 1) {
+                store_sb(tp + 1);
+                load_sb(tp + 2);
+                const uint32_t *st = sbst[bp];
+                for (uint32_t q = th; q < nph * CSD_SB; q += 256u) {
+                    const uint32_t ps = q / CSD_SB, u = q - ps * CSD_SB;
+                    const uint32_t lo = 20u * u + phs[ps], li = lo >> 2;
+                    uint32_t x[9];
 #pragma unroll
-            for (int u = 0; u < QL; u++) {
-                const uint32_t q = th + 256u * u;
-                if (q < nent) {
-                    const uint32_t sh = (uint32_t)entry_off(tp, q) & 3u;
-                    uint32_t w8[8], v[6];
-#pragma unroll
-                    for (int k = 0; k < 8; k++) w8[k] = csd_alignbyte(xs[u][k + 1], xs[u][k], sh);
-                    csd_premix(w8[0], w8[1], w8[2], w8[3], w8[4], w8[5], w8[6], w8[7], v);
-                    pw[3 * q] = make_uint2(v[0], v[1]);
-                    pw[3 * q + 1] = make_uint2(v[2], v[3]);
-                    pw[3 * q + 2] = make_uint2(v[4], v[5]);
+                    for (int k = 0; k < 9; k++) x[k] = st[li + k];
+                    const uint32_t sl = nbs + u;
+                    put(ps, sl >= R ? sl - R : sl, x, lo & 3u);
                 }
             }
-            load_win(tp + 1);
             // (b) this row's exception blocks and jumps in blocks K0 .. K0 + SB - 1
             const uint32_t K0 = tp * CSD_SB;
-            const bool act = rflag[r] == 0u && K0 < iters;
+            const bool act = rflag[r] == 0u && K0 < iters && (a.dmode & 3u) != 3u;
             uint32_t ne = 0;
 #pragma unroll
             for (int q = 0; q < CSD_E; q++) ne += (act && bk[q] < K0 + CSD_SB) ? 1u : 0u;
             uint32_t fl = 0;
-            if (ne == (uint32_t)CSD_E && cur + CSD_E < ecnt) fl |= CSD_F_BATCH;   // more than the batch holds
-            // exception slots of the helper wave: exclusive prefix of ne over its 64 lanes
-            uint32_t pre = ne;
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const uint32_t y = (uint32_t)__shfl_up((int)pre, off, 64);
-                if (lane >= (uint32_t)off) pre += y;
+            // more exception blocks in this super step than the batch holds (a run of adjacent differing records):
+            // the rest are counted and read with synchronous loads (rare)
+            const bool ovf = ne == (uint32_t)CSD_E && cur + CSD_E < ecnt;
+            auto kat = [&](uint32_t e) -> uint32_t { return ((const uint32_t *)(ent + 2 * e))[0]; };
+            if (__builtin_expect(__ballot(ovf) != 0, 0)) {
+                if (ovf)
+                    while (cur + ne < ecnt && kat(cur + ne) < K0 + CSD_SB) ne++;
             }
-            const uint32_t sb = pre - ne;
-            if (sb + ne > (uint32_t)CSD_EXW) fl |= CSD_F_SLOTS;
+            // exception slots of the helper wave (only when some lane has exceptions): an LDS counter per wave and buffer
+            const bool anyx = __ballot(ne > 0) != 0;
+            uint32_t sb = 0;
+            if (__builtin_expect(anyx, 0)) {
+                if (lane == 0) xcnt[bp][hw] = 0u;                   // the wave's LDS operations complete in order
+                if (ne) sb = atomicAdd(&xcnt[bp][hw], ne);
+                if (sb + ne > (uint32_t)CSD_EXW) fl |= CSD_F_SLOTS;
+            }
             const uint32_t exb = CSD_EXB + (bp * CSD_HW + hw) * CSD_EXW * 3;   // uint2 index of slot 0
             uint32_t jw[CSD_NJ], nj = 0;
 #pragma unroll
@@ -485,108 +572,177 @@ __global__ void __launch_bounds__(CSD_THREADS) k_cs_delta(DS d, const uint32_t *
                 const int32_t tB = 20 * (int32_t)k - sh;
                 const int32_t j = csd_floordiv20(tB);
                 const uint32_t ph = (uint32_t)(tB - 20 * j);
-                const int32_t jr = j - jlo;
-                if (!((phm >> ph) & 1u) || jr < 0 || jr >= (int32_t)JW) { fl |= CSD_F_WIN; return bp * CSD_PWENT * 3; }
-                const uint32_t slot = (uint32_t)__popc(phm & ((1u << ph) - 1u));
-                return bp * CSD_PWENT * 3 + 3u * (slot * JW + (uint32_t)jr);
+                const int32_t jr = j - (jlo0 + (int32_t)K0);
+                if (!((phm >> ph) & 1u) || jr < 0 || jr >= (int32_t)JW) { fl |= CSD_F_WIN; return 0u; }
+                const uint32_t sl = ws + (uint32_t)jr;
+                return ring_at((uint32_t)__popc(phm & ((1u << ph) - 1u)), sl >= R ? sl - R : sl);
             };
             if (act && !fl) {
                 add_jump(0, (ne && bk[0] == K0) ? exb + 3u * sb : clean(K0, s));
-#pragma unroll
-                for (int q = 0; q < CSD_E; q++) {
-                    if ((uint32_t)q < ne) {
-                        const uint32_t k = bk[q], i = k - K0, slot = exb + 3u * (sb + q);
-                        L2[slot] = bv[q][0];
-                        L2[slot + 1] = bv[q][1];
-                        L2[slot + 2] = bv[q][2];
-                        const bool starts = q == 0 ? i > 0 : bk[q - 1] + 1 != k;
+                if (__builtin_expect(anyx, 0)) {
+                    // entry q of the super step (block k, shift after, values), its predecessor's and successor's blocks
+                    auto place = [&](uint32_t q, uint32_t k, int32_t sa, uint2 v0, uint2 v1, uint2 v2, uint32_t kprev,
+                                     uint32_t knext) {
+                        const uint32_t i = k - K0, slot = exb + 3u * (sb + q);
+                        L2[slot] = v0;
+                        L2[slot + 1] = v1;
+                        L2[slot + 2] = v2;
+                        const bool starts = q == 0 ? i > 0 : kprev + 1 != k;
                         if (starts) add_jump(i, slot);
-                        s = bs[q];
-                        const bool ends = (uint32_t)(q + 1) < ne ? bk[q + 1] != k + 1 : true;
+                        s = sa;
+                        const bool ends = q + 1 < ne ? knext != k + 1 : true;
                         if (ends && i + 1 < (uint32_t)CSD_SB) add_jump(i + 1, clean(k + 1, s));
+                    };
+#pragma unroll
+                    for (int q = 0; q < CSD_E; q++) {
+                        if ((uint32_t)q < ne) {
+                            const uint32_t kn = q + 1 < CSD_E ? bk[q + 1] : (ne > (uint32_t)CSD_E ? kat(cur + CSD_E) : 0u);
+                            place((uint32_t)q, bk[q], bs[q], bv[q][0], bv[q][1], bv[q][2], q ? bk[q - 1] : 0u, kn);
+                        }
                     }
+                    for (uint32_t q = CSD_E; q < ne; q++) {                // the overflow, from global memory
+                        const uint4 x = ent[2 * (cur + q)], y = ent[2 * (cur + q) + 1];
+                        place(q, x.x, (int32_t)x.y, make_uint2(x.z, x.w), make_uint2(y.x, y.y), make_uint2(y.z, y.w),
+                              kat(cur + q - 1), q + 1 < ne ? kat(cur + q + 1) : 0u);
+                    }
+                    if (nj > (uint32_t)CSD_NJ) fl |= CSD_F_JUMPS;
                 }
-                if (nj > (uint32_t)CSD_NJ) fl |= CSD_F_JUMPS;
             }
             if (!act || fl) {                                       // a valid window address, nothing else
 #pragma unroll
-                for (int q = 0; q < CSD_NJ; q++) jw[q] = q == 0 ? bp * CSD_PWENT * 3 + CSD_JB : CSD_NOJ << 16;
+                for (int q = 0; q < CSD_NJ; q++) jw[q] = q == 0 ? CSD_JB : CSD_NOJ << 16;
             }
             if (fl) rflag[r] |= fl;
-            uint32_t um = 0;
+            uint2 *jp = (uint2 *)&jl[bp][r][0];
 #pragma unroll
-            for (int q = 0; q < CSD_NJ; q++) {
-                jl[bp][r][q] = jw[q];
-                const uint32_t ji = jw[q] >> 16;
-                um |= ji < (uint32_t)CSD_SB ? 1u << ji : 0u;
+            for (int q = 0; q < CSD_NJ; q += 2) jp[q / 2] = make_uint2(jw[q], jw[q + 1]);
+            // blocks where some row of the wave jumps: block 0 always, the rest from the (few) rows with exceptions
+            if (lane == 0) uni[bp][hw] = 1u;
+            if (__builtin_expect(anyx, 0)) {
+                uint32_t um = 0;
+#pragma unroll
+                for (int q = 1; q < CSD_NJ; q++) {
+                    const uint32_t ji = jw[q] >> 16;
+                    um |= ji < (uint32_t)CSD_SB ? 1u << ji : 0u;
+                }
+                if (um) atomicOr(&uni[bp][hw], um);
             }
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) um |= (uint32_t)__shfl_xor((int)um, off, 64);
-            if (lane == 0) uni[bp][hw] = um;
             if (ne) {                                               // the next batch, needed one super step on
                 cur += ne;
                 load_batch();
             }
+            ws = ws + CSD_SB >= R ? ws + CSD_SB - R : ws + CSD_SB;
+            if (tp >= 1) nbs = nbs + CSD_SB >= R ? nbs + CSD_SB - R : nbs + CSD_SB;
         };
-        if (T > 0) prepare(0);
+        const bool hidle = (a.dmode & 3u) == 2u;
+        if (hidle) {                                                // diagnostics: every row at window slot 0, no jumps
+#pragma unroll
+            for (int q = 0; q < CSD_NJ; q++) { jl[0][r][q] = q == 0 ? CSD_JB : CSD_NOJ << 16; jl[1][r][q] = jl[0][r][q]; }
+            if (lane == 0) { uni[0][hw] = 1u; uni[1][hw] = 1u; }
+        }
+        if (T > 0 && !hidle) prepare(0);
         lds_barrier();
         for (uint32_t t = 0; t < T; t++) {
-            if (t + 1 < T) prepare(t + 1);
-            lds_barrier();
+            if (t + 1 < T && !hidle) prepare(t + 1);
+            if (!(a.dmode & 8u)) lds_barrier();
         }
+        lds_barrier();                                              // the h lanes' results published
         return;
     }
 
-    // ================================= hashers =================================
+    // ================================= chains =================================
+    // role 0 runs the h lane of its 64 rows, role 1 the coupled g and f lanes: two chain waves per SIMD, so that the
+    // SIMD issues from one while the other waits on its dependencies (a lone wave issues at most every 4 cycles)
     __builtin_amdgcn_s_setprio(2);
     FH fh{0, 0, 0};
     uint32_t it2 = 0;
     const bool ok = cs_prologue<W>(d, id, is_row, row, fh, it2);
     uint32_t Xg = fh.g + ri.b0, Xf = fh.f + ri.c0, Xh = fh.h + ri.a0;
     const uint32_t myit = live ? iters : 0u;
+    lds_barrier();                                                  // window 0 staged
     lds_barrier();                                                  // super step 0 prepared
     for (uint32_t t = 0; t < T; t++) {
         const uint32_t bp = t & 1u, K0 = t * CSD_SB;
         uint32_t ji[CSD_NJ], jt[CSD_NJ];
 #pragma unroll
-        for (int q = 0; q < CSD_NJ; q++) { const uint32_t x = jl[bp][r][q]; ji[q] = x >> 16; jt[q] = (x & 0xFFFFu) - CSD_JB; }
+        for (int q = 0; q < CSD_NJ; q++) { const uint32_t x = jl[bp][r][q]; ji[q] = x >> 16; jt[q] = 8u * ((x & 0xFFFFu) - CSD_JB); }
         const uint32_t u = __builtin_amdgcn_readfirstlane(uni[bp][hw]);
-        uint32_t base = jt[0];                                      // every row jumps at block 0
+        uint32_t base = jt[0];                                      // byte offset in L2; every row jumps at block 0
         auto apply = [&](uint32_t i) {
 #pragma unroll
             for (int q = 1; q < CSD_NJ; q++) base = ji[q] == i ? jt[q] : base;
         };
         const bool full = __all(myit == 0u || K0 + CSD_SB <= myit);
-        uint2 v[3][3];
-        auto fetch = [&](int i) {
-            const uint2 *p = L2 + base + 3 * i;
-            v[i % 3][0] = p[0];
-            v[i % 3][1] = p[1];
-            v[i % 3][2] = p[2];
-        };
-        auto body = [&](auto FULLC) {
+        // CHK: some row of the wave jumps after block 0 in this super step (u > 1). The common case runs a body without
+        // per-block tests: a test whose skip branch is taken on the common path costs an instruction-fetch restart
+        auto run = [&](auto FULLC, auto ROLEC, auto CHKC) {
             constexpr bool FULL = decltype(FULLC)::value;
+            constexpr int RL = decltype(ROLEC)::value;
+            constexpr bool CHK = decltype(CHKC)::value;
+            // reads run CSD_PF blocks ahead of the chain (LDS latency under twelve waves exceeds two blocks of chain)
+            constexpr int PF = CSD_PF;
+            uint2 v[PF + 1][2];
+            auto fetch = [&](int i) {
+                const uint2 *p = (const uint2 *)((const char *)L2 + base + 24 * i);
+                if (RL == 0) {
+                    v[i % (PF + 1)][0] = p[2];                      // {Mh, KH}
+                } else {
+                    v[i % (PF + 1)][0] = p[0];                      // {Mg, D}
+                    v[i % (PF + 1)][1] = p[1];                      // {Mf, PF}
+                }
+            };
             fetch(0);
-            if ((u >> 1) & 1u) apply(1);
-            fetch(1);
+#pragma unroll
+            for (int i = 1; i < PF; i++) {
+                if (CHK && __builtin_expect((u >> i) & 1u, 0)) apply((uint32_t)i);
+                fetch(i);
+            }
 #pragma unroll
             for (int i = 0; i < CSD_SB; i++) {
-                if (i + 2 < CSD_SB) {
-                    if ((u >> (i + 2)) & 1u) apply((uint32_t)(i + 2));
-                    fetch(i + 2);
+                if (i + PF < CSD_SB) {
+                    if (CHK && __builtin_expect((u >> (i + PF)) & 1u, 0)) apply((uint32_t)(i + PF));
+                    fetch(i + PF);
                 }
-                const uint2 g = v[i % 3][0], f = v[i % 3][1], hh = v[i % 3][2];
-                const uint32_t Fg = x5(ror32(Xg ^ g.x, 19)), Ff = x5(ror32(Xf ^ f.x, 19)), Fh = x5(ror32(Xh ^ hh.x, 19));
-                const uint32_t nf = Ff + Fg + f.y;
-                const uint32_t ng = Fg + nf + g.y;
-                const uint32_t nh = Fh + hh.y;
-                if (FULL || K0 + (uint32_t)i < myit) { Xf = nf; Xg = ng; Xh = nh; }
+                if (RL == 0) {
+                    const uint2 hh = v[i % (PF + 1)][0];
+                    if (FULL) csd_h_step(Xh, hh.x, hh.y);
+                    else {
+                        uint32_t n = Xh;
+                        csd_h_step(n, hh.x, hh.y);
+                        Xh = K0 + (uint32_t)i < myit ? n : Xh;
+                    }
+                } else {
+                    const uint2 g = v[i % (PF + 1)][0], f = v[i % (PF + 1)][1];
+                    if (FULL) csd_gf_step(Xg, Xf, g.x, g.y, f.x, f.y);
+                    else {
+                        uint32_t ng = Xg, nf = Xf;
+                        csd_gf_step(ng, nf, g.x, g.y, f.x, f.y);
+                        const bool act = K0 + (uint32_t)i < myit;
+                        Xg = act ? ng : Xg;
+                        Xf = act ? nf : Xf;
+                    }
+                }
             }
         };
-        if (full) body(std::integral_constant<bool, true>{});
-        else body(std::integral_constant<bool, false>{});
-        lds_barrier();
+        if ((a.dmode & 3u) != 1u) {
+            using TT = std::integral_constant<bool, true>;
+            using FF = std::integral_constant<bool, false>;
+            const bool chk = u > 1u;
+            if (role == 0) {
+                if (full && !chk) run(TT{}, std::integral_constant<int, 0>{}, FF{});
+                else if (full) run(TT{}, std::integral_constant<int, 0>{}, TT{});
+                else run(FF{}, std::integral_constant<int, 0>{}, TT{});
+            } else {
+                if (full && !chk) run(TT{}, std::integral_constant<int, 1>{}, FF{});
+                else if (full) run(TT{}, std::integral_constant<int, 1>{}, TT{});
+                else run(FF{}, std::integral_constant<int, 1>{}, TT{});
+            }
+        }
+        if (!(a.dmode & 8u)) lds_barrier();
     }
+    if (role == 0) xh[r] = Xh;
+    lds_barrier();                                                  // the h lanes' results published
+    if (role == 0) return;
     const bool mine = valid && rflag[r] == 0u;
     const uint32_t nmine = (uint32_t)__popcll(__ballot(mine));
     if (lane == 0 && nmine) ctr_add(d, C_X_CS_ROWS, (unsigned long long)nmine);   // rows this launch hashed
@@ -599,7 +755,7 @@ __global__ void __launch_bounds__(CSD_THREADS) k_cs_delta(DS d, const uint32_t *
             if ((fl >> b) & 1u) atomicAdd(a.fb_cnt + 1 + b, 1u);
         return;
     }
-    fh.h = Xh; fh.g = Xg; fh.f = Xf;
+    fh.h = xh[r]; fh.g = Xg; fh.f = Xf;
     const uint32_t hv = ok ? fh.fin() : 0u;
     if (is_row) {
         d.cs[id] = hv;

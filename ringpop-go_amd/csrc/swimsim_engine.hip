@@ -337,7 +337,7 @@ struct swimsim {
     size_t csd_sbw_words = 0;
     uint4 *csd_ent = nullptr;
     CsdRow *csd_rinfo = nullptr;
-    uint32_t csd_ecap = 1024;
+    uint32_t csd_ecap = 3072;
     uint64_t csd_launches = 0, csd_fallback_rows = 0, csd_reasons[CSD_NFLAGS] = {0};
     std::string err;
 
@@ -697,7 +697,7 @@ int csd_alloc(swimsim *h) {
 
 // hash the n listed rows (count on the device) by the reference-row path. Returns 0 when every row is hashed, 1 when
 // the path is unavailable (the caller hashes them), < 0 on a HIP error (h->err set)
-int csd_hash(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t n) {
+int csd_hash(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t n, uint32_t dmode = 0) {
     if (n > h->NL) return 1;
     if (csd_alloc(h)) return 1;
     CsdArgs a{};
@@ -710,6 +710,7 @@ int csd_hash(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t n) 
     a.ecap = h->csd_ecap;
     a.fb_list = h->csd_fb;
     a.fb_cnt = h->csd_fbcnt;
+    a.dmode = dmode;
     {
         Scope sc(h, F_CSD_SCAN);
         hipLaunchKernelGGL(k_csd_ref, dim3((h->N + 256) / 256), dim3(256), 0, h->s, h->d, list, n, h->csd_B, h->csd_Lb);
@@ -1980,12 +1981,15 @@ __global__ void k_iota(uint32_t *list, uint32_t *cnt, uint32_t n) {
 int swimsim_bench_checksum(swimsim_t *h, uint32_t nrows, int32_t mode, int32_t reps, double *ms) {
     if (!h || !ms || nrows == 0 || nrows > h->NL || reps < 1) return SWIMSIM_EINVAL;
 #ifndef SWIMSIM_DIAG
-    if (mode < 0 || mode > 3) return h->fail(SWIMSIM_EINVAL, "checksum mode %d: diagnostics build only", mode);
+    if ((mode < 0 || mode > 3) && !(mode >= 31 && mode <= 46))
+        return h->fail(SWIMSIM_EINVAL, "checksum mode %d: diagnostics build only", mode);
 #endif
-    // mode 3: the reference-row path (swimsim_checksum_delta.hip), its preparation and any fallback launch included
-    if (mode == 3 && (csd_alloc(h) || nrows > h->NL)) return h->fail(SWIMSIM_EINVAL, "reference-row path unavailable");
+    // mode 3: the reference-row path (swimsim_checksum_delta.hip), its preparation and any fallback launch included;
+    // 31..33: its diagnostic splits (garbage checksums: helpers alone, hashers alone, helpers without exceptions)
+    const bool csd = mode == 3 || (mode >= 31 && mode <= 46);
+    if (csd && (csd_alloc(h) || nrows > h->NL)) return h->fail(SWIMSIM_EINVAL, "reference-row path unavailable");
     auto launch = [&]() {
-        if (mode == 3) (void)csd_hash(h, h->list, h->cnt, nrows);
+        if (csd) (void)csd_hash(h, h->list, h->cnt, nrows, mode == 3 ? 0u : (uint32_t)(mode - 30));
         else if (mode <= 2) launch_checksum_kind(h->d, h->list, h->cnt, nrows, mode == 0 ? cs_kind(nrows) : (CsKind)mode, h->s);
 #ifdef SWIMSIM_DIAG
         else launch_checksum_mode(h->d, h->list, h->cnt, nrows, mode, h->s);
