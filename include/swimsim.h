@@ -230,9 +230,10 @@ int swimsim_profile_mark(swimsim_t *h, uint32_t id);
  * variants) only in the diagnostics library tools/libswimsim_diag.so */
 int swimsim_bench_checksum(swimsim_t *h, uint32_t nrows, int32_t mode, int32_t reps, double *ms);
 /* the reference-row checksum path so far (swimsim_checksum_delta.hip; SWIMSIM_CS_DELTA = 0 off, 1 wide launches,
- * 2 every launch of >= 1024 rows): its launches, the rows it left to the production kernels and, per reason (7
+ * 2 every launch of >= 1024 rows): its launches, the rows it left to the production kernels and, per reason (8
  * entries: short string, entry capacity, workgroup window, entry batch, exception slots, jump slots, window miss),
- * how many of those rows had it */
+ * how many of those rows had it; reasons[7]: launches it declined (sampled rows further from the reference row than
+ * SWIMSIM_CS_DELTA_MAXDIFF members on average) */
 int swimsim_checksum_path_stats(swimsim_t *h, uint64_t *delta_launches, uint64_t *fallback_rows, uint64_t *reasons);
 /* diagnostics library only: the 32-bit words of every 20-byte block the checksum kernel hashes for row o (W = 19) */
 int swimsim_debug_cs_stream(swimsim_t *h, uint32_t o, uint32_t *out, size_t cap_words);

@@ -31,10 +31,13 @@
 
 constexpr int CSD_SB = 32;            // blocks per super step
 constexpr int CSD_PF = 4;             // blocks the chain waves' LDS reads run ahead
-constexpr int CSD_ROWS = 256;         // rows per workgroup
-constexpr int CSD_HW = 4;             // row groups of 64: h-chain waves 0..3, g/f-chain waves 4..7, helper waves 8..11
-constexpr int CSD_THREADS = 768;
-constexpr int CSD_RING = 2240;        // premixed S_B blocks in the window ring (phases x (ring + mirror) positions)
+// k_cs_delta's workgroup: G row groups of 64 rows, each served by an h-chain wave, a g/f-chain wave and a helper wave.
+// G = 4 (256 rows, one workgroup per CU). (A 64-row workgroup, G = 1, measured 5.8 / 6.0 ms against 9.4 / 14.9 ms for
+// k_checksum_q16 at 12,288 / 16,384 light rows, but failed parity on the partition workload and is not launched.)
+template <int G> struct CsdGeo {
+    static constexpr int ROWS = 64 * G, THREADS = 192 * G;
+    static constexpr int RING = G == 4 ? 2240 : 1600;   // premixed S_B blocks in the window ring (phases x (ring + mirror))
+};
 // exception slots per helper wave per buffer: differing members are column-correlated (the members whose state is
 // in flux differ in many rows at once), so a super step can hold a run of 3-4 exception blocks in every row
 constexpr int CSD_EXW = 320;
@@ -46,9 +49,7 @@ constexpr int CSD_JWMAX = 160;        // window positions at most (the workgroup
 constexpr int CSD_SBST = 5 * CSD_SB + 16;      // staged S_B words per super step (its SB new positions)
 constexpr uint32_t CSD_C = 0xe6546b64u;
 constexpr uint32_t CSD_MIN_ROWS = 1024; // launches of fewer rows keep the production kernels
-// LDS of k_cs_delta in uint2 units: the window ring, then 2 x 4 exception regions
-constexpr int CSD_EXB = CSD_RING * 3;
-constexpr int CSD_LDS2 = CSD_EXB + 2 * CSD_HW * CSD_EXW * 3;
+
 
 // per listed row: what k_csd_scan found (32 B)
 struct CsdRow {
@@ -117,6 +118,18 @@ __global__ void k_csd_ref(DS d, const uint32_t *list, uint32_t n, uint32_t *B, u
     }
     B[m] = cand;
     Lb[m] = csd_reclen(d, cand);
+}
+
+// the launch's mean distance from B, on CSD_NSAMPLE rows sampled evenly from the list: differing members counted
+// into *out (one workgroup per sampled row). Decides whether the reference-row path pays for this launch.
+constexpr uint32_t CSD_NSAMPLE = 64;
+__global__ void __launch_bounds__(256) k_csd_sample(DS d, const uint32_t *list, uint32_t n, const uint32_t *B, uint32_t *out) {
+    const uint32_t id = list[(uint32_t)(((uint64_t)blockIdx.x * n) / CSD_NSAMPLE)];
+    const uint32_t *row = csd_row(d, id);
+    uint32_t c = 0;
+    for (uint32_t m = threadIdx.x; m < d.N; m += 256u) c += csd_same(row[m], B[m]) ? 0u : 1u;
+    for (int off = 32; off > 0; off >>= 1) c += (uint32_t)__shfl_xor((int)c, off, 64);
+    if ((threadIdx.x & 63u) == 0 && c) atomicAdd(out, c);
 }
 
 template <int W>
@@ -363,8 +376,13 @@ __device__ __forceinline__ void csd_h_step(uint32_t &Xh, uint32_t mh, uint32_t k
                  : "v"(mh), "v"(kh));
 }
 
-template <int W>
-__global__ void __launch_bounds__(CSD_THREADS) k_cs_delta(DS d, const uint32_t *list, const uint32_t *count, CsdArgs a) {
+template <int W, int G>
+__global__ void __launch_bounds__(CsdGeo<G>::THREADS) k_cs_delta(DS d, const uint32_t *list, const uint32_t *count, CsdArgs a) {
+    constexpr int CSD_ROWS = CsdGeo<G>::ROWS, CSD_HW = G, CSD_RING = CsdGeo<G>::RING;
+    constexpr uint32_t HT = 64u * G;                     // helper threads
+    // LDS in uint2 units: the window ring, then 2 x G exception regions
+    constexpr int CSD_EXB = CSD_RING * 3;
+    constexpr int CSD_LDS2 = CSD_EXB + 2 * CSD_HW * CSD_EXW * 3;
     __shared__ uint2 L2[CSD_LDS2];                       // window ring, then exception regions (24-B entries)
     __shared__ __attribute__((aligned(8))) uint32_t jl[2][CSD_ROWS][CSD_NJ];   // per row: jump words (CSD_JB);
                                                                                 // block CSD_NOJ: unused
@@ -393,10 +411,10 @@ __global__ void __launch_bounds__(CSD_THREADS) k_cs_delta(DS d, const uint32_t *
     if (lane == 0) slot = atomicAdd(&simd_n[simd], 1u);
     slot = __builtin_amdgcn_readfirstlane(slot);
     __syncthreads();
-    const bool even = simd_n[0] == 3u && simd_n[1] == 3u && simd_n[2] == 3u && simd_n[3] == 3u;
-    const uint32_t role = even ? slot : wave >> 2;                  // 0: h chains, 1: g/f chains, 2: helpers
-    const uint32_t hw = even ? simd : wave & 3u;
-    if (!even && threadIdx.x == 0) ctr_add(d, C_NALL, 1ull);       // diagnostics: uneven placements
+    const bool even = G == 4 && simd_n[0] == 3u && simd_n[1] == 3u && simd_n[2] == 3u && simd_n[3] == 3u;
+    const uint32_t role = even ? slot : wave / G;                   // 0: h chains, 1: g/f chains, 2: helpers
+    const uint32_t hw = even ? simd : wave % G;
+    if (G == 4 && !even && threadIdx.x == 0) ctr_add(d, C_NALL, 1ull);   // diagnostics: uneven placements
     const uint32_t r = hw * 64 + lane;                              // this lane's row
     const uint32_t gi = g0 + r;
     const bool valid = gi < cnt;
@@ -484,7 +502,7 @@ __global__ void __launch_bounds__(CSD_THREADS) k_cs_delta(DS d, const uint32_t *
             }
         };
         // window 0 (positions 0 .. JW - 1), from global memory once
-        for (uint32_t q = th; q < nph * JW; q += 256u) {
+        for (uint32_t q = th; q < nph * JW; q += HT) {
             const uint32_t ps = q / JW, p = q - ps * JW;
             const int32_t off = 20 * (jlo0 + (int32_t)p) + (int32_t)phs[ps];
             uint32_t x[9];
@@ -495,20 +513,20 @@ __global__ void __launch_bounds__(CSD_THREADS) k_cs_delta(DS d, const uint32_t *
         }
         // the SB new positions of super step tp >= 1 are JW + (tp - 1) SB .. JW + tp SB - 1; their S_B words (from byte
         // 20 (jlo0 + JW + (tp - 1) SB) on) are loaded into registers two super steps ahead and staged in LDS one ahead
-        constexpr int SL = (CSD_SBST + 255) / 256;
+        constexpr int SL = (CSD_SBST + HT - 1) / HT;
         uint32_t sw[SL];
         auto load_sb = [&](uint32_t tp) {
             const int32_t wb = 5 * (jlo0 + (int32_t)JW + (int32_t)((tp - 1) * CSD_SB));
 #pragma unroll
             for (int u = 0; u < SL; u++) {
-                const int32_t w = wb + (int32_t)(th + 256u * u);
-                sw[u] = (th + 256u * u < (uint32_t)CSD_SBST && w >= 0 && (uint32_t)w < a.sbw_words) ? a.SBw[w] : 0u;
+                const int32_t w = wb + (int32_t)(th + HT * u);
+                sw[u] = (th + HT * u < (uint32_t)CSD_SBST && w >= 0 && (uint32_t)w < a.sbw_words) ? a.SBw[w] : 0u;
             }
         };
         auto store_sb = [&](uint32_t tp) {
 #pragma unroll
             for (int u = 0; u < SL; u++)
-                if (th + 256u * u < (uint32_t)CSD_SBST) sbst[tp & 1u][th + 256u * u] = sw[u];
+                if (th + HT * u < (uint32_t)CSD_SBST) sbst[tp & 1u][th + HT * u] = sw[u];
         };
         load_sb(1);
         store_sb(1);
@@ -524,7 +542,7 @@ __global__ void __launch_bounds__(CSD_THREADS) k_cs_delta(DS d, const uint32_t *
                 store_sb(tp + 1);
                 load_sb(tp + 2);
                 const uint32_t *st = sbst[bp];
-                for (uint32_t q = th; q < nph * CSD_SB; q += 256u) {
+                for (uint32_t q = th; q < nph * CSD_SB; q += HT) {
                     const uint32_t ps = q / CSD_SB, u = q - ps * CSD_SB;
                     const uint32_t lo = 20u * u + phs[ps], li = lo >> 2;
                     uint32_t x[9];
@@ -773,7 +791,7 @@ void launch_csd_w(const DS &d, const uint32_t *list, uint32_t n, const uint32_t 
     } else if (part == 1) {
         hipLaunchKernelGGL((k_csd_scan<W>), dim3((n + 3) / 4), dim3(256), 0, s, d, list, n, a);
     } else {
-        hipLaunchKernelGGL((k_cs_delta<W>), dim3((n + CSD_ROWS - 1) / CSD_ROWS), dim3(CSD_THREADS), 0, s, d, list, count, a);
+        hipLaunchKernelGGL((k_cs_delta<W, 4>), dim3((n + 255) / 256), dim3(CsdGeo<4>::THREADS), 0, s, d, list, count, a);
     }
 }
 

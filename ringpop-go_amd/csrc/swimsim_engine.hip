@@ -339,6 +339,10 @@ struct swimsim {
     CsdRow *csd_rinfo = nullptr;
     uint32_t csd_ecap = 3072;
     uint64_t csd_launches = 0, csd_fallback_rows = 0, csd_reasons[CSD_NFLAGS] = {0};
+    uint32_t csd_maxdiff = 12;                    // SWIMSIM_CS_DELTA_MAXDIFF: mean differing members per sampled row above
+                                                  // which a launch keeps the production kernels (0: always the path)
+    uint64_t csd_declined = 0;
+    double csd_last_mean = 0;
     std::string err;
 
     int fail(int code, const char *fmt, ...) {
@@ -714,6 +718,16 @@ int csd_hash(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t n, 
     {
         Scope sc(h, F_CSD_SCAN);
         hipLaunchKernelGGL(k_csd_ref, dim3((h->N + 256) / 256), dim3(256), 0, h->s, h->d, list, n, h->csd_B, h->csd_Lb);
+        if (h->csd_maxdiff && !dmode) {
+            // rows far from the majority make many exception blocks, and the path loses to the production kernels
+            // (DESIGN.md §4): decide on a sample
+            HIPCHK(h, hipMemsetAsync(h->csd_fbcnt, 0, 4, h->s));
+            hipLaunchKernelGGL(k_csd_sample, dim3(CSD_NSAMPLE), dim3(256), 0, h->s, h->d, list, n, h->csd_B, h->csd_fbcnt);
+            HIPCHK(h, hipMemcpyAsync(h->hinfo + 16, h->csd_fbcnt, 4, hipMemcpyDeviceToHost, h->s));
+            HIPCHK(h, hipStreamSynchronize(h->s));
+            h->csd_last_mean = (double)h->hinfo[16] / CSD_NSAMPLE;
+            if (h->csd_last_mean > (double)h->csd_maxdiff) { h->csd_declined++; return 1; }
+        }
         size_t bytes = h->cub_bytes;
         HIPCHK(h, hipcub::DeviceScan::ExclusiveSum(h->cub_tmp, bytes, h->csd_Lb, h->csd_OB, (int)h->N + 1, h->s));
         HIPCHK(h, hipMemsetAsync(h->csd_SBw, 0, h->csd_sbw_words * 4, h->s));
@@ -1446,6 +1460,7 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
     if (const char *v = getenv("SWIMSIM_CS_ASYNC")) h->cs_async = atoi(v) != 0;
     if (const char *v = getenv("SWIMSIM_CS_NARROW_ROWS")) g_cs_narrow_rows = (uint32_t)strtoul(v, nullptr, 10);
     if (const char *v = getenv("SWIMSIM_CS_DELTA")) h->csd_mode = atoi(v);
+    if (const char *v = getenv("SWIMSIM_CS_DELTA_MAXDIFF")) h->csd_maxdiff = (uint32_t)strtoul(v, nullptr, 10);
     DS &d = h->d;
     d.N = h->N; d.NP = h->NP; d.NL = h->NL; d.lo = h->lo;
     d.NB = h->NP / 64;
@@ -1989,7 +2004,12 @@ int swimsim_bench_checksum(swimsim_t *h, uint32_t nrows, int32_t mode, int32_t r
     const bool csd = mode == 3 || (mode >= 31 && mode <= 46);
     if (csd && (csd_alloc(h) || nrows > h->NL)) return h->fail(SWIMSIM_EINVAL, "reference-row path unavailable");
     auto launch = [&]() {
-        if (csd) (void)csd_hash(h, h->list, h->cnt, nrows, mode == 3 ? 0u : (uint32_t)(mode - 30));
+        if (csd) {                                                 // the path itself, never declined here
+            const uint32_t keep = h->csd_maxdiff;
+            h->csd_maxdiff = 0;
+            (void)csd_hash(h, h->list, h->cnt, nrows, mode == 3 ? 0u : (uint32_t)(mode - 30));
+            h->csd_maxdiff = keep;
+        }
         else if (mode <= 2) launch_checksum_kind(h->d, h->list, h->cnt, nrows, mode == 0 ? cs_kind(nrows) : (CsKind)mode, h->s);
 #ifdef SWIMSIM_DIAG
         else launch_checksum_mode(h->d, h->list, h->cnt, nrows, mode, h->s);
@@ -2495,8 +2515,10 @@ int swimsim_checksum_path_stats(swimsim_t *h, uint64_t *delta_launches, uint64_t
     if (!h) return SWIMSIM_EINVAL;
     if (delta_launches) *delta_launches = h->csd_launches;
     if (fallback_rows) *fallback_rows = h->csd_fallback_rows;
-    if (reasons)
+    if (reasons) {
         for (uint32_t b = 0; b < CSD_NFLAGS; b++) reasons[b] = h->csd_reasons[b];
+        reasons[CSD_NFLAGS] = h->csd_declined;
+    }
     return SWIMSIM_OK;
 }
 

@@ -530,7 +530,8 @@ class Cluster:
         return {"shards": g.value, "rank": r.value, "lo": lo.value, "hi": hi.value, "exchanged_bytes": xb.value,
                 "exchanges": xc.value}
 
-    CSD_REASONS = ("short", "entry_cap", "window_plan", "entry_batch", "exception_slots", "jump_slots", "window_miss")
+    CSD_REASONS = ("short", "entry_cap", "window_plan", "entry_batch", "exception_slots", "jump_slots", "window_miss",
+                   "declined_launches")
 
     def checksum_path_stats(self):
         dl, fb = C.c_uint64(), C.c_uint64()

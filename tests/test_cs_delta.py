@@ -20,10 +20,11 @@ pytestmark = pytest.mark.gpu
 
 
 def forced(n, **kw):
-    old = {k: os.environ.get(k) for k in ("SWIMSIM_CS_DELTA", "SWIMSIM_CS_ASYNC")}
+    old = {k: os.environ.get(k) for k in ("SWIMSIM_CS_DELTA", "SWIMSIM_CS_ASYNC", "SWIMSIM_CS_DELTA_MAXDIFF")}
     try:
         os.environ["SWIMSIM_CS_DELTA"] = "2"
         os.environ["SWIMSIM_CS_ASYNC"] = "0"
+        os.environ["SWIMSIM_CS_DELTA_MAXDIFF"] = str(kw.pop("maxdiff", 0))
         return swimsim.Cluster(n, **kw)
     finally:
         for k, v in old.items():
@@ -92,3 +93,19 @@ def test_incarnation_bursts_n2048_every_round():
     st = eng.checksum_path_stats()
     print("bursts n2048", st)
     assert st["delta_launches"] >= 3, st
+
+
+def test_predictor_declines_far_rows_and_stays_exact():
+    """with the default threshold the path declines the partition's launches (rows half a membership apart) and the
+    production kernels hash them; the cascade's early launches (rows a few members apart) take the path"""
+    wl = W.config4(n=2048, rounds=70)
+    eng = forced(wl.n, maxdiff=12)
+    ora = OracleSim(wl.n)
+    for r in range(70):
+        ev = wl.events_for(r)
+        eng.step(1, ev)
+        ora.step(ev)
+        assert (eng.checksums() == ora.checksums()).all(), f"round {r}"
+    st = eng.checksum_path_stats()
+    print("partition predictor", st)
+    assert st["reasons"]["declined_launches"] >= 1, st
