@@ -36,14 +36,31 @@ def cores():
     return max(1, min(n, int(cap))) if cap and cap.isdigit() else max(1, n)
 
 
+def heartbeat(tag):
+    """a line on stderr every 30 s while the oracle runs (a 65,536-member round can take minutes: the GPU box
+    takes a silent command for a hung one); ctypes releases the GIL, so the thread runs during a call"""
+    import threading
+    t0 = time.time()
+
+    def beat():
+        while True:
+            time.sleep(30)
+            print(f"[{tag}] {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
+    threading.Thread(target=beat, daemon=True).start()
+
+
 def run_variant(n, warmup, steps, budget, reference_cost):
     from oracle_ffi import OracleSim
     from swimsim import workloads as W
+
+    tag = f"{'ref' if reference_cost else 'opt'} n={n} thr={os.environ.get('OMP_NUM_THREADS', '1')}"
+    heartbeat(tag)
 
     wl = W.config3(n=n, rounds=warmup + steps)
     sim = OracleSim(n, faithful_checksum=reference_cost, reference_cost=reference_cost)
     for r in range(warmup):
         sim.step(wl.events_for(r))
+        print(f"[{tag}] warmup round {r} done", file=sys.stderr, flush=True)
     live = n - sum(1 for e in wl.events if e[1] == W.EV_KILL and e[0] < warmup)
     done, mr, spent, per_round = 0, 0, 0.0, []
     for r in range(warmup, warmup + steps):
@@ -56,20 +73,32 @@ def run_variant(n, warmup, steps, budget, reference_cost):
         per_round.append(round(dt, 3))
         mr += live
         done += 1
+        res = {"value": round(mr / spent, 1), "rounds": [warmup, warmup + done - 1], "seconds": round(spent, 2),
+               "round_s": per_round}
+        print(json.dumps(res), flush=True)                # partial result: the parent keeps the last on timeout
+        print(f"[{tag}] round {r}: {dt:.2f} s", file=sys.stderr, flush=True)
         if spent > budget:
             break
-    return {"value": round(mr / spent, 1), "rounds": [warmup, warmup + done - 1], "seconds": round(spent, 2),
-            "round_s": per_round}
+    return res
 
 
-def run_threads(nthr, fn):
-    """run fn() in a child process with OMP_NUM_THREADS = nthr (the OpenMP runtime reads it once, at load)"""
+def run_threads(nthr, fn, timeout=1800):
+    """run fn() in a child process with OMP_NUM_THREADS = nthr (the OpenMP runtime reads it once, at load); the
+    child's stderr (progress) passes through; past the timeout the last partial result is kept, marked"""
     import subprocess
+    if fn is None:
+        return {"skipped": True}
     env = dict(os.environ, OMP_NUM_THREADS=str(nthr))
-    out = subprocess.run([sys.executable, os.path.abspath(__file__), "--variant", fn], capture_output=True, text=True,
-                         env=env, timeout=1800)
+    try:
+        out = subprocess.run([sys.executable, os.path.abspath(__file__), "--variant", fn], stdout=subprocess.PIPE,
+                             text=True, env=env, timeout=timeout)
+    except subprocess.TimeoutExpired as e:
+        lines = (e.stdout.decode() if isinstance(e.stdout, bytes) else e.stdout or "").strip().splitlines()
+        if not lines:
+            return {"error": f"timeout after {timeout} s before the first timed round"}
+        return {**json.loads(lines[-1]), "note": f"variant stopped at its {timeout}-s limit inside the next round"}
     if out.returncode != 0:
-        return {"error": out.stderr[-400:]}
+        return {"error": f"exit {out.returncode}"}
     return json.loads(out.stdout.strip().splitlines()[-1])
 
 
@@ -78,6 +107,8 @@ def main():
     ap.add_argument("--budget", type=float, default=60.0, help="seconds of CPU-side timing over all four runs")
     ap.add_argument("--window", default="65536:5:20", help="GPU line's members:warmup:steps")
     ap.add_argument("--members", type=int, default=16384)
+    ap.add_argument("--variants", default="ref,opt,ref1,opt1", help="which of the four runs (ref1/opt1: one thread)")
+    ap.add_argument("--variant-timeout", type=float, default=1800.0)
     ap.add_argument("--variant", default=None, help=argparse.SUPPRESS)   # child: "ref|opt:n:warmup:steps:budget"
     args = ap.parse_args()
     os.environ["ORACLE_LIB"] = os.path.join(REPO, "oracle", "build", "libswim_oracle_omp.so")
@@ -92,10 +123,13 @@ def main():
     n = min(args.members, gpu_n)
     b = args.budget
     spec = lambda kind, share: f"{kind}:{n}:{warmup}:{steps}:{share * b}"
-    ref = run_threads(nthr, spec("ref", 0.45))
-    opt = run_threads(nthr, spec("opt", 0.15))
-    ref1 = run_threads(1, spec("ref", 0.25))
-    opt1 = run_threads(1, spec("opt", 0.15))
+    want = set(args.variants.split(","))
+    pick = lambda name, kind, share: spec(kind, share) if name in want else None
+    vt = args.variant_timeout
+    ref = run_threads(nthr, pick("ref", "ref", 0.45), vt)
+    opt = run_threads(nthr, pick("opt", "opt", 0.15), vt)
+    ref1 = run_threads(1, pick("ref1", "ref", 0.25), vt)
+    opt1 = run_threads(1, pick("opt1", "opt", 0.15), vt)
     host = "unknown"
     try:
         with open("/proc/cpuinfo") as f:
