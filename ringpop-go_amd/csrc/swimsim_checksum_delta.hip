@@ -72,10 +72,18 @@ struct CsdArgs {
     CsdRow *rinfo;            // [rows]
     uint32_t ecap;
     uint32_t *fb_list, *fb_cnt; // rows left to the production kernels; fb_cnt[1 + b]: rows with flag bit b
-    uint32_t dmode;           // diagnostics (swimsim_bench_checksum modes 31..46 = dmode + 30, garbage checksums): 1 helpers
-                              // alone, 2 chains alone, 3 helpers without the exception work; bit 8: no barrier between
-                              // super steps; 0 in production
+    uint32_t dmode;           // diagnostics library only (swimsim_bench_checksum modes 31..46 = dmode + 30, garbage
+                              // checksums): 1 helpers alone, 2 chains alone, 3 helpers without the exception work; bit 8:
+                              // no barrier between super steps. Ignored by the product library (CSD_DMODE)
 };
+
+// the diagnostic split modes exist only in the diagnostics library (tools/libswimsim_diag.so); in the product
+// library the mode is the constant 0 and its branches compile away
+#ifdef SWIMSIM_DIAG
+#define CSD_DMODE(a) ((a).dmode)
+#else
+#define CSD_DMODE(a) 0u
+#endif
 
 __device__ __forceinline__ const uint32_t *csd_row(const DS &d, uint32_t id) {
     return id < d.NL ? d.mw + (size_t)id * d.NP : d.dense + (size_t)(id - d.NL) * d.NP;
@@ -554,7 +562,7 @@ __global__ void __launch_bounds__(CsdGeo<G>::THREADS) k_cs_delta(DS d, const uin
             }
             // (b) this row's exception blocks and jumps in blocks K0 .. K0 + SB - 1
             const uint32_t K0 = tp * CSD_SB;
-            const bool act = rflag[r] == 0u && K0 < iters && (a.dmode & 3u) != 3u;
+            const bool act = rflag[r] == 0u && K0 < iters && (CSD_DMODE(a) & 3u) != 3u;
             uint32_t ne = 0;
 #pragma unroll
             for (int q = 0; q < CSD_E; q++) ne += (act && bk[q] < K0 + CSD_SB) ? 1u : 0u;
@@ -652,7 +660,7 @@ __global__ void __launch_bounds__(CsdGeo<G>::THREADS) k_cs_delta(DS d, const uin
             ws = ws + CSD_SB >= R ? ws + CSD_SB - R : ws + CSD_SB;
             if (tp >= 1) nbs = nbs + CSD_SB >= R ? nbs + CSD_SB - R : nbs + CSD_SB;
         };
-        const bool hidle = (a.dmode & 3u) == 2u;
+        const bool hidle = (CSD_DMODE(a) & 3u) == 2u;
         if (hidle) {                                                // diagnostics: every row at window slot 0, no jumps
 #pragma unroll
             for (int q = 0; q < CSD_NJ; q++) { jl[0][r][q] = q == 0 ? CSD_JB : CSD_NOJ << 16; jl[1][r][q] = jl[0][r][q]; }
@@ -662,7 +670,7 @@ __global__ void __launch_bounds__(CsdGeo<G>::THREADS) k_cs_delta(DS d, const uin
         lds_barrier();
         for (uint32_t t = 0; t < T; t++) {
             if (t + 1 < T && !hidle) prepare(t + 1);
-            if (!(a.dmode & 8u)) lds_barrier();
+            if (!(CSD_DMODE(a) & 8u)) lds_barrier();
         }
         lds_barrier();                                              // the h lanes' results published
         return;
@@ -742,7 +750,7 @@ __global__ void __launch_bounds__(CsdGeo<G>::THREADS) k_cs_delta(DS d, const uin
                 }
             }
         };
-        if ((a.dmode & 3u) != 1u) {
+        if ((CSD_DMODE(a) & 3u) != 1u) {
             using TT = std::integral_constant<bool, true>;
             using FF = std::integral_constant<bool, false>;
             const bool chk = u > 1u;
@@ -756,7 +764,7 @@ __global__ void __launch_bounds__(CsdGeo<G>::THREADS) k_cs_delta(DS d, const uin
                 else run(FF{}, std::integral_constant<int, 1>{}, TT{});
             }
         }
-        if (!(a.dmode & 8u)) lds_barrier();
+        if (!(CSD_DMODE(a) & 8u)) lds_barrier();
     }
     if (role == 0) xh[r] = Xh;
     lds_barrier();                                                  // the h lanes' results published

@@ -1996,11 +1996,12 @@ __global__ void k_iota(uint32_t *list, uint32_t *cnt, uint32_t n) {
 int swimsim_bench_checksum(swimsim_t *h, uint32_t nrows, int32_t mode, int32_t reps, double *ms) {
     if (!h || !ms || nrows == 0 || nrows > h->NL || reps < 1) return SWIMSIM_EINVAL;
 #ifndef SWIMSIM_DIAG
-    if ((mode < 0 || mode > 3) && !(mode >= 31 && mode <= 46))
+    if (mode < 0 || mode > 3)
         return h->fail(SWIMSIM_EINVAL, "checksum mode %d: diagnostics build only", mode);
 #endif
     // mode 3: the reference-row path (swimsim_checksum_delta.hip), its preparation and any fallback launch included;
-    // 31..33: its diagnostic splits (garbage checksums: helpers alone, hashers alone, helpers without exceptions)
+    // 31..46 (diagnostics library): its split modes (garbage checksums: helpers alone, hashers alone, helpers without
+    // exceptions; + 8: no barrier between super steps)
     const bool csd = mode == 3 || (mode >= 31 && mode <= 46);
     if (csd && (csd_alloc(h) || nrows > h->NL)) return h->fail(SWIMSIM_EINVAL, "reference-row path unavailable");
     auto launch = [&]() {
