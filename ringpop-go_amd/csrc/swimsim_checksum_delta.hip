@@ -41,7 +41,11 @@ template <int G> struct CsdGeo {
 // exception slots per helper wave per buffer: differing members are column-correlated (the members whose state is
 // in flux differ in many rows at once), so a super step can hold a run of 3-4 exception blocks in every row
 constexpr int CSD_EXW = 320;
-constexpr int CSD_NJ = 6;             // jumps per row per super step (block 0, then a start and an end per run)
+#ifndef CSD_NJ_DEF                    // (a build-time define for experiments with other slot counts; even)
+#define CSD_NJ_DEF 6
+#endif
+constexpr int CSD_NJ = CSD_NJ_DEF;    // jumps per row per super step (block 0, then a start and an end per run)
+static_assert(CSD_NJ % 2 == 0, "jump words are stored in pairs");
 constexpr int CSD_E = 8;              // exception entries a helper lane holds in registers
 constexpr uint32_t CSD_NOJ = 0xFFFFu; // unused jump slot
 constexpr uint32_t CSD_JB = 128;      // jump word: block i << 16 | (target - 3 i + CSD_JB), target in uint2 units
