@@ -25,7 +25,7 @@ The JSON line carries:
                  them; profiles/r03_pmc_summary.json; null when that summary was taken on another workload).
                  `kernels` gives the same figures for the other kernels (the other checksum kernel, k_recv,
                  k_resp, k_issue); `merge_kernel` repeats k_recv, the north-star merge kernel.
-  cpu_baseline : the C oracle on the GPU box's host cores (rank 0, N=1 only), bounded sample.
+  cpu_baseline : the C oracle on the GPU box's host cores (rank 0, N=1 only) at the GPU line's N, bounded sample.
 """
 import argparse
 import json
@@ -141,6 +141,16 @@ def roofline_entry(fam, kt, units, n_members):
     return out
 
 
+def dom_bound(fam, entry):
+    """The bound of the dominant kernel. The FarmHash checksum kernels are bounded by integer VALU issue (a row's chain is
+    sequential and every block costs tens of VALU instructions per 20 string bytes), not by HBM: for them
+    the line keeps the §8(d) HBM figures (achieved / peak / frac) and names "valu" as the bound, whose fraction is
+    entry["valu"]["frac"]. The merge and issue kernels are HBM-gather kernels."""
+    if fam.startswith("checksum"):
+        return "valu"
+    return "hbm"
+
+
 def add_pmc(entry, fam, workload):
     if not entry:
         return entry
@@ -212,11 +222,14 @@ def live_member_rounds(wl, first, last):
     return total
 
 
-def cpu_baseline(gpu_window, seconds_budget=60.0):
-    """The CPU oracle on a bounded sample of the same protocol (tools/cpu_baseline.py does the timing in a
-    child process so that OpenMP threads do not share this process with the HIP runtime)."""
+def cpu_baseline(gpu_window, members, seconds_budget=40.0):
+    """The CPU oracle on a bounded sample of the same protocol at the GPU line's own N (tools/cpu_baseline.py does the
+    timing in a child process so that OpenMP threads do not share this process with the HIP runtime): the reference
+    cost model and the optimized port, each on the box's cores, over the first rounds of the GPU window that fit the
+    budget (at 65,536 members a cascade round of the reference cost model takes tens of seconds)."""
     out = subprocess.run([sys.executable, os.path.join(REPO, "tools", "cpu_baseline.py"), "--budget",
-                          str(seconds_budget), "--window", gpu_window], capture_output=True, text=True, timeout=1200)
+                          str(seconds_budget), "--window", gpu_window, "--members", str(members), "--variants", "ref,opt"],
+                         capture_output=True, text=True, timeout=1200)
     if out.returncode != 0:
         return {"error": out.stderr[-400:]}
     return json.loads(out.stdout.strip().splitlines()[-1])
@@ -397,17 +410,23 @@ def main():
                        "members": n, "rounds_timed": args.steps, "live_member_rounds": live_mr,
                        "parallelism": (f"observer-row shards x{ws} over " + ("host transport (diagnostic)" if args.host_transport
                                                                               else "RCCL")) if ws > 1 else "1 GPU"},
-            "roofline": {"bound": "hbm", **dom, "dominant_family": dominant,
+            "roofline": {"bound": dom_bound(dominant, dom), **dom, "dominant_family": dominant,
                          "kernels": {f: e for f, e in entries.items() if e and f != dominant},
                          "merge_kernel": entries.get("recv_merge")},
             "kernel_ms": {k: round(v["avg_ms"] * v["launches"], 3) for k, v in kt.items()},
             "counters": counters,
         }
+        if line["roofline"]["bound"] == "valu":
+            line["roofline"]["bound_frac"] = (dom.get("valu") or {}).get("frac")
+            line["roofline"]["frac_basis"] = "achieved / peak / frac: HBM bytes of SURVEY.md §8(d); the bound is VALU issue (bound_frac)"
         if ws > 1:
             line["exchange"] = {"bytes_rank0": shard["exchanged_bytes"], "exchanges_rank0": shard["exchanges"],
-                                "bytes_per_round_rank0": round(shard["exchanged_bytes"] / max(1, total_rounds), 1)}
+                                "bytes_per_round_rank0": round(shard["exchanged_bytes"] / max(1, total_rounds), 1),
+                                "exchanges_per_round_rank0": round(shard["exchanges"] / max(1, total_rounds), 2),
+                                "host_syncs_per_exchange_rank0": round(shard.get("exchange_host_syncs", 0) /
+                                                                       max(1, shard["exchanges"]), 2)}
         if ws == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(f"{n}:{args.warmup}:{args.steps}")
+            line["cpu_baseline"] = cpu_baseline(f"{n}:{args.warmup}:{args.steps}", n)
         if ws == 1 and not args.no_ring:
             line["hashring"] = ring_bench(n)
         sys.stdout.flush()

@@ -62,7 +62,20 @@ typedef struct swimsim_config {
     uint32_t max_rounds;               /* incarnation table capacity (default 65536 rounds) */
     uint64_t message_pool_bytes;       /* change-record pool; 0 = automatic */
     uint32_t observer_begin, observer_end; /* shard of observer rows held by this handle; 0,0 = all */
+    const struct swimsim_tuning *tuning;   /* NULL: the production engine; else variants for tests (below) */
 } swimsim_config;
+
+/* Engine variants the tests and diagnostics select per handle (results are identical in every variant; only where
+ * and how the work runs changes). Every field: -1 = the production default. */
+typedef struct swimsim_tuning {
+    int32_t hot_slots;        /* hot-column slots per row; 0 = no hot columns; default 2,048 */
+    int32_t dense_slots;      /* dense snapshot slots (at least 64); default: 2 per row + 64, bounded by a third of
+                                 the free HBM; small pools exercise the lazy-snapshot fallbacks */
+    int32_t cs_async;         /* 0: every phase-C checksum on the main stream; default 1 (side stream) */
+    int32_t cs_async_rows;    /* phase-C launches of at most this many rows go to the side stream; default 12,288 */
+    int32_t cs_narrow_rows;   /* launches of at most this many rows use the narrow checksum kernel; 0 = the wide
+                                 kernel only; default 8,192 */
+} swimsim_tuning;
 
 /* Events applied in phase E of a round (docs/ROUND_SEMANTICS.md §4). */
 enum {
@@ -255,6 +268,10 @@ int swimsim_comm_unique_id(uint8_t *out, size_t cap);   /* returns the id length
 int swimsim_comm_attach(swimsim_t *h, uint32_t nranks, uint32_t rank, const uint8_t *id, size_t len);
 int swimsim_shard_info(swimsim_t *h, uint32_t *nshards, uint32_t *rank, uint32_t *lo, uint32_t *hi,
                        uint64_t *exchanged_bytes, uint64_t *exchanges);
+/* Host synchronisations the cross-shard exchanges of this handle took so far (measurement): one per exchange on the
+ * RCCL transport (segment sizes travel on the device behind the pack-size kernel), three on the local and host
+ * transports. */
+int swimsim_exchange_syncs(swimsim_t *h, uint64_t *syncs);
 /* one process per shard with a caller-supplied host transport (any process group: a test harness
  * over gloo, an MPI job, ...). The library stages the packed parcels through host memory and calls:
  *   alltoall_u64: k values to every shard; recv[s*k + i] = shard s's send[rank*k + i]

@@ -142,9 +142,9 @@ constexpr int cs_no(int W, int maxtail) { return (3 + W + maxtail + 3) / 4; }
 
 #include "swimsim_checksum3.hip"
 #include "swimsim_checksum4.hip"
-#include "swimsim_checksum_delta.hip"
-#ifdef SWIMSIM_DIAG                            // tools/diag (diagnostics library only): the 3-wave and
-#include "swimsim_checksum5.hip"               // fast-path experiments and every superseded kernel
+#ifdef SWIMSIM_DIAG                            // tools/diag (diagnostics library only): the reference-row path
+#include "swimsim_checksum_delta.hip"          // (off by default in round 3, not a win over the cascade), the 3-wave
+#include "swimsim_checksum5.hip"               // and fast-path experiments and every superseded kernel
 #include "swimsim_checksum6.hip"
 #include "swimsim_checksum_diag.hip"
 #endif
@@ -156,12 +156,13 @@ constexpr uint32_t CS_NARROW_ROWS = 8192;
 // (swimsim_engine.hip checksum_dirty); the kernel is still chosen by row count
 constexpr uint32_t CS_ASYNC_ROWS = 12288;
 static uint32_t g_csq16_groups = 256;                  // q16 row groups up to which 16 records per step are used
-static uint32_t g_cs_narrow_rows = CS_NARROW_ROWS;     // SWIMSIM_CS_NARROW_ROWS (tests: 0 = wide kernel only)
 
 enum CsKind { CS_NONE = 0, CS_WIDE = 1, CS_NARROW = 2 };
 
-// which production kernel a launch of n rows uses
-inline CsKind cs_kind(uint32_t n) { return n == 0 ? CS_NONE : n <= g_cs_narrow_rows ? CS_NARROW : CS_WIDE; }
+// which production kernel a launch of n rows uses (narrow_rows: the handle's crossover, swimsim_tuning)
+inline CsKind cs_kind(uint32_t n, uint32_t narrow_rows = CS_NARROW_ROWS) {
+    return n == 0 ? CS_NONE : n <= narrow_rows ? CS_NARROW : CS_WIDE;
+}
 
 // one launch of the production kernel `kind` over the listed rows (count on the device; n = at most that many)
 void launch_checksum_kind(const DS &d, const uint32_t *list, const uint32_t *count, uint32_t n, CsKind kind, hipStream_t s) {
@@ -188,8 +189,15 @@ void launch_checksum_kind(const DS &d, const uint32_t *list, const uint32_t *cou
     }
 }
 
-void launch_checksum(const DS &d, const uint32_t *list, const uint32_t *count, uint32_t maxn, uint32_t nrows,
-                     hipStream_t s) {
-    const uint32_t n = std::min(maxn, nrows);
-    launch_checksum_kind(d, list, count, n, cs_kind(n), s);
+// the wide kernel with 4 row groups per workgroup and SIMD-placed roles (k_checksum3<..., G = 4>)
+void launch_checksum_wide4(const DS &d, const uint32_t *list, const uint32_t *count, uint32_t n, hipStream_t s) {
+    const uint32_t grid = (n + 4 * CS_ROWS - 1) / (4 * CS_ROWS);
+    switch (d.W) {
+#define CS_CASE(Wv) case Wv: launch_cs3_w<Wv, 0, 4>(d, list, count, grid, s); break;
+        CS_W_CASES(CS_CASE)
+#undef CS_CASE
+    default: break;
+    }
 }
+
+

@@ -6,8 +6,8 @@
 //               complete blocks. It hashes nothing;
 //   wave 1 (H): runs all three FarmHash-mk lanes of every row (h, and the coupled g and f) over the blocks F
 //               completed one step earlier, the M() premixes included.
-// Included by swimsim_kernels.hip after swimsim_checksum2.hip (same record tables, buffer layout and step
-// structure as k_checksum2, whose formatter wave also ran the h lane).
+// Included by swimsim_checksum.hip (record tables, buffer geometry C2_* and lds_barrier are defined there). The
+// superseded k_checksum2, whose formatter wave also ran the h lane, lives in tools/diag.
 //
 // Why the split moved: the chain arithmetic needs no LDS round trip of its own, while the formatter's work is
 // LDS-latency bound (carry copy, record writes, address-word broadcasts). With the h lane on the formatter,
@@ -18,21 +18,44 @@
 // formatter publishes 8 blocks per step and writes nothing; checksums are garbage); 3 as 2 without the
 // per-block predication; 4 as 3 without the hasher's LDS reads (block words from registers); 5 formatter only,
 // without its record stores (the words are folded into a register)
-template <int W, int NO, int NB, int BW, int MODE = 0>
-__global__ void __launch_bounds__(128) k_checksum3(DS d, const uint32_t *list, const uint32_t *count,
-                                                   const uint32_t *__restrict__ addrw, const uint4 *__restrict__ rtail) {
-    __shared__ uint32_t buf[2 * BW * C2_ROWS];
-    __shared__ uint32_t bend[2][C2_ROWS];        // blocks complete after step t (t & 1)
-    __shared__ uint32_t ast[2][16 * 6];          // address words of a super step's 16 members (F only)
+template <int W, int NO, int NB, int BW, int MODE = 0, int G = 1>
+__global__ void __launch_bounds__(128 * G) k_checksum3(DS d, const uint32_t *list, const uint32_t *count,
+                                                       const uint32_t *__restrict__ addrw, const uint4 *__restrict__ rtail) {
+    __shared__ uint32_t bufs[G][2 * BW * C2_ROWS];
+    __shared__ uint32_t bends[G][2][C2_ROWS];    // blocks complete after step t (t & 1)
+    __shared__ uint32_t asts[G][2][16 * 6];      // address words of a super step's 16 members (F only)
     constexpr int Q = W / 4;                     // record words that are pure address words
     static_assert(NO <= Q + 8, "record tail table holds 7 words after the address words");
     static_assert(5 * NB + 4 < BW, "hasher reads past the buffer");
     const uint32_t cnt = *count;
-    if (blockIdx.x * C2_ROWS >= cnt) return;                       // uniform per workgroup
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
-    const uint32_t gi = blockIdx.x * C2_ROWS + lane;
+    if (blockIdx.x * C2_ROWS * G >= cnt) return;                   // uniform per workgroup
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), grp = 0;
+    if (G > 1) {
+        // G row groups of 64 rows, each a formatter and a hasher wave. A workgroup of 2 G waves lands on the CU's four
+        // SIMDs two per SIMD; each SIMD should hold one formatter and one hasher (two hashers on one SIMD share its
+        // VALU and take twice as long), so the roles follow the placement read from HW_ID: on SIMD x the first wave
+        // formats and the second hashes row group x. An uneven placement keeps the wave-index roles.
+        __shared__ uint32_t simd_n[4];
+        uint32_t hwid;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+        const uint32_t simd = (hwid >> 4) & 3u;
+        if (threadIdx.x < 4) simd_n[threadIdx.x] = 0u;
+        __syncthreads();
+        uint32_t slot = 0;
+        if (lane == 0) slot = atomicAdd(&simd_n[simd], 1u);
+        slot = __builtin_amdgcn_readfirstlane(slot);
+        __syncthreads();
+        const bool even = G == 4 && simd_n[0] == 2u && simd_n[1] == 2u && simd_n[2] == 2u && simd_n[3] == 2u;
+        grp = even ? simd : wave % G;
+        wave = even ? slot : wave / G;
+    }
+    uint32_t *const buf = bufs[grp];
+    uint32_t (*const bend)[C2_ROWS] = bends[grp];
+    uint32_t (*const ast)[16 * 6] = asts[grp];
+    const uint32_t gi = (blockIdx.x * G + grp) * C2_ROWS + lane;
     const bool valid = gi < cnt;
-    const uint32_t id = list[valid ? gi : blockIdx.x * C2_ROWS];
+    const uint32_t id = list[valid ? gi : blockIdx.x * C2_ROWS * G];
     const bool is_row = id < d.NL;
     const uint32_t *row = is_row ? d.mw + (size_t)id * d.NP : d.dense + (size_t)(id - d.NL) * d.NP;
     const uint32_t N = d.N;
@@ -241,15 +264,15 @@ __global__ void __launch_bounds__(128) k_checksum3(DS d, const uint32_t *list, c
     }
 }
 
-template <int W, int MODE = 0>
+template <int W, int MODE = 0, int G = 1>
 void launch_cs3_w(const DS &d, const uint32_t *list, const uint32_t *count, uint32_t grid, hipStream_t s) {
     if (W == 19 && d.max_tail <= 21 && d.min_tail >= 19) {     // 13-digit incarnations: records of 38..40 bytes
         constexpr int NO = cs_no(W, 21);
-        hipLaunchKernelGGL((k_checksum3<W, NO, c2_nb(W + 21), c2_bw(W + 21, NO), MODE>), dim3(grid), dim3(128), 0, s, d, list,
-                           count, d.addrw, (const uint4 *)d.rtail8);
+        hipLaunchKernelGGL((k_checksum3<W, NO, c2_nb(W + 21), c2_bw(W + 21, NO), MODE, G>), dim3(grid), dim3(128 * G), 0, s, d,
+                           list, count, d.addrw, (const uint4 *)d.rtail8);
     } else {                                                   // any tail of up to 24 bytes
         constexpr int NO = cs_no(W, 24);
-        hipLaunchKernelGGL((k_checksum3<W, NO, c2_nb(W + 24), c2_bw(W + 24, NO)>), dim3(grid), dim3(128), 0, s, d, list,
-                           count, d.addrw, (const uint4 *)d.rtail8);
+        hipLaunchKernelGGL((k_checksum3<W, NO, c2_nb(W + 24), c2_bw(W + 24, NO), 0, G>), dim3(grid), dim3(128 * G), 0, s, d,
+                           list, count, d.addrw, (const uint4 *)d.rtail8);
     }
 }

@@ -116,8 +116,8 @@ struct DS {
     // change in apply order, {member, member word, source, source e}, tagged with its Update's sequence number
     // (useq of the row when the Update began; all changes of one Update share it, memberlist.go:366-384)
     uint64_t wev_mask;
-    uint4 *wev;               // [slots][wev_cap]
-    unsigned long long *wevt; // [slots][wev_cap] Update tag
+    uint4 **wevs;             // [slots] -> [wev_cap] records (allocated when the slot first turns on = 2)
+    unsigned long long **wevts; // [slots] -> [wev_cap] Update tags
     uint32_t *wev_cnt;        // [slots] records appended since the last drain (may exceed wev_cap: overflow)
     uint32_t wev_cap;
     unsigned long long *useq; // [NL] Update sequence of each row (nullptr: no event stream on); +1 per applying

@@ -64,8 +64,11 @@ struct Transport {
     virtual int bcast(void *buf, size_t bytes, uint32_t root) = 0;
     virtual const char *name() const = 0;
     // true: data() moves the segments in order on the caller's stream (no host synchronisation before the
-    // segments are read, none after they land: later kernels on the stream are ordered after the transfer)
+    // segments are read, none after they land: later kernels on the stream are ordered after the transfer), and
+    // sizes_dev() exchanges device-resident sizes the same way
     virtual bool stream_ordered() const { return false; }
+    // device arrays dsend[G*k] -> drecv[G*k] on stream st, ordered like data() (stream_ordered transports only)
+    virtual int sizes_dev(const uint64_t *dsend, uint64_t *drecv, int k, hipStream_t st) { return SWIMSIM_EINVAL; }
 };
 
 // shards of one process (threads): device-to-device (peer) copies between the shards' buffers
@@ -165,14 +168,18 @@ struct RcclPort : Transport {
         if (int rc = stage(2 * n * 8)) return rc;
         uint64_t *ds = dsz, *dr = dsz + n;
         if (hipMemcpyAsync(ds, send, n * 8, hipMemcpyHostToDevice, st) != hipSuccess) return SWIMSIM_EHIP;
-        ncclGroupStart();
-        for (uint32_t p = 0; p < G; p++) {
-            ncclSend(ds + (size_t)p * k, k, ncclUint64, (int)p, comm, st);
-            ncclRecv(dr + (size_t)p * k, k, ncclUint64, (int)p, comm, st);
-        }
-        if (ncclGroupEnd() != ncclSuccess) return SWIMSIM_EHIP;
+        if (int rc = sizes_dev(ds, dr, k, st)) return rc;
         if (hipMemcpyAsync(recv, dr, n * 8, hipMemcpyDeviceToHost, st) != hipSuccess) return SWIMSIM_EHIP;
         return hipStreamSynchronize(st) == hipSuccess ? 0 : SWIMSIM_EHIP;
+    }
+    int sizes_dev(const uint64_t *dsend, uint64_t *drecv, int k, hipStream_t s) override {
+        if (s != st) return SWIMSIM_EINVAL;                        // one order with data() / bcast()
+        ncclGroupStart();
+        for (uint32_t p = 0; p < G; p++) {
+            ncclSend(dsend + (size_t)p * k, k, ncclUint64, (int)p, comm, st);
+            ncclRecv(drecv + (size_t)p * k, k, ncclUint64, (int)p, comm, st);
+        }
+        return ncclGroupEnd() == ncclSuccess ? 0 : SWIMSIM_EHIP;
     }
     int data(const uint8_t *sbuf, const uint64_t *soff, const uint64_t *sbytes, uint8_t *rbuf, const uint64_t *roff,
              const uint64_t *rbytes, hipStream_t s) override {
@@ -253,6 +260,7 @@ struct swimsim {
     hipStream_t side = nullptr;
     hipEvent_t ev_snap = nullptr, ev_side = nullptr;
     bool cs_async = true, side_pending = false;
+    uint32_t cs_narrow_rows = CS_NARROW_ROWS;     // checksum launches of at most this many rows: narrow kernel
     uint32_t snap_cap = 0;
     uint32_t *side_ids = nullptr, *side_cnt = nullptr;
     uint2 *side_map = nullptr;
@@ -279,6 +287,7 @@ struct swimsim {
     unsigned long long *keys = nullptr, *keys_sorted = nullptr;
     uint32_t keycap = 0;
     uint64_t x_bytes = 0, x_calls = 0;        // exchanged bytes / exchanges (measurement)
+    uint64_t x_syncs = 0;                     // host synchronisations the exchanges took (measurement)
     uint64_t lazy_fallbacks = 0;              // phases whose dirty senders were hashed before issue
     uint64_t alloc_bytes = 0;                 // device bytes held by the handle (dalloc)
     // work buffers
@@ -326,8 +335,11 @@ struct swimsim {
     std::vector<uint8_t> wused;                   // [kWatchCap]
     std::vector<uint32_t> wcs;                    // checksum at the last drain (OldChecksum), per slot
     std::vector<uint32_t> wcs_ev;                 // the same for the per-Update stream's drains
+    std::vector<uint4 *> wev_h;                   // per-Update event log of each slot (allocated at its first on = 2)
+    std::vector<unsigned long long *> wevt_h;
     uint4 *wout = nullptr;
     uint32_t *winfo = nullptr;
+#ifdef SWIMSIM_DIAG
     // reference-row checksum path (swimsim_checksum_delta.hip), allocated at its first launch
     int csd_mode = 0;                             // SWIMSIM_CS_DELTA: 0 off, 1 wide launches, 2 every launch >= 1024 rows
     bool csd_ready = false, csd_failed = false;
@@ -343,6 +355,7 @@ struct swimsim {
                                                   // which a launch keeps the production kernels (0: always the path)
     uint64_t csd_declined = 0;
     double csd_last_mean = 0;
+#endif
     std::string err;
 
     int fail(int code, const char *fmt, ...) {
@@ -429,7 +442,14 @@ constexpr uint32_t kWavesPerBlock = SWIM_WAVE_BLOCK / 64;
 inline uint32_t blocks_for_waves(uint32_t waves) { return waves ? (waves + kWavesPerBlock - 1) / kWavesPerBlock : 1; }
 inline uint32_t blocks_for_threads(uint32_t n) { return n ? (n + 255) / 256 : 1; }
 
+// incarnation steps the checksum tables can hold: the wide formatter addresses d.rtail8 by member word ((e << 3) | status)
+// with 32-byte entries and a 32-bit byte offset, so 2^24 incarnation steps (2^32 bytes) is the limit
+constexpr uint32_t kMaxEcap = 1u << 24;
+
 int build_tail_table(swimsim *h, uint32_t ecap) {
+    if (ecap > kMaxEcap)
+        return h->fail(SWIMSIM_ERANGE, "incarnation step %u beyond the checksum tables (at most 2^24 steps of the period)",
+                       ecap - 1);
     std::vector<uint32_t> t((size_t)ecap * 4 * 8, 0u);
     uint32_t max_tl = 0, min_tl = 0xFFFFFFFFu;
     for (uint32_t e = 0; e < ecap; e++) {
@@ -587,14 +607,25 @@ int xchg(swimsim *h) {
     HIPCHK(h, hipMemsetAsync(h->xsz, 0, 2 * G * 8, h->s));
     hipLaunchKernelGGL(k_x_size, dim3(blocks_for_threads(h->xcap)), dim3(256), 0, h->s, h->d, x, h->xitems, h->xcnt,
                        h->xcap, h->xsz);
-    std::vector<uint64_t> sz(2 * G);
+    // A stream-ordered transport (RcclPort) exchanges the segment sizes on the device right behind k_x_size, so that
+    // the host waits once per exchange, for its own sizes and the peers' together; the others exchange host arrays
+    // after the pack (two host synchronisations).
+    const bool dev_sizes = h->xp->stream_ordered();
+    std::vector<uint64_t> sz(2 * G), sendsz(2 * G), recvsz(2 * G);
     uint32_t nitems = 0;
+    if (dev_sizes) {
+        hipLaunchKernelGGL(k_x_sendsz, dim3(1), dim3(64), 0, h->s, h->xsz, G, h->xsz + 2 * G);
+        if (int rc = h->xp->sizes_dev((const uint64_t *)(h->xsz + 2 * G), (uint64_t *)(h->xsz + 4 * G), 2, h->s))
+            return h->fail(rc, "shard size exchange failed (%s)", h->xp->name());
+        HIPCHK(h, hipMemcpyAsync(recvsz.data(), h->xsz + 4 * G, 2 * G * 8, hipMemcpyDeviceToHost, h->s));
+    }
     HIPCHK(h, hipMemcpyAsync(sz.data(), h->xsz, 2 * G * 8, hipMemcpyDeviceToHost, h->s));
     HIPCHK(h, hipMemcpyAsync(&nitems, h->xcnt, 4, hipMemcpyDeviceToHost, h->s));
     HIPCHK(h, hipStreamSynchronize(h->s));
+    h->x_syncs++;
     if (nitems > h->xcap) return h->fail(SWIMSIM_ECAPACITY, "exchange item list overflow (%u items)", nitems);
     // send segments: [parcel offset table][parcels], 16-byte aligned
-    std::vector<uint64_t> soff(G), sbytes(G), tbl(G), cur(3 * G), sendsz(2 * G), recvsz(2 * G);
+    std::vector<uint64_t> soff(G), sbytes(G), tbl(G), cur(3 * G);
     uint64_t total = 0;
     for (uint32_t p = 0; p < G; p++) {
         tbl[p] = (sz[2 * p + 1] * 4 + 15) & ~15ull;
@@ -604,7 +635,7 @@ int xchg(swimsim *h) {
         cur[p] = soff[p];            // xseg
         cur[G + p] = 0;              // table cursor
         cur[2 * G + p] = tbl[p];     // parcel cursor
-        sendsz[2 * p] = sbytes[p];
+        sendsz[2 * p] = sbytes[p];   // (k_x_sendsz computes the same on the device)
         sendsz[2 * p + 1] = sz[2 * p + 1];
     }
     if (total > h->sbuf_cap) {
@@ -616,10 +647,12 @@ int xchg(swimsim *h) {
     if (nitems)
         hipLaunchKernelGGL(k_x_pack, dim3(blocks_for_waves(nitems)), dim3(SWIM_WAVE_BLOCK), 0, h->s, h->d, x, h->xitems, h->xcnt,
                            h->xcap, h->sbuf, h->xseg, h->xtcur, h->xdcur);
-    // the packed segments are read by the peers (local copies) or staged through the host: complete them first;
-    // RCCL sends them in stream order after the pack
-    if (!h->xp->stream_ordered()) HIPCHK(h, hipStreamSynchronize(h->s));
-    if (int rc = h->xp->sizes(sendsz.data(), recvsz.data(), 2)) return h->fail(rc, "shard size exchange failed (%s)", h->xp->name());
+    if (!dev_sizes) {
+        // the packed segments are read by the peers (local copies) or staged through the host: complete them first
+        HIPCHK(h, hipStreamSynchronize(h->s));
+        if (int rc = h->xp->sizes(sendsz.data(), recvsz.data(), 2)) return h->fail(rc, "shard size exchange failed (%s)", h->xp->name());
+        h->x_syncs += 2;
+    }
     std::vector<uint64_t> roff(G), rbytes(G);
     std::vector<ulonglong2> srcs(G);
     uint64_t rtotal = 0, nparc = 0;
@@ -662,6 +695,7 @@ int shard_sum(swimsim *h, uint64_t v, uint64_t *out) {
 // checksums of the dirty rows selected by mode (k_list). Mode 0 (all dirty rows) hashes one row per
 // distinct content: rows are grouped by fingerprint, compared word for word with their group's first
 // row, and equal rows copy its checksum (k_fp_*).
+#ifdef SWIMSIM_DIAG
 // the reference-row path (swimsim_checksum_delta.hip) for launches of n rows (n known on the host)
 bool csd_wanted(swimsim *h, uint32_t n, CsKind kind) {
     if (h->csd_mode == 0 || h->csd_failed || n < CSD_MIN_ROWS || h->N < 1024) return false;
@@ -750,12 +784,13 @@ int csd_hash(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t n, 
     if (nf) {
         h->csd_fallback_rows += nf;
         for (uint32_t b = 0; b < CSD_NFLAGS; b++) h->csd_reasons[b] += hf[1 + b];
-        const CsKind k2 = cs_kind(nf);
+        const CsKind k2 = cs_kind(nf, h->cs_narrow_rows);
         Scope sc(h, k2 == CS_WIDE ? F_CS_WIDE : F_CS_NARROW);
         launch_checksum_kind(h->d, h->csd_fb, h->csd_fbcnt, nf, k2, h->s);
     }
     return 0;
 }
+#endif
 
 // one FarmHash dispatch over the rows listed (count on the device; nrows = the count if the host
 // knows it, else ~0u), timed as F_CS_WIDE / F_CS_NARROW
@@ -777,11 +812,13 @@ void hash_rows(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t m
             list = out;
     }
     const uint32_t n = std::min(maxn, nrows);
-    const CsKind kind = cs_kind(n);
-    if (!st && nrows != ~0u && csd_wanted(h, n, kind)) {
+    const CsKind kind = cs_kind(n, h->cs_narrow_rows);
+#ifdef SWIMSIM_DIAG
+    if (!st && nrows != ~0u && csd_wanted(h, n, kind)) {          // diagnostics library: the reference-row path
         const int rc = csd_hash(h, list, cnt, n);
         if (rc <= 0) return;                                       // done (or failed loudly: h->err)
     }
+#endif
     Scope sc(h, kind == CS_WIDE ? F_CS_WIDE : F_CS_NARROW, st);
     launch_checksum_kind(h->d, list, cnt, n, kind, st ? st : h->s);
 }
@@ -1324,8 +1361,10 @@ int step_one(swimsim *h, const swimsim_event *ev, size_t nev) {
 
 int ensure_ecap(swimsim *h, uint32_t upto) {
     if (upto < h->ecap) return 0;
+    if (upto >= kMaxEcap)
+        return h->fail(SWIMSIM_ERANGE, "incarnation step %u beyond the checksum tables (at most 2^24 steps of the period)", upto);
     uint32_t c = h->ecap;
-    while (c <= upto) c *= 2;
+    while (c <= upto) c = c >= kMaxEcap / 2 ? kMaxEcap : c * 2;
     HIPCHK(h, hipStreamSynchronize(h->s));
     return build_tail_table(h, c);
 }
@@ -1334,7 +1373,7 @@ int to_e(swimsim *h, int64_t inc_ms, uint32_t *e) {
     const int64_t dlt = inc_ms - h->t0;
     if (dlt < 0 || dlt % h->period) return h->fail(SWIMSIM_ERANGE, "incarnation %lld is not t0 + e*period", (long long)inc_ms);
     const int64_t q = dlt / h->period;
-    if (q >= (1ll << 29)) return h->fail(SWIMSIM_ERANGE, "incarnation %lld too far from t0", (long long)inc_ms);
+    if (q >= (int64_t)kMaxEcap) return h->fail(SWIMSIM_ERANGE, "incarnation %lld too far from t0 (at most 2^24 periods)", (long long)inc_ms);
     *e = (uint32_t)q;
     return 0;
 }
@@ -1357,7 +1396,7 @@ int set_shards(swimsim *h, uint32_t G, uint32_t rank, const std::vector<uint32_t
     h->xcap = (uint32_t)((size_t)h->N * h->K + h->N + 64);
     h->needcap = h->NL * (G - 1) + 64;
     if ((rc = dalloc(h, &sl, G + 1, "shard table")) || (rc = dalloc(h, &h->xitems, h->xcap, "exchange items")) ||
-        (rc = dalloc(h, &h->xcnt, 1, "exchange count")) || (rc = dalloc(h, &h->xsz, 2 * G, "exchange sizes")) ||
+        (rc = dalloc(h, &h->xcnt, 1, "exchange count")) || (rc = dalloc(h, &h->xsz, 6 * G, "exchange sizes")) ||
         (rc = dalloc(h, &h->xseg, 3 * G, "exchange cursors")) || (rc = dalloc(h, &h->xsrcs, G, "exchange sources")) ||
         (rc = dalloc(h, &h->needlist, h->needcap, "need list")) || (rc = dalloc(h, &h->needcnt, 1, "need count")))
         return rc;
@@ -1446,6 +1485,12 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
         h->err = "address width must be 13..20 bytes";
         return bail(SWIMSIM_EINVAL);
     }
+#ifdef SWIMSIM_DEV_W19
+    if (h->W != 19) {                      // a development build has checksum kernels for W = 19 only
+        h->err = "this library was built with DEV=1 (checksum kernels for 19-byte addresses only)";
+        return bail(SWIMSIM_EINVAL);
+    }
+#endif
     if (hipSetDevice(h->device) != hipSuccess) {
         h->err = "hipSetDevice failed (no usable MI355X device)";
         return bail(SWIMSIM_EHIP);
@@ -1457,10 +1502,13 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
         h->err = "hipStreamCreate / hipEventCreate failed";
         return bail(SWIMSIM_EHIP);
     }
-    if (const char *v = getenv("SWIMSIM_CS_ASYNC")) h->cs_async = atoi(v) != 0;
-    if (const char *v = getenv("SWIMSIM_CS_NARROW_ROWS")) g_cs_narrow_rows = (uint32_t)strtoul(v, nullptr, 10);
+    const swimsim_tuning *tun = cfg->tuning;     // test / diagnostic variants (NULL: production)
+    if (tun && tun->cs_async >= 0) h->cs_async = tun->cs_async != 0;
+    if (tun && tun->cs_narrow_rows >= 0) h->cs_narrow_rows = (uint32_t)tun->cs_narrow_rows;
+#ifdef SWIMSIM_DIAG                                 // diagnostics library only: the reference-row path
     if (const char *v = getenv("SWIMSIM_CS_DELTA")) h->csd_mode = atoi(v);
     if (const char *v = getenv("SWIMSIM_CS_DELTA_MAXDIFF")) h->csd_maxdiff = (uint32_t)strtoul(v, nullptr, 10);
+#endif
     DS &d = h->d;
     d.N = h->N; d.NP = h->NP; d.NL = h->NL; d.lo = h->lo;
     d.NB = h->NP / 64;
@@ -1488,10 +1536,10 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
     hipMemset(d.nhe, 0, (size_t)h->NL * 4);
     hipMemset(d.cpslot, 0xFF, (size_t)h->NL * 4);
     {
-        // hot columns: 2,048 slots per row (1.6 GB at 65,536 rows); SWIMSIM_HOT_SLOTS=0 turns
-        // them off (results are the same either way: the columns are copies)
+        // hot columns: 2,048 slots per row (1.6 GB at 65,536 rows); swimsim_tuning.hot_slots = 0
+        // turns them off (results are the same either way)
         uint32_t hp = std::min<uint32_t>(2048u, h->NP);
-        if (const char *v = getenv("SWIMSIM_HOT_SLOTS")) hp = std::min<uint32_t>((uint32_t)strtoul(v, nullptr, 10), h->NP);
+        if (tun && tun->hot_slots >= 0) hp = std::min<uint32_t>((uint32_t)tun->hot_slots, h->NP);
         hp = (hp + 63) & ~63u;
         d.hidx = nullptr; d.hlist = nullptr; d.hmw = nullptr; d.hde = nullptr; d.hotnew = nullptr; d.hot_cnt = nullptr;
         d.HP = 0;
@@ -1545,12 +1593,12 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
         hipMemGetInfo(&freeb, &totalb);
         const uint64_t by_mem = (uint64_t)(freeb / 3) / (4ull * h->NP);
         d.dense_cap = (uint32_t)std::max<uint64_t>(64, std::min<uint64_t>(2ull * h->NL + 64, by_mem));
-        if (const char *v = getenv("SWIMSIM_DENSE_CAP"))               // tests: a small pool exercises the fallbacks
-            d.dense_cap = (uint32_t)std::max<unsigned long>(64, std::min<unsigned long>(d.dense_cap, strtoul(v, nullptr, 10)));
+        if (tun && tun->dense_slots >= 0)                           // tests: a small pool exercises the fallbacks
+            d.dense_cap = std::max<uint32_t>(64, std::min<uint32_t>(d.dense_cap, (uint32_t)tun->dense_slots));
         // side-stream checksum snapshots (latency-bound phase C launches only), up to 1/8 of the free HBM
         const uint64_t snap_mem = (uint64_t)(freeb / 8) / (4ull * h->NP);
         uint64_t async_rows = CS_ASYNC_ROWS;
-        if (const char *v = getenv("SWIMSIM_CS_ASYNC_ROWS")) async_rows = strtoull(v, nullptr, 10);
+        if (tun && tun->cs_async_rows >= 0) async_rows = (uint64_t)tun->cs_async_rows;
         h->snap_cap = h->cs_async ? (uint32_t)std::min<uint64_t>(std::min<uint64_t>(async_rows, h->NL), snap_mem) : 0u;
     }
     const size_t nslots = (size_t)d.dense_cap + h->snap_cap;
@@ -1991,27 +2039,33 @@ __global__ void k_iota(uint32_t *list, uint32_t *cnt, uint32_t n) {
     if (i < n) list[i] = i;
 }
 
-// mode 0: the production choice for nrows rows; 1: k_checksum3; 2: k_checksum_q16 (both production kernels).
-// Other modes (superseded kernels, diagnostic variants) exist only in the diagnostics library.
+// mode 0: the production choice for nrows rows; 1: k_checksum3; 2: k_checksum_q16 (both production kernels); 4: the
+// wide kernel with four row groups per workgroup (k_checksum3<..., G = 4>). Other modes (the reference-row path,
+// superseded kernels, diagnostic variants) exist only in the diagnostics library.
 int swimsim_bench_checksum(swimsim_t *h, uint32_t nrows, int32_t mode, int32_t reps, double *ms) {
     if (!h || !ms || nrows == 0 || nrows > h->NL || reps < 1) return SWIMSIM_EINVAL;
 #ifndef SWIMSIM_DIAG
-    if (mode < 0 || mode > 3)
+    if (mode < 0 || mode > 4 || mode == 3)
         return h->fail(SWIMSIM_EINVAL, "checksum mode %d: diagnostics build only", mode);
-#endif
+    const bool csd = false;
+#else
     // mode 3: the reference-row path (swimsim_checksum_delta.hip), its preparation and any fallback launch included;
-    // 31..46 (diagnostics library): its split modes (garbage checksums: helpers alone, hashers alone, helpers without
-    // exceptions; + 8: no barrier between super steps)
+    // 31..46: its split modes (garbage checksums: helpers alone, hashers alone, helpers without exceptions; + 8: no
+    // barrier between super steps)
     const bool csd = mode == 3 || (mode >= 31 && mode <= 46);
     if (csd && (csd_alloc(h) || nrows > h->NL)) return h->fail(SWIMSIM_EINVAL, "reference-row path unavailable");
+#endif
     auto launch = [&]() {
         if (csd) {                                                 // the path itself, never declined here
+#ifdef SWIMSIM_DIAG
             const uint32_t keep = h->csd_maxdiff;
             h->csd_maxdiff = 0;
             (void)csd_hash(h, h->list, h->cnt, nrows, mode == 3 ? 0u : (uint32_t)(mode - 30));
             h->csd_maxdiff = keep;
+#endif
         }
-        else if (mode <= 2) launch_checksum_kind(h->d, h->list, h->cnt, nrows, mode == 0 ? cs_kind(nrows) : (CsKind)mode, h->s);
+        else if (mode <= 2) launch_checksum_kind(h->d, h->list, h->cnt, nrows, mode == 0 ? cs_kind(nrows, h->cs_narrow_rows) : (CsKind)mode, h->s);
+        else if (mode == 4) launch_checksum_wide4(h->d, h->list, h->cnt, nrows, h->s);
 #ifdef SWIMSIM_DIAG
         else launch_checksum_mode(h->d, h->list, h->cnt, nrows, mode, h->s);
 #endif
@@ -2086,17 +2140,21 @@ int swimsim_watch(swimsim_t *h, uint32_t o, int32_t on) {
         h->wused.assign(kWatchCap, 0);
         h->wcs.assign(kWatchCap, 0);
     }
-    if (on == 2 && !h->d.useq) {                                   // the per-Update stream's buffers, on first use
+    if (on == 2 && !h->d.useq) {                                   // the per-Update stream's tables, on first use
         int rc = 0;
         h->d.wev_cap = std::max<uint32_t>(4u * h->NP, 4096u);
-        if ((rc = dalloc(h, &h->d.wev, (size_t)kWatchCap * h->d.wev_cap, "per-Update event log")) ||
-            (rc = dalloc(h, &h->d.wevt, (size_t)kWatchCap * h->d.wev_cap, "per-Update event tags")) ||
+        if ((rc = dalloc(h, &h->d.wevs, kWatchCap, "per-Update event log pointers")) ||
+            (rc = dalloc(h, &h->d.wevts, kWatchCap, "per-Update event tag pointers")) ||
             (rc = dalloc(h, &h->d.wev_cnt, kWatchCap, "per-Update event counts")) ||
             (rc = dalloc(h, &h->d.useq, h->NL, "Update sequence")))
             return rc;
+        HIPCHK(h, hipMemsetAsync(h->d.wevs, 0, kWatchCap * sizeof(void *), h->s));
+        HIPCHK(h, hipMemsetAsync(h->d.wevts, 0, kWatchCap * sizeof(void *), h->s));
         HIPCHK(h, hipMemsetAsync(h->d.wev_cnt, 0, kWatchCap * 4, h->s));
         HIPCHK(h, hipMemsetAsync(h->d.useq, 0, (size_t)h->NL * 8, h->s));
         h->wcs_ev.assign(kWatchCap, 0);
+        h->wev_h.assign(kWatchCap, nullptr);
+        h->wevt_h.assign(kWatchCap, nullptr);
     }
     uint32_t slot = h->wslot_h[ol];
     if (on && slot == SRC_NONE) {
@@ -2119,6 +2177,14 @@ int swimsim_watch(swimsim_t *h, uint32_t o, int32_t on) {
         return SWIMSIM_OK;
     }
     if (on == 2 && !((h->d.wev_mask >> slot) & 1ull)) {                // the per-Update stream starts empty now
+        if (!h->wev_h[slot]) {            // this slot's log (24 B x wev_cap), kept for the slot's later watches
+            int rc = 0;
+            if ((rc = dalloc(h, &h->wev_h[slot], h->d.wev_cap, "per-Update event log")) ||
+                (rc = dalloc(h, &h->wevt_h[slot], h->d.wev_cap, "per-Update event tags")))
+                return rc;
+            HIPCHK(h, hipMemcpyAsync(h->d.wevs + slot, &h->wev_h[slot], sizeof(void *), hipMemcpyHostToDevice, h->s));
+            HIPCHK(h, hipMemcpyAsync(h->d.wevts + slot, &h->wevt_h[slot], sizeof(void *), hipMemcpyHostToDevice, h->s));
+        }
         if (int rc = checksum_dirty(h, 0)) return rc;
         HIPCHK(h, hipMemsetAsync(h->d.wev_cnt + slot, 0, 4, h->s));
         HIPCHK(h, hipMemcpyAsync(&h->wcs_ev[slot], h->d.cs + ol, 4, hipMemcpyDeviceToHost, h->s));
@@ -2159,8 +2225,8 @@ int swimsim_applied_events(swimsim_t *h, uint32_t o, int32_t *member, int32_t *s
     std::vector<uint4> rec(cnt);
     std::vector<unsigned long long> tag(cnt);
     if (cnt) {
-        HIPCHK(h, hipMemcpyAsync(rec.data(), h->d.wev + (size_t)slot * h->d.wev_cap, (size_t)cnt * 16, hipMemcpyDeviceToHost, h->s));
-        HIPCHK(h, hipMemcpyAsync(tag.data(), h->d.wevt + (size_t)slot * h->d.wev_cap, (size_t)cnt * 8, hipMemcpyDeviceToHost, h->s));
+        HIPCHK(h, hipMemcpyAsync(rec.data(), h->wev_h[slot], (size_t)cnt * 16, hipMemcpyDeviceToHost, h->s));
+        HIPCHK(h, hipMemcpyAsync(tag.data(), h->wevt_h[slot], (size_t)cnt * 8, hipMemcpyDeviceToHost, h->s));
     }
     HIPCHK(h, hipMemsetAsync(h->d.wev_cnt + slot, 0, 4, h->s));
     HIPCHK(h, hipStreamSynchronize(h->s));
@@ -2514,12 +2580,25 @@ int swimsim_debug_exchange(swimsim_t *h, const uint8_t *send, const uint64_t *sb
 
 int swimsim_checksum_path_stats(swimsim_t *h, uint64_t *delta_launches, uint64_t *fallback_rows, uint64_t *reasons) {
     if (!h) return SWIMSIM_EINVAL;
+#ifdef SWIMSIM_DIAG
     if (delta_launches) *delta_launches = h->csd_launches;
     if (fallback_rows) *fallback_rows = h->csd_fallback_rows;
     if (reasons) {
         for (uint32_t b = 0; b < CSD_NFLAGS; b++) reasons[b] = h->csd_reasons[b];
         reasons[CSD_NFLAGS] = h->csd_declined;
     }
+#else                                       // the product library has no reference-row path (tools/diag)
+    if (delta_launches) *delta_launches = 0;
+    if (fallback_rows) *fallback_rows = 0;
+    if (reasons)
+        for (uint32_t b = 0; b < 8; b++) reasons[b] = 0;
+#endif
+    return SWIMSIM_OK;
+}
+
+int swimsim_exchange_syncs(swimsim_t *h, uint64_t *syncs) {
+    if (!h || !syncs) return SWIMSIM_EINVAL;
+    *syncs = h->x_syncs;
     return SWIMSIM_OK;
 }
 

@@ -128,8 +128,8 @@ __device__ __forceinline__ void merge_change_w(const DS &d, uint32_t ol, uint32_
             if ((d.wev_mask >> ws) & 1ull) {                       // per-Update stream: append in apply order
                 const uint32_t at = atomicAdd(d.wev_cnt + ws, 1u);
                 if (at < d.wev_cap) {
-                    d.wev[(size_t)ws * d.wev_cap + at] = make_uint4(m, nw_, nsrc, nsinc);
-                    d.wevt[(size_t)ws * d.wev_cap + at] = acc.tag;
+                    d.wevs[ws][at] = make_uint4(m, nw_, nsrc, nsinc);
+                    d.wevts[ws][at] = acc.tag;
                 }
             }
         }

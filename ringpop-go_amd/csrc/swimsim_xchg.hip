@@ -84,6 +84,18 @@ __global__ void k_x_size(DS d, XArgs x, const uint4 *items, const uint32_t *cnt,
     atomicAdd(&sz[2 * it.x + 1], 1ull);
 }
 
+// the segment each destination receives from this shard, {bytes, parcels}, from k_x_size's totals: the layout xchg()
+// computes on the host (a 4-B offset per parcel, the table 16-byte aligned, then the parcels). A stream-ordered
+// transport sends these to the peers on the device, so the host waits once per exchange
+__global__ void k_x_sendsz(const unsigned long long *sz, uint32_t G, unsigned long long *out) {
+    for (uint32_t p = threadIdx.x; p < G; p += blockDim.x) {
+        const unsigned long long n = sz[2 * p + 1];
+        const unsigned long long tbl = (n * 4ull + 15ull) & ~15ull;
+        out[2 * p] = n ? tbl + sz[2 * p] : 0ull;
+        out[2 * p + 1] = n;
+    }
+}
+
 // one wave per item: claim a table slot and a parcel offset in the destination's segment, write both
 __global__ void k_x_pack(DS d, XArgs x, const uint4 *items, const uint32_t *cnt, uint32_t cap, uint8_t *buf,
                          const unsigned long long *segoff, unsigned long long *tcur, unsigned long long *dcur) {

@@ -49,7 +49,26 @@ class Config(C.Structure):
         ("max_reverse_full_sync_jobs", C.c_uint32), ("p_factor", C.c_uint32), ("seed", C.c_uint64),
         ("addresses", C.c_char_p), ("addr_stride", C.c_uint32), ("max_rounds", C.c_uint32),
         ("message_pool_bytes", C.c_uint64), ("observer_begin", C.c_uint32), ("observer_end", C.c_uint32),
+        ("tuning", C.c_void_p),
     ]
+
+
+class Tuning(C.Structure):
+    """swimsim_tuning (include/swimsim.h): engine variants for tests and diagnostics, -1 = the production default."""
+    _fields_ = [("hot_slots", C.c_int32), ("dense_slots", C.c_int32), ("cs_async", C.c_int32),
+                ("cs_async_rows", C.c_int32), ("cs_narrow_rows", C.c_int32)]
+
+
+def make_tuning(tuning):
+    """a Tuning struct from a dict of its fields (None: the production engine)"""
+    if not tuning:
+        return None
+    t = Tuning(-1, -1, -1, -1, -1)
+    for k, v in tuning.items():
+        if k not in dict(Tuning._fields_):
+            raise ValueError(f"unknown tuning field {k}")
+        setattr(t, k, int(v))
+    return t
 
 
 class Event(C.Structure):
@@ -148,6 +167,7 @@ def load_library(path: str = LIB_PATH):
         "swimsim_comm_attach": (C.c_int, [P, u32, u32, P, sz]),
         "swimsim_shard_info": (C.c_int, [P, C.POINTER(u32), C.POINTER(u32), C.POINTER(u32), C.POINTER(u32),
                                          C.POINTER(u64), C.POINTER(u64)]),
+        "swimsim_exchange_syncs": (C.c_int, [P, C.POINTER(u64)]),
         "swimsim_comm_attach_host": (C.c_int, [P, u32, u32, C.POINTER(HostTransport)]),
         "swimsim_debug_exchange": (C.c_int, [P, P, P, P, sz, P]),
         "swimsim_watch": (C.c_int, [P, u32, i32]),
@@ -175,7 +195,7 @@ def _events(events):
 
 def make_config(n, *, t0_ms=T0_MS, period_ms=200, suspect_ms=5000, faulty_ms=24 * 3600 * 1000, tombstone_ms=60_000,
                 ping_request_size=3, max_rfs_jobs=5, p_factor=15, seed=1, device=0, max_rounds=0,
-                message_pool_bytes=0, observer_range=None):
+                message_pool_bytes=0, observer_range=None, tuning=None):
     cfg = Config()
     cfg.num_members, cfg.device, cfg.t0_ms, cfg.protocol_period_ms = n, device, t0_ms, period_ms
     cfg.suspect_timeout_ms, cfg.faulty_timeout_ms, cfg.tombstone_timeout_ms = suspect_ms, faulty_ms, tombstone_ms
@@ -183,6 +203,9 @@ def make_config(n, *, t0_ms=T0_MS, period_ms=200, suspect_ms=5000, faulty_ms=24 
     cfg.seed, cfg.max_rounds, cfg.message_pool_bytes = seed, max_rounds, message_pool_bytes
     if observer_range:
         cfg.observer_begin, cfg.observer_end = observer_range
+    cfg._tuning = make_tuning(tuning)               # kept alive with the config
+    if cfg._tuning is not None:
+        cfg.tuning = C.cast(C.pointer(cfg._tuning), C.c_void_p)
     return cfg
 
 
@@ -214,10 +237,12 @@ class Cluster:
 
     def __init__(self, n, *, t0_ms=T0_MS, period_ms=200, suspect_ms=5000, faulty_ms=24 * 3600 * 1000,
                  tombstone_ms=60_000, ping_request_size=3, max_rfs_jobs=5, p_factor=15, seed=1, addresses=None,
-                 device=0, init="converged", max_rounds=0, message_pool_bytes=0, observer_range=None, comm=None):
+                 device=0, init="converged", max_rounds=0, message_pool_bytes=0, observer_range=None, comm=None,
+                 tuning=None):
         """comm = (nranks, rank, unique_id): attach this handle as shard `rank` of a cluster spread over
         nranks processes (RCCL); or comm = (nranks, rank, transport) with a swimsim.dist host transport
-        object (any process group). observer_range then defaults to the canonical shard."""
+        object (any process group). observer_range then defaults to the canonical shard.
+        tuning = {field: value} of swimsim_tuning (tests and diagnostics: engine variants, identical results)."""
         L = load_library()
         self.n = n
         self.t0_ms, self.period_ms = t0_ms, period_ms
@@ -231,6 +256,9 @@ class Cluster:
         cfg.seed, cfg.max_rounds, cfg.message_pool_bytes = seed, max_rounds, message_pool_bytes
         if observer_range:
             cfg.observer_begin, cfg.observer_end = observer_range
+        self._tuning = make_tuning(tuning)
+        if self._tuning is not None:
+            cfg.tuning = C.cast(C.pointer(self._tuning), C.c_void_p)
         self._addr_buf = None
         if addresses is not None:
             stride = max(len(a) for a in addresses)
@@ -527,8 +555,10 @@ class Cluster:
         xb, xc = C.c_uint64(), C.c_uint64()
         self._chk(load_library().swimsim_shard_info(self.h, C.byref(g), C.byref(r), C.byref(lo), C.byref(hi),
                                                     C.byref(xb), C.byref(xc)))
+        xs = C.c_uint64()
+        self._chk(load_library().swimsim_exchange_syncs(self.h, C.byref(xs)))
         return {"shards": g.value, "rank": r.value, "lo": lo.value, "hi": hi.value, "exchanged_bytes": xb.value,
-                "exchanges": xc.value}
+                "exchanges": xc.value, "exchange_host_syncs": xs.value}
 
     CSD_REASONS = ("short", "entry_cap", "window_plan", "entry_batch", "exception_slots", "jump_slots", "window_miss",
                    "declined_launches")
@@ -697,18 +727,18 @@ class ShardedCluster:
         return all(c.converged() for c in self.shards) and len(set(int(cs[o]) for o in live)) <= 1
 
     def kernel_units(self):
-        """unit counts behind kernel_times' bytes since enable_timing: rows hashed per checksum kernel, changes
-        processed / applied per merge kernel, records issued, ..."""
-        cap = 32
-        names = (C.c_char_p * cap)()
-        vals = np.zeros(cap, np.float64)
-        n = C.c_size_t()
-        self._chk(load_library().swimsim_kernel_units(self.h, names, vals.ctypes.data, cap, C.byref(n)))
-        return {names[i].decode(): float(vals[i]) for i in range(n.value)}
+        """unit counts behind kernel_times' bytes since enable_timing, summed over the shards: rows hashed per
+        checksum kernel, changes processed / applied per merge kernel, records issued, ..."""
+        tot = {}
+        for c in self.shards:
+            for k, v in c.kernel_units().items():
+                tot[k] = tot.get(k, 0.0) + v
+        return tot
 
     def profile_mark(self, mark_id):
-        """one k_profile_mark dispatch: rocprofv3 counter passes are cut between two marks (tools/pmc_summary.py)"""
-        self._chk(load_library().swimsim_profile_mark(self.h, mark_id))
+        """one k_profile_mark dispatch per shard (rocprofv3 counter passes are cut between marks)"""
+        for c in self.shards:
+            c.profile_mark(mark_id)
 
     def shard_info(self):
         return [c.shard_info() for c in self.shards]

@@ -54,6 +54,8 @@ class Workload:
     events: list = field(default_factory=list)
     description: str = ""
     until_converged: bool = False
+    init: str = "converged"                      # initial rows: "converged" (everyone knows everyone) or "self"
+    seed_members: list = field(default_factory=list)   # members every node learns by MakeChange before round 0
 
     def events_for(self, r):
         return [e for e in self.events if e[0] == r]
@@ -104,3 +106,14 @@ def config5(n=262144, rounds=100, frac=0.10, every=20, seed=13):
     for r in range(0, rounds, every):
         ev += [(r, EV_REINCARNATE, m, 0) for m in distinct_members(seed, r, 6, k, n)]
     return Workload(f"config5_bursts_n{n}", n, rounds, ev, f"{k} members reincarnate every {every} rounds")
+
+
+def selfstart(n=16384, seeds=2, rounds=40):
+    """Every node starts knowing only itself (a swim.Node before Bootstrap) plus members 0..seeds-1, which each node
+    learns by MakeChange (memberlist.go:282-307). Gossip spreads the seeded changes; once a sender's filtered
+    changes run dry while the two checksums differ, the receiver answers with its whole membership (full sync,
+    disseminator.go:156-181) and the sender asks back (reverse full sync, disseminator.go:257-304), so both paths
+    run at size."""
+    return Workload(f"selfstart_n{n}_s{seeds}", n, rounds, [], f"self-only start, members 0..{seeds - 1} seeded by "
+                    f"MakeChange at every node", init="self", seed_members=list(range(seeds)))
+

@@ -6,8 +6,10 @@
                        node has changes and all live checksums are equal) (configs[3])
   config5_n4096.json   4,096 members, 10 % of them Reincarnate every 20 rounds, 100 rounds (configs[4] at the
                        largest size the oracle runs in minutes)
+  selfstart_n16384.json 16,384 members starting self-only, members 0 and 1 seeded at every node by MakeChange, 40
+                       rounds: the full-sync and reverse-full-sync paths at size (counters full_syncs, rfs_done > 0)
   config3_n65536.json  bench.py's own workload: 65,536 members, 655 killed at round 10 (Philox seed 11), rounds
-                       0-44: steady state, the kill, the suspect wave and the first faulty timers (r >= 35)
+                       0-99: steady state, the kill, the suspect wave and the whole faulty wave (r >= 35)
                        (configs[2]; dense oracle rows ~39 GB, generated in the 62-GB build container)
 
 Each per-round record holds: the round, sha256 of the checksum vector (uint32 little-endian, observer order),
@@ -18,7 +20,7 @@ The oracle is oracle/swim_oracle.c built with OpenMP over observers (oracle/buil
 tests/test_oracle_kats.py::test_openmp_oracle_equals_single_thread pins that build to the single-threaded one.
 TEST INFRASTRUCTURE ONLY: tests/test_parity_at_size.py compares the MI355X engine with these files on the GPU.
 
-usage: python tests/golden/make_size_fixtures.py {config2|config4|config5|config3} [threads]"""
+usage: python tests/golden/make_size_fixtures.py {config2|config4|config5|config3|selfstart} [threads]"""
 import hashlib
 import json
 import os
@@ -42,8 +44,18 @@ CONFIGS = {
     "config2": (lambda: W.config2(n=4096, rounds=200), False, "config2_n4096.json"),
     "config4": (lambda: W.config4(n=16384, rounds=260), True, "config4_n16384.json"),
     "config5": (lambda: W.config5(n=4096, rounds=100), False, "config5_n4096.json"),
-    "config3": (lambda: W.config3(n=65536, rounds=45, kill_round=10), False, "config3_n65536.json"),
+    "config3": (lambda: W.config3(n=65536, rounds=100, kill_round=10), False, "config3_n65536.json"),
+    "selfstart": (lambda: W.selfstart(n=16384, seeds=2, rounds=40), False, "selfstart_n16384.json"),
 }
+
+
+def seed_rows(sim, wl, alive=0):
+    """the workload's MakeChange seeding before round 0 (oracle or engine: both take make_change(o, m, inc, status))"""
+    t0 = 1_500_000_000_000
+    for o in range(wl.n):
+        for m in wl.seed_members:
+            if m != o:
+                sim.make_change(o, m, t0, alive)
 
 
 def sha(a, dt):
@@ -59,8 +71,9 @@ def record(ora, r, conv):
 def generate(name):
     make, until_conv, fname = CONFIGS[name]
     wl = make()
-    last_event = max(e[0] for e in wl.events)
-    ora = OracleSim(wl.n)
+    last_event = max((e[0] for e in wl.events), default=-1)
+    ora = OracleSim(wl.n, init=wl.init)
+    seed_rows(ora, wl)
     recs, t0 = [], time.time()
     for r in range(wl.rounds):
         ora.step(wl.events_for(r))

@@ -6,9 +6,8 @@ full-sync decision are read from that slot once the side stream has finished.
 The overlap only happens inside one swimsim_step call of several rounds (a step returns with every
 checksum current), so these tests step the engine several rounds at a time and compare with the
 oracle at every chunk boundary, bit-exact. They also check that the side-stream path and the
-synchronous path (SWIMSIM_CS_ASYNC=0) give identical states.
+synchronous path (swimsim_tuning.cs_async = 0) give identical states.
 """
-import os
 
 import numpy as np
 import pytest
@@ -95,17 +94,8 @@ def test_chunked_sharded_self_only():
 
 def test_async_equals_sync_path():
     wl = W.config3(n=1024, rounds=50, kill_round=5)
-    old = os.environ.get("SWIMSIM_CS_ASYNC")
-    try:
-        os.environ["SWIMSIM_CS_ASYNC"] = "0"
-        sync = swimsim.Cluster(wl.n)
-        os.environ["SWIMSIM_CS_ASYNC"] = "1"
-        asy = swimsim.Cluster(wl.n)
-    finally:
-        if old is None:
-            os.environ.pop("SWIMSIM_CS_ASYNC", None)
-        else:
-            os.environ["SWIMSIM_CS_ASYNC"] = old
+    sync = swimsim.Cluster(wl.n, tuning={"cs_async": 0})
+    asy = swimsim.Cluster(wl.n, tuning={"cs_async": 1})
     for r0 in range(0, wl.rounds, 10):
         ev = [e for e in wl.events if r0 <= e[0] < r0 + 10]
         sync.step(10, ev)

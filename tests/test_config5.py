@@ -3,7 +3,6 @@ budget. A reincarnation burst dirties many rows at once, and lazy C_o (k_issue) 
 per dirty sender. When the snapshot slots could not hold them, the engine hashes the dirty senders before issue
 instead (bound_lazy_snapshots): exact either way. These tests force a small slot pool so that the
 fallback runs, and compare every round with the oracle."""
-import os
 
 import pytest
 
@@ -15,11 +14,7 @@ pytestmark = pytest.mark.gpu
 
 
 def _small_pool_pair(n, cap=64):
-    os.environ["SWIMSIM_DENSE_CAP"] = str(cap)
-    try:
-        return make_pair(n)
-    finally:
-        del os.environ["SWIMSIM_DENSE_CAP"]
+    return make_pair(n, tuning={"dense_slots": cap})
 
 
 def test_config5_bursts_with_a_small_snapshot_pool():

@@ -1,12 +1,14 @@
-"""The reference-row checksum path (swimsim_checksum_delta.hip: k_csd_scan + k_cs_delta) against the CPU oracle.
+"""The reference-row checksum path (tools/diag/swimsim_checksum_delta.hip: k_csd_scan + k_cs_delta) against the CPU
+oracle. The path lives in the diagnostics library only (round 4: it did not pay over the cascade), so
+these tests run when that library is the one loaded:
+    SWIMSIM_LIBRARY=tools/libswimsim_diag.so python -m pytest tests/test_cs_delta.py -m gpu
+and skip otherwise.
 
 The path is forced onto every phase-C launch of at least 1,024 rows (SWIMSIM_CS_DELTA=2, synchronous phase C so
 every launch goes through it) at sizes where the oracle runs every round: the cascade (rows a few records apart),
 churn (incarnation bumps: longer and shorter records), a partition (rows half a membership apart: the workgroup
 plans fail and the rows go to the production kernels) and a self-only start. Bit-exact per round, as every
-other checksum kernel (memberlist.go:83-128). At the bench's own size the path runs by default (wide launches)
-under tests/test_parity_at_size.py's per-round fixture of config 3 at 65,536 members.
-"""
+other checksum kernel (memberlist.go:83-128). """
 import os
 
 import numpy as np
@@ -16,16 +18,17 @@ from oracle_ffi import OracleSim
 import swimsim
 from swimsim import workloads as W
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif("libswimsim_diag" not in os.environ.get("SWIMSIM_LIBRARY", ""),
+                                 reason="reference-row path: diagnostics library only (SWIMSIM_LIBRARY=tools/libswimsim_diag.so)")]
 
 
 def forced(n, **kw):
-    old = {k: os.environ.get(k) for k in ("SWIMSIM_CS_DELTA", "SWIMSIM_CS_ASYNC", "SWIMSIM_CS_DELTA_MAXDIFF")}
+    old = {k: os.environ.get(k) for k in ("SWIMSIM_CS_DELTA", "SWIMSIM_CS_DELTA_MAXDIFF")}
     try:
         os.environ["SWIMSIM_CS_DELTA"] = "2"
-        os.environ["SWIMSIM_CS_ASYNC"] = "0"
         os.environ["SWIMSIM_CS_DELTA_MAXDIFF"] = str(kw.pop("maxdiff", 0))
-        return swimsim.Cluster(n, **kw)
+        return swimsim.Cluster(n, tuning={"cs_async": 0}, **kw)
     finally:
         for k, v in old.items():
             if v is None:

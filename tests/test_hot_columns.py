@@ -1,10 +1,9 @@
 """Hot columns: per-row compact copies of the row words and dissemination cells of the members that sit
 in dissemination buffers, read by issue, merge and bump instead of one scattered sector per member. They are copies,
 so no result may depend on them (the slot is a hot member's dissemination cell, written back to the dense
-array before the slots are dropped or a row is read back): these tests run workloads with the columns off (SWIMSIM_HOT_SLOTS=0), with a few
+array before the slots are dropped or a row is read back): these tests run workloads with the columns off (swimsim_tuning.hot_slots = 0), with a few
 slots that overflow (members beyond them stay on the dense path) and with the default, and require every round to
 match the oracle or the column-free engine bit for bit."""
-import os
 
 import pytest
 
@@ -15,30 +14,18 @@ from test_engine_parity import make_pair, run_parity
 pytestmark = pytest.mark.gpu
 
 
-def _with_slots(slots, fn):
-    old = os.environ.get("SWIMSIM_HOT_SLOTS")
-    os.environ["SWIMSIM_HOT_SLOTS"] = str(slots)
-    try:
-        return fn()
-    finally:
-        if old is None:
-            del os.environ["SWIMSIM_HOT_SLOTS"]
-        else:
-            os.environ["SWIMSIM_HOT_SLOTS"] = old
-
-
 @pytest.mark.parametrize("slots", [0, 64])
 def test_churn_parity_with_few_or_no_hot_slots(slots):
     # config 2's churn brings new members into buffers every round: 64 slots fill up and later members stay dense
     wl = W.config2(n=256, rounds=40)
-    eng, ora = _with_slots(slots, lambda: make_pair(wl.n))
+    eng, ora = make_pair(wl.n, tuning={"hot_slots": slots})
     run_parity(eng, ora, wl.n, wl.rounds, wl.events)
 
 
 def test_cascade_same_with_and_without_hot_columns():
     wl = W.config3(n=4096, rounds=45, kill_round=3)
     on = swimsim.Cluster(wl.n)
-    off = _with_slots(0, lambda: swimsim.Cluster(wl.n))
+    off = swimsim.Cluster(wl.n, tuning={"hot_slots": 0})
     try:
         for r in range(wl.rounds):
             ev = wl.events_for(r)

@@ -7,8 +7,9 @@
   oracle fixtures (tests/golden/make_size_fixtures.py): every round, the sha256 of the checksum vector and of the
   phase-S targets, the three canonical state digests (rows, dissemination buffers, timer tables) and the protocol
   counters must be equal.
-* config 3 at 65,536 members, bench.py's exact workload (kill at round 10), rounds 0-44 against a committed
-  fixture of the OpenMP oracle, every round as above.
+* config 3 at 65,536 members, bench.py's exact workload (kill at round 10), all 100 rounds against a committed
+  fixture of the OpenMP oracle, every round as above; unsharded and split over 8 observer-row shards.
+* a self-only start at 16,384 members (full syncs and reverse full syncs at size) against its fixture.
 * config 3 at 65,536 members through the suspect AND faulty waves (75 rounds, kill at round 2): beyond the fixture,
   parity is checked through size-independent properties every 5 rounds: each sampled observer's checksum equals
   Fingerprint32 of the reference's checksum string (memberlist.go:106-128) rebuilt on the host from the engine's
@@ -44,10 +45,21 @@ def load_fixture(name):
         return json.load(f)
 
 
-def compare_with_fixture(wl, fx):
+def seed_rows(eng, wl):
+    """the workload's MakeChange seeding before round 0 (tests/golden/make_size_fixtures.py seed_rows)"""
+    for o in range(wl.n):
+        for m in wl.seed_members:
+            if m != o:
+                eng.make_change(o, m, swimsim.T0_MS, swimsim.ALIVE)
+
+
+def compare_with_fixture(wl, fx, shards=None, on_round=None, **kw):
+    """every round of the fixture: checksum vector, phase-S targets, the three state digests and the counters.
+    shards: the same run split over that many observer-row shards of this process (ShardedCluster, LocalPort)."""
     assert fx["n"] == wl.n and fx["workload"] == wl.name
-    eng = swimsim.Cluster(wl.n)
+    eng = swimsim.ShardedCluster(wl.n, shards, init=wl.init, **kw) if shards else swimsim.Cluster(wl.n, init=wl.init, **kw)
     try:
+        seed_rows(eng, wl)
         for rec in fx["records"]:
             r = rec["round"]
             assert eng.round == r
@@ -58,6 +70,8 @@ def compare_with_fixture(wl, fx):
                 assert v == rec[k], f"round {r}: {k} differs: engine {v} oracle {rec[k]}"
             if rec["converged"]:
                 assert eng.converged(), f"round {r}: the oracle converged, the engine does not"
+            if on_round:
+                on_round(eng, r)
         return eng.counters(), fx["records"][-1]
     finally:
         eng.close()
@@ -79,12 +93,46 @@ def test_config4_full_size_to_convergence_vs_oracle_fixture():
 
 def test_config3_n65536_bench_workload_vs_oracle_fixture():
     """bench.py's own workload at its own size, every round against the OpenMP oracle (north star: bit-exact
-    per-round parity at 16-64k members): 65,536 members, 655 killed at round 10, rounds 0-44 (steady state, the
-    kill, the suspect wave, the first faulty timers at r >= 35)."""
-    wl = W.config3(n=65536, rounds=45, kill_round=10)
-    c, last = compare_with_fixture(wl, load_fixture("config3_n65536.json"))
-    assert last["round"] == 44
+    per-round parity at 16-64k members): 65,536 members, 655 killed at round 10, all of config 3's 100 rounds
+    (steady state, the kill, the suspect wave, the whole faulty wave from r = 35 on: state_transitions.go:90-117)."""
+    fx = load_fixture("config3_n65536.json")
+    wl = W.config3(n=65536, rounds=fx["rounds"], kill_round=10)
+    c, last = compare_with_fixture(wl, fx)
+    assert last["round"] == 99
     assert c["suspect_decl"] > 0 and c["timers_fired"] > 0 and c["pingreqs"] > 0
+
+
+def test_config3_n65536_eight_shards_vs_oracle_fixture():
+    """The 8-way observer-row split the north star names, at full size on one GPU: ShardedCluster(65536, 8) (eight
+    shards of 8,192 rows in this process, cross-shard messages by device copies: the exchange RCCL carries between
+    GPUs, ping_sender.go:90), every round against the same oracle fixture. Each shard's message pool is sized
+    explicitly (the automatic size takes a share of the HBM left, which the first shards would exhaust). Records
+    the bytes each shard exchanged per round."""
+    fx = load_fixture("config3_n65536.json")
+    wl = W.config3(n=65536, rounds=fx["rounds"], kill_round=10)
+    per_round = []
+    last = [0] * 8
+
+    def xbytes(eng, r):
+        now = [s["exchanged_bytes"] for s in eng.shard_info()]
+        per_round.append([a - b for a, b in zip(now, last)])
+        last[:] = now
+
+    c, rec = compare_with_fixture(wl, fx, shards=8, on_round=xbytes, message_pool_bytes=4 << 30)
+    assert rec["round"] == 99 and c["timers_fired"] > 0
+    peak = max(max(x) for x in per_round)
+    print(f"exchanged bytes per shard per round: peak {peak}, round 20 {per_round[20]}, round 60 {per_round[60]}")
+    assert all(x > 0 for x in per_round[20])
+
+
+def test_selfstart_n16384_full_syncs_vs_oracle_fixture():
+    """Full syncs and reverse full syncs at size (disseminator.go:156-181, 257-304): 16,384 nodes that start knowing
+    only themselves and two seeded members, 40 rounds, every round against the oracle fixture."""
+    wl = W.selfstart(n=16384, seeds=2, rounds=40)
+    c, last = compare_with_fixture(wl, load_fixture("selfstart_n16384.json"))
+    assert last["round"] == 39
+    assert last["counters"]["full_syncs"] > 0 and last["counters"]["rfs_done"] > 0
+    assert c["full_syncs"] > 0 and c["rfs_done"] > 0
 
 
 def test_config5_bursts_n4096_vs_oracle_fixture():
