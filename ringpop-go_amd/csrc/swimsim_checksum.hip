@@ -142,6 +142,8 @@ constexpr int cs_no(int W, int maxtail) { return (3 + W + maxtail + 3) / 4; }
 
 #include "swimsim_checksum3.hip"
 #include "swimsim_checksum4.hip"
+#include "swimsim_checksum_ref.hip"
+#include "swimsim_checksum_csr.hip"
 #ifdef SWIMSIM_DIAG                            // tools/diag (diagnostics library only): the reference-row path
 #include "swimsim_checksum_delta.hip"          // (off by default in round 3, not a win over the cascade), the 3-wave
 #include "swimsim_checksum5.hip"               // and fast-path experiments and every superseded kernel

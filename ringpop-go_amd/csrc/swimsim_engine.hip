@@ -339,6 +339,21 @@ struct swimsim {
     std::vector<unsigned long long *> wevt_h;
     uint4 *wout = nullptr;
     uint32_t *winfo = nullptr;
+    // reference-row checksum path (swimsim_checksum_ref.hip + swimsim_checksum_csr.hip), allocated at its first launch
+    int csr_mode = 0;                             // swimsim_tuning.cs_ref: 0 off, 1 wide launches, 2 every launch of
+                                                  // at least CSD_MIN_ROWS rows
+    bool csr_ready = false, csr_failed = false;
+    uint32_t *csr_B = nullptr, *csr_Lb = nullptr, *csr_OB = nullptr, *csr_SBw = nullptr, *csr_fb = nullptr,
+             *csr_fbcnt = nullptr, *csr_nrec = nullptr;
+    size_t csr_sbw_words = 0;
+    uint4 *csr_ent = nullptr, *csr_P = nullptr;
+    CsdRow *csr_rinfo = nullptr;
+    CsrPlan *csr_plan = nullptr;
+    CsrRec *csr_rec = nullptr;
+    uint32_t csr_ecap = 2048, csr_rcap = 512, csr_KP = 0;
+    uint32_t csr_maxdiff = 0;                     // swimsim_tuning.cs_ref_maxdiff: mean differing members per sampled
+                                                  // row above which a launch keeps the production kernels (0: never)
+    uint64_t csr_launches = 0, csr_fallback_rows = 0, csr_declined = 0;
 #ifdef SWIMSIM_DIAG
     // reference-row checksum path (swimsim_checksum_delta.hip), allocated at its first launch
     int csd_mode = 0;                             // SWIMSIM_CS_DELTA: 0 off, 1 wide launches, 2 every launch >= 1024 rows
@@ -792,6 +807,113 @@ int csd_hash(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t n, 
 }
 #endif
 
+// the reference-row path (swimsim_checksum_csr.hip) for a launch of n rows (n known on the host)
+bool csr_wanted(swimsim *h, uint32_t n, CsKind kind) {
+    if (h->csr_mode == 0 || h->csr_failed || n < CSD_MIN_ROWS || h->N < 1024) return false;
+    return kind == CS_WIDE || h->csr_mode == 2;
+}
+
+int csr_alloc(swimsim *h) {
+    if (h->csr_ready) return 0;
+    const uint32_t rows = h->NL + h->d.dense_cap;                    // a launch lists rows and dense snapshots
+    h->csr_sbw_words = ((size_t)h->N * (h->W + 32) + 256) / 4;
+    h->csr_KP = (uint32_t)(h->csr_sbw_words * 4 / 20 + 2);
+    int rc = 0;
+    if ((rc = dalloc(h, &h->csr_B, (size_t)h->NP, "csr reference row")) ||
+        (rc = dalloc(h, &h->csr_Lb, (size_t)h->N + 1, "csr reference lengths")) ||
+        (rc = dalloc(h, &h->csr_OB, (size_t)h->N + 1, "csr reference offsets")) ||
+        (rc = dalloc(h, &h->csr_SBw, h->csr_sbw_words, "csr reference string")) ||
+        (rc = dalloc(h, &h->csr_P, (size_t)20 * h->csr_KP * 2, "csr premix table")) ||
+        (rc = dalloc(h, &h->csr_fb, (size_t)rows, "csr fallback list")) ||
+        (rc = dalloc(h, &h->csr_fbcnt, 1, "csr fallback count")) ||
+        (rc = dalloc(h, &h->csr_rinfo, (size_t)rows, "csr row info")) ||
+        (rc = dalloc(h, &h->csr_ent, (size_t)rows * h->csr_ecap * 2, "csr exception entries")) ||
+        (rc = dalloc(h, &h->csr_plan, (size_t)rows / CSR_ROWS + 1, "csr plans")) ||
+        (rc = dalloc(h, &h->csr_rec, (size_t)rows * h->csr_rcap, "csr records")) ||
+        (rc = dalloc(h, &h->csr_nrec, (size_t)rows, "csr record counts"))) {
+        h->csr_failed = true;                                      // the production kernels stay in charge
+        h->err.clear();
+        return rc;
+    }
+    size_t need = 0;
+    hipcub::DeviceScan::ExclusiveSum(nullptr, need, h->csr_Lb, h->csr_OB, (int)h->N + 1, h->s);
+    if (need > h->cub_bytes) {
+        void *p = nullptr;
+        if (hipMalloc(&p, need) != hipSuccess) { h->csr_failed = true; return SWIMSIM_ENOMEM; }
+        h->allocs.push_back(p);
+        h->alloc_bytes += need;
+        h->cub_tmp = p;
+        h->cub_bytes = need;
+    }
+    h->csr_ready = true;
+    return 0;
+}
+
+// hash the n listed rows (count on the device) by the reference-row path. Returns 0 when every row is hashed (rows the
+// path leaves go to the production kernels here), 1 when the path is unavailable or declined (the caller hashes them),
+// < 0 on a HIP error (h->err set)
+int csr_hash(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t n, bool force = false) {
+    if (n > h->NL + h->d.dense_cap) return 1;
+    if (csr_alloc(h)) return 1;
+    CsdArgs ca{};
+    ca.B = h->csr_B;
+    ca.OB = h->csr_OB;
+    ca.SBw = h->csr_SBw;
+    ca.sbw_words = (uint32_t)h->csr_sbw_words;
+    ca.ent = h->csr_ent;
+    ca.rinfo = h->csr_rinfo;
+    ca.ecap = h->csr_ecap;
+    CsrArgs a{};
+    a.P = h->csr_P;
+    a.KP = h->csr_KP;
+    a.ent = h->csr_ent;
+    a.rinfo = h->csr_rinfo;
+    a.ecap = h->csr_ecap;
+    a.plan = h->csr_plan;
+    a.rec = h->csr_rec;
+    a.nrec = h->csr_nrec;
+    a.rcap = h->csr_rcap;
+    a.fb_list = h->csr_fb;
+    a.fb_cnt = h->csr_fbcnt;
+    {
+        Scope sc(h, F_CSD_SCAN);
+        hipLaunchKernelGGL(k_csd_ref, dim3((h->N + 256) / 256), dim3(256), 0, h->s, h->d, list, n, h->csr_B, h->csr_Lb);
+        if (h->csr_maxdiff && !force) {
+            // rows far from the majority make many exception blocks: decide on a sample
+            HIPCHK(h, hipMemsetAsync(h->csr_fbcnt, 0, 4, h->s));
+            hipLaunchKernelGGL(k_csd_sample, dim3(CSD_NSAMPLE), dim3(256), 0, h->s, h->d, list, n, h->csr_B, h->csr_fbcnt);
+            HIPCHK(h, hipMemcpyAsync(h->hinfo + 16, h->csr_fbcnt, 4, hipMemcpyDeviceToHost, h->s));
+            HIPCHK(h, hipStreamSynchronize(h->s));
+            if ((double)h->hinfo[16] / CSD_NSAMPLE > (double)h->csr_maxdiff) { h->csr_declined++; return 1; }
+        }
+        size_t bytes = h->cub_bytes;
+        HIPCHK(h, hipcub::DeviceScan::ExclusiveSum(h->cub_tmp, bytes, h->csr_Lb, h->csr_OB, (int)h->N + 1, h->s));
+        HIPCHK(h, hipMemsetAsync(h->csr_SBw, 0, h->csr_sbw_words * 4, h->s));
+        launch_csr(h->d, list, n, cnt, ca, a, h->s, 0);
+        launch_csr(h->d, list, n, cnt, ca, a, h->s, 1);
+        launch_csr(h->d, list, n, cnt, ca, a, h->s, 2);
+        launch_csr(h->d, list, n, cnt, ca, a, h->s, 3);
+        HIPCHK(h, hipMemsetAsync(h->csr_fbcnt, 0, 4, h->s));
+        hipLaunchKernelGGL(k_ctr_add, dim3(1), dim3(1), 0, h->s, h->d, (int)C_X_CSD_SCANNED, (unsigned long long)n);
+    }
+    {
+        Scope sc(h, F_CS_WIDE);
+        launch_csr(h->d, list, n, cnt, ca, a, h->s, 4);
+    }
+    h->csr_launches++;
+    uint32_t nf = 0;
+    HIPCHK(h, hipMemcpyAsync(h->hinfo + 16, h->csr_fbcnt, 4, hipMemcpyDeviceToHost, h->s));
+    HIPCHK(h, hipStreamSynchronize(h->s));
+    nf = h->hinfo[16];
+    if (nf) {                                                      // rows the path left: the production kernels
+        h->csr_fallback_rows += nf;
+        const CsKind k2 = cs_kind(nf, h->cs_narrow_rows);
+        Scope sc(h, k2 == CS_WIDE ? F_CS_WIDE : F_CS_NARROW);
+        launch_checksum_kind(h->d, h->csr_fb, h->csr_fbcnt, nf, k2, h->s);
+    }
+    return 0;
+}
+
 // one FarmHash dispatch over the rows listed (count on the device; nrows = the count if the host
 // knows it, else ~0u), timed as F_CS_WIDE / F_CS_NARROW
 // A main-stream launch of a known number of rows (at least 64) hashes them in row order: lists come out of atomic
@@ -813,8 +935,12 @@ void hash_rows(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t m
     }
     const uint32_t n = std::min(maxn, nrows);
     const CsKind kind = cs_kind(n, h->cs_narrow_rows);
+    if (!st && nrows != ~0u && csr_wanted(h, n, kind)) {          // the reference-row path (swimsim_checksum_csr.hip)
+        const int rc = csr_hash(h, list, cnt, n);
+        if (rc <= 0) return;                                       // done (or failed loudly: h->err)
+    }
 #ifdef SWIMSIM_DIAG
-    if (!st && nrows != ~0u && csd_wanted(h, n, kind)) {          // diagnostics library: the reference-row path
+    if (!st && nrows != ~0u && csd_wanted(h, n, kind)) {          // diagnostics library: round 3's reference-row path
         const int rc = csd_hash(h, list, cnt, n);
         if (rc <= 0) return;                                       // done (or failed loudly: h->err)
     }
@@ -1505,6 +1631,8 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
     const swimsim_tuning *tun = cfg->tuning;     // test / diagnostic variants (NULL: production)
     if (tun && tun->cs_async >= 0) h->cs_async = tun->cs_async != 0;
     if (tun && tun->cs_narrow_rows >= 0) h->cs_narrow_rows = (uint32_t)tun->cs_narrow_rows;
+    if (tun && tun->cs_ref >= 0) h->csr_mode = tun->cs_ref;
+    if (tun && tun->cs_ref_maxdiff >= 0) h->csr_maxdiff = (uint32_t)tun->cs_ref_maxdiff;
 #ifdef SWIMSIM_DIAG                                 // diagnostics library only: the reference-row path
     if (const char *v = getenv("SWIMSIM_CS_DELTA")) h->csd_mode = atoi(v);
     if (const char *v = getenv("SWIMSIM_CS_DELTA_MAXDIFF")) h->csd_maxdiff = (uint32_t)strtoul(v, nullptr, 10);
@@ -2040,12 +2168,13 @@ __global__ void k_iota(uint32_t *list, uint32_t *cnt, uint32_t n) {
 }
 
 // mode 0: the production choice for nrows rows; 1: k_checksum3; 2: k_checksum_q16 (both production kernels); 4: the
-// wide kernel with four row groups per workgroup (k_checksum3<..., G = 4>). Other modes (the reference-row path,
+// wide kernel with four row groups per workgroup (k_checksum3<..., G = 4>); 5: the reference-row path (k_csd_scan,
+// k_csr and the fallback launch for rows it leaves), forced. Other modes (the reference-row path,
 // superseded kernels, diagnostic variants) exist only in the diagnostics library.
 int swimsim_bench_checksum(swimsim_t *h, uint32_t nrows, int32_t mode, int32_t reps, double *ms) {
     if (!h || !ms || nrows == 0 || nrows > h->NL || reps < 1) return SWIMSIM_EINVAL;
 #ifndef SWIMSIM_DIAG
-    if (mode < 0 || mode > 4 || mode == 3)
+    if (mode < 0 || mode > 5 || mode == 3)
         return h->fail(SWIMSIM_EINVAL, "checksum mode %d: diagnostics build only", mode);
     const bool csd = false;
 #else
@@ -2055,6 +2184,7 @@ int swimsim_bench_checksum(swimsim_t *h, uint32_t nrows, int32_t mode, int32_t r
     const bool csd = mode == 3 || (mode >= 31 && mode <= 46);
     if (csd && (csd_alloc(h) || nrows > h->NL)) return h->fail(SWIMSIM_EINVAL, "reference-row path unavailable");
 #endif
+    if (mode == 5 && csr_alloc(h)) return h->fail(SWIMSIM_EINVAL, "reference-row path unavailable");
     auto launch = [&]() {
         if (csd) {                                                 // the path itself, never declined here
 #ifdef SWIMSIM_DIAG
@@ -2066,6 +2196,7 @@ int swimsim_bench_checksum(swimsim_t *h, uint32_t nrows, int32_t mode, int32_t r
         }
         else if (mode <= 2) launch_checksum_kind(h->d, h->list, h->cnt, nrows, mode == 0 ? cs_kind(nrows, h->cs_narrow_rows) : (CsKind)mode, h->s);
         else if (mode == 4) launch_checksum_wide4(h->d, h->list, h->cnt, nrows, h->s);
+        else if (mode == 5) (void)csr_hash(h, h->list, h->cnt, nrows, true);   // the reference-row path, forced
 #ifdef SWIMSIM_DIAG
         else launch_checksum_mode(h->d, h->list, h->cnt, nrows, mode, h->s);
 #endif
@@ -2587,11 +2718,13 @@ int swimsim_checksum_path_stats(swimsim_t *h, uint64_t *delta_launches, uint64_t
         for (uint32_t b = 0; b < CSD_NFLAGS; b++) reasons[b] = h->csd_reasons[b];
         reasons[CSD_NFLAGS] = h->csd_declined;
     }
-#else                                       // the product library has no reference-row path (tools/diag)
-    if (delta_launches) *delta_launches = 0;
-    if (fallback_rows) *fallback_rows = 0;
-    if (reasons)
+#else                                       // the product's reference-row path (swimsim_checksum_csr.hip)
+    if (delta_launches) *delta_launches = h->csr_launches;
+    if (fallback_rows) *fallback_rows = h->csr_fallback_rows;
+    if (reasons) {
         for (uint32_t b = 0; b < 8; b++) reasons[b] = 0;
+        reasons[7] = h->csr_declined;
+    }
 #endif
     return SWIMSIM_OK;
 }

@@ -1140,7 +1140,13 @@ __device__ __forceinline__ void recv_one(const DS &d, const RecvArgs &a, uint32_
 // phase: a receiver writes only its own row, dissemination buffer and timers, and reads only the
 // senders' issue-time snapshots (S_o, I_o, C_o). So this equals the wave-by-wave schedule of
 // docs/ROUND_SEMANTICS.md §4 D, without a launch per inbox position.
-__global__ void k_recv(DS d, RecvArgs a) {
+// launch bounds: 256 threads (SWIM_WAVE_BLOCK) and at least RECV_MIN_WAVES waves per SIMD. The receive waves are
+// gather-latency bound (each message is a chain of dependent loads: record, hot index, row word, then the stores), so
+// resident waves, not registers, set the pace
+#ifndef RECV_MIN_WAVES
+#define RECV_MIN_WAVES 4
+#endif
+__global__ void __launch_bounds__(256, RECV_MIN_WAVES) k_recv(DS d, RecvArgs a) {
     const uint32_t u = wave_gid();
     if (u >= a.nruns_max) return;
     const uint32_t key = a.ukeys[u];

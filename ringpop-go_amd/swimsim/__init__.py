@@ -56,14 +56,15 @@ class Config(C.Structure):
 class Tuning(C.Structure):
     """swimsim_tuning (include/swimsim.h): engine variants for tests and diagnostics, -1 = the production default."""
     _fields_ = [("hot_slots", C.c_int32), ("dense_slots", C.c_int32), ("cs_async", C.c_int32),
-                ("cs_async_rows", C.c_int32), ("cs_narrow_rows", C.c_int32)]
+                ("cs_async_rows", C.c_int32), ("cs_narrow_rows", C.c_int32), ("cs_ref", C.c_int32),
+                ("cs_ref_maxdiff", C.c_int32)]
 
 
 def make_tuning(tuning):
     """a Tuning struct from a dict of its fields (None: the production engine)"""
     if not tuning:
         return None
-    t = Tuning(-1, -1, -1, -1, -1)
+    t = Tuning(*([-1] * len(Tuning._fields_)))
     for k, v in tuning.items():
         if k not in dict(Tuning._fields_):
             raise ValueError(f"unknown tuning field {k}")

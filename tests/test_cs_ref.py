@@ -1,0 +1,90 @@
+"""The product's reference-row checksum path (csrc/swimsim_checksum_csr.hip: k_csd_scan + k_csr_ptable + k_csr_rec +
+k_csr, and the production kernels for the rows it leaves) against the CPU oracle, bit for bit
+(memberlist.go:83-128: every checksum is Fingerprint32 of the row's sorted member string).
+
+The path is forced onto every phase-C launch of at least 1,024 rows (swimsim_tuning.cs_ref = 2, cs_async = 0 so that
+every launch runs on the main stream) at sizes where the oracle runs every round: the cascade (rows a few records
+apart), churn (incarnation bumps: longer and shorter records), a partition (rows half a membership apart: wide
+shift ranges, workgroups whose window does not fit fall back), incarnation bursts and a self-only start (rows that
+differ from the reference almost everywhere). At size, the path is compared with the engine's own checksums on real
+cascade rows (swimsim_bench_checksum mode 5).
+"""
+import numpy as np
+import pytest
+
+from oracle_ffi import OracleSim
+import swimsim
+from swimsim import workloads as W
+
+pytestmark = pytest.mark.gpu
+
+
+def forced(n, **kw):
+    return swimsim.Cluster(n, tuning={"cs_ref": 2, "cs_async": 0, "cs_ref_maxdiff": kw.pop("maxdiff", 0)}, **kw)
+
+
+def run_vs_oracle(wl, rounds, init="converged", seed_members=()):
+    eng = forced(wl.n, init=init)
+    ora = OracleSim(wl.n, init=init)
+    for o in range(wl.n):
+        for m in seed_members:
+            if m != o:
+                eng.make_change(o, m, swimsim.T0_MS, swimsim.ALIVE)
+                ora.make_change(o, m, swimsim.T0_MS, 0)
+    for r in range(rounds):
+        ev = wl.events_for(r)
+        eng.step(1, ev)
+        ora.step(ev)
+        ec, oc = eng.checksums(), ora.checksums()
+        bad = np.nonzero(ec != oc)[0]
+        assert len(bad) == 0, f"round {r}: {len(bad)} checksums differ, first rows {bad[:5]}"
+        assert eng.digest() == ora.digest(), f"round {r}: state digest differs"
+    return eng
+
+
+def test_cascade_n2048_every_round():
+    wl = W.config3(n=2048, rounds=60, kill_round=5)
+    eng = run_vs_oracle(wl, 60)
+    st = eng.checksum_path_stats()
+    print("cascade n2048", st)
+    assert st["delta_launches"] >= 4, st
+
+
+def test_churn_n2048_every_round():
+    wl = W.config2(n=2048, rounds=40)
+    eng = run_vs_oracle(wl, 40)
+    st = eng.checksum_path_stats()
+    print("churn n2048", st)
+    assert st["delta_launches"] >= 5, st
+
+
+def test_partition_n2048_every_round():
+    wl = W.config4(n=2048, rounds=90)
+    eng = run_vs_oracle(wl, 90)
+    print("partition n2048", eng.checksum_path_stats())
+
+
+def test_bursts_n2048_every_round():
+    wl = W.config5(n=2048, rounds=45, every=20)
+    eng = run_vs_oracle(wl, 45)
+    print("bursts n2048", eng.checksum_path_stats())
+
+
+def test_selfstart_n1024_every_round():
+    wl = W.selfstart(n=1024, seeds=2, rounds=25)
+    eng = run_vs_oracle(wl, 25, init="self", seed_members=wl.seed_members)
+    print("selfstart n1024", eng.checksum_path_stats())
+
+
+@pytest.mark.parametrize("n,rounds", [(4096, 18), (16384, 16)])
+def test_mode5_on_real_cascade_rows(n, rounds):
+    wl = W.config3(n=n, rounds=rounds + 1, kill_round=10)
+    c = swimsim.Cluster(n)
+    for r in range(rounds):
+        c.step(1, wl.events_for(r))
+    ref = c.checksums().copy()
+    for rows in (1024, 3000, n):
+        c.bench_checksum(rows, 5, reps=1)
+        got = c.checksums()
+        assert (got[:rows] == ref[:rows]).all(), f"{rows} rows: {(got[:rows] != ref[:rows]).sum()} differ"
+    print(f"real rows n{n}", c.checksum_path_stats())

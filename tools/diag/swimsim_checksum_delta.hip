@@ -1,20 +1,8 @@
-// swimsim_checksum_delta.hip — phase C FarmHash-32 (memberlist.go:83-128, go-farm Fingerprint32) for launches of many
-// rows that are nearly equal: the reference-row ("delta") path. Included by swimsim_checksum.hip.
+// tools/diag/swimsim_checksum_delta.hip — DIAGNOSTICS LIBRARY ONLY: round 3's reference-row chain kernel k_cs_delta
+// (helper waves premix S_B's window at every phase, copy exception blocks and write jump lists; h-chain and g/f-chain
+// waves), kept for comparison with the product's k_csr (csrc/swimsim_checksum_csr.hip). The reference row, string and
+// scan it consumes are csrc/swimsim_checksum_ref.hip's.
 //
-// The rows hashed in one round are views of the same membership: in a cascade round a row differs from the
-// column-wise majority of the rows in 0.1-100 of 65,536 members (tools/delta_probe.py, profiles/r03_delta_probe.json).
-// The FarmHash chain is still one sequential chain per row, but everything the chain consumes besides its own state
-// is a function of 32 string bytes (the block's 20 and the next block's first 12). Outside the few blocks whose 32
-// bytes touch a differing record, a row's string IS the reference string S_B shifted by the row's accumulated
-// record-length difference s, so the block's premixed values are those of S_B at byte offset 20k - s:
-//
-//   k_csd_ref     reference words B: per member, the Boyer-Moore majority of up to 31 rows sampled from the launch
-//   (hipcub)      O_B: B's record offsets (exclusive sum of B's record lengths; O_B[N] = |S_B|)
-//   k_csd_string  S_B, B's checksum string, materialised once per launch (2.5 MB at 65,536 members)
-//   k_csd_scan    one wave per row: the members whose record differs from B's (one coalesced pass over the row),
-//                 merged into runs of "exception" blocks (blocks whose 32 bytes meet a differing record, plus block 0
-//                 and the row's last block, whose look-ahead is zero), and the premixed values of every exception
-//                 block, generated from the row's own words
 //   k_cs_delta    256 rows per workgroup, one workgroup per CU. Four hasher waves (lane = row, one wave per SIMD) run
 //                 the chain in carried-sum form: 12 VALU instructions a block, its premixed values read from LDS at
 //                 an address that advances by 24 bytes a block and jumps only where an exception run begins or ends.
@@ -23,11 +11,6 @@
 //                 blocks beside it, and each row's jump list.
 // Rows the delta path cannot take (entry or LDS-slot overflow, a workgroup whose shifts spread too far) are flagged
 // and re-hashed by the production kernels (k_checksum3 / k_checksum_q16); results are bit-exact either way.
-//
-// Carried-sum block (swimsim_checksum4.hip): with X = state + the block's first word of that lane,
-//   F = 5 ror(X ^ M, 19);  Xf' = F_f + F_g + PF;  Xg' = F_g + Xf' + D;  Xh' = F_h + KH
-//   M_g = M(c), M_f = M(b + e c1), M_h = M(d), PF = 2C + a + d + c', D = PG - PF = C + a + b' - c', KH = C + e + a'
-// (a', b', c' = the next block's first words, zero after the last block, so that X ends as the state itself).
 
 constexpr int CSD_SB = 32;            // blocks per super step
 constexpr int CSD_PF = 4;             // blocks the chain waves' LDS reads run ahead
@@ -51,342 +34,6 @@ constexpr uint32_t CSD_NOJ = 0xFFFFu; // unused jump slot
 constexpr uint32_t CSD_JB = 128;      // jump word: block i << 16 | (target - 3 i + CSD_JB), target in uint2 units
 constexpr int CSD_JWMAX = 160;        // window positions at most (the workgroup's shifts spread < 2,500 bytes)
 constexpr int CSD_SBST = 5 * CSD_SB + 16;      // staged S_B words per super step (its SB new positions)
-constexpr uint32_t CSD_C = 0xe6546b64u;
-constexpr uint32_t CSD_MIN_ROWS = 1024; // launches of fewer rows keep the production kernels
-
-
-// per listed row: what k_csd_scan found (32 B)
-struct CsdRow {
-    uint32_t ecnt;       // exception entries
-    int32_t smin, smax;  // shift range of the clean blocks
-    uint32_t phmask;     // phases (-s mod 20) of the clean blocks
-    uint32_t flags;      // nonzero: the delta path does not hash this row
-    uint32_t a0, b0, c0; // the string's first three words
-};
-// flags
-constexpr uint32_t CSD_F_SHORT = 1, CSD_F_ECAP = 2, CSD_F_PLAN = 4, CSD_F_BATCH = 8, CSD_F_SLOTS = 16, CSD_F_JUMPS = 32,
-                   CSD_F_WIN = 64, CSD_NFLAGS = 7;
-
-struct CsdArgs {
-    const uint32_t *B;        // [NP] reference words
-    const uint32_t *OB;       // [N+1] reference record offsets, OB[N] = |S_B|
-    const uint32_t *SBw;      // S_B as little-endian words, zero padded (sbw_words of them)
-    uint32_t sbw_words;
-    uint4 *ent;               // [rows][ecap] exception entries, 2 uint4 each: {k, s_after, Mg, D}, {Mf, PF, Mh, KH}
-    CsdRow *rinfo;            // [rows]
-    uint32_t ecap;
-    uint32_t *fb_list, *fb_cnt; // rows left to the production kernels; fb_cnt[1 + b]: rows with flag bit b
-    uint32_t dmode;           // diagnostics library only (swimsim_bench_checksum modes 31..46 = dmode + 30, garbage
-                              // checksums): 1 helpers alone, 2 chains alone, 3 helpers without the exception work; bit 8:
-                              // no barrier between super steps. Ignored by the product library (CSD_DMODE)
-};
-
-// the diagnostic split modes exist only in the diagnostics library (tools/libswimsim_diag.so); in the product
-// library the mode is the constant 0 and its branches compile away
-#ifdef SWIMSIM_DIAG
-#define CSD_DMODE(a) ((a).dmode)
-#else
-#define CSD_DMODE(a) 0u
-#endif
-
-__device__ __forceinline__ const uint32_t *csd_row(const DS &d, uint32_t id) {
-    return id < d.NL ? d.mw + (size_t)id * d.NP : d.dense + (size_t)(id - d.NL) * d.NP;
-}
-__device__ __forceinline__ uint32_t csd_len(const DS &d, uint32_t id) {
-    return id < d.NL ? d.clen[id] : d.dense_len[id - d.NL];
-}
-__device__ __forceinline__ uint32_t csd_reclen(const DS &d, uint32_t w) { return (uint32_t)reclen(d, w & 7u, w >> 3); }
-// rows equal at member m in the checksum string: the same word, or a record in neither
-__device__ __forceinline__ bool csd_same(uint32_t a, uint32_t b) { return a == b || ((a & 7u) >= 4u && (b & 7u) >= 4u); }
-__device__ __forceinline__ uint32_t csd_phase(int32_t s) { return (uint32_t)(((-s) % 20 + 20) % 20); }
-__device__ __forceinline__ int32_t csd_floordiv20(int32_t x) { return x >= 0 ? x / 20 : -((-x + 19) / 20); }
-
-__device__ __forceinline__ void csd_premix(uint32_t a, uint32_t b, uint32_t c, uint32_t dd, uint32_t e, uint32_t an,
-                                           uint32_t bn, uint32_t cn, uint32_t (&v)[6]) {
-    v[0] = fh_m(c);
-    v[1] = CSD_C + a + bn - cn;
-    v[2] = fh_m(b + e * FH_C1);
-    v[3] = 2u * CSD_C + a + dd + cn;
-    v[4] = fh_m(dd);
-    v[5] = CSD_C + e + an;
-}
-
-__global__ void k_ctr_add(DS d, int c, unsigned long long v) { ctr_add(d, c, v); }
-
-// ---------------------------------------------------------------------------------------------------------------
-// reference row and reference string
-// ---------------------------------------------------------------------------------------------------------------
-__global__ void k_csd_ref(DS d, const uint32_t *list, uint32_t n, uint32_t *B, uint32_t *Lb) {
-    const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
-    if (m > d.N) return;
-    if (m == d.N) { Lb[m] = 0; return; }
-    const uint32_t S = min(n, 31u);
-    uint32_t cand = 0, c = 0;
-    for (uint32_t s = 0; s < S; s++) {
-        const uint32_t id = list[(uint32_t)(((uint64_t)s * n) / S)];
-        const uint32_t w = csd_row(d, id)[m];
-        if (c == 0) { cand = w; c = 1; }
-        else c += w == cand ? 1u : 0xFFFFFFFFu;
-    }
-    B[m] = cand;
-    Lb[m] = csd_reclen(d, cand);
-}
-
-// the launch's mean distance from B, on CSD_NSAMPLE rows sampled evenly from the list: differing members counted
-// into *out (one workgroup per sampled row). Decides whether the reference-row path pays for this launch.
-constexpr uint32_t CSD_NSAMPLE = 64;
-__global__ void __launch_bounds__(256) k_csd_sample(DS d, const uint32_t *list, uint32_t n, const uint32_t *B, uint32_t *out) {
-    const uint32_t id = list[(uint32_t)(((uint64_t)blockIdx.x * n) / CSD_NSAMPLE)];
-    const uint32_t *row = csd_row(d, id);
-    uint32_t c = 0;
-    for (uint32_t m = threadIdx.x; m < d.N; m += 256u) c += csd_same(row[m], B[m]) ? 0u : 1u;
-    for (int off = 32; off > 0; off >>= 1) c += (uint32_t)__shfl_xor((int)c, off, 64);
-    if ((threadIdx.x & 63u) == 0 && c) atomicAdd(out, c);
-}
-
-template <int W>
-__global__ void k_csd_string(DS d, const uint32_t *B, const uint32_t *OB, uint8_t *SB) {
-    const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
-    if (m >= d.N) return;
-    uint32_t R[CS_RW];
-    const uint32_t L = record<W>(d, m, B[m], R);
-    uint8_t *o = SB + OB[m];
-    for (uint32_t b = 0; b < L; b++) {
-        uint32_t w = 0;
-#pragma unroll
-        for (int i = 0; i < CS_RW; i++) w = (b >> 2) == (uint32_t)i ? R[i] : w;
-        o[b] = (uint8_t)(w >> (8u * (b & 3u)));
-    }
-}
-
-// ---------------------------------------------------------------------------------------------------------------
-// k_csd_scan: one wave per row
-// ---------------------------------------------------------------------------------------------------------------
-// premixed entries of blocks klo..khi of one row (one lane): the row's string from byte 20 klo, which is byte o0 of
-// member m0's record, as a word stream through a window of 8 words. Block j of the run is words [5j, 5j + 8) of the
-// stream (words [5j, 5j + 5) and a zero look-ahead for the row's last block kl).
-template <int W>
-__device__ void csd_run_entries(const DS &d, const uint32_t *row, uint32_t m0, uint32_t o0, uint32_t klo, uint32_t khi,
-                                uint32_t kl, int32_t s_after, uint4 *out, CsdRow *ri) {
-    const uint32_t N = d.N;
-    const uint32_t nbk = khi - klo + 1;
-    const bool tail0 = khi == kl;
-    uint32_t win[8] = {0, 0, 0, 0, 0, 0, 0, 0}, nw = 0, done = 0;
-    uint32_t ready = (nbk == 1 && tail0) ? 5u : 8u;                 // stream words block `done` needs
-    uint64_t acc = 0;
-    uint32_t nacc = 0;
-    auto push = [&](uint32_t w) {
-#pragma unroll
-        for (int q = 0; q < 7; q++) win[q] = win[q + 1];
-        win[7] = w;
-        nw++;
-        if (done < nbk && nw == ready) {
-            const bool z = tail0 && done == nbk - 1;               // words a..e at win[0..4], or win[3..7]
-            const uint32_t wa = z ? win[3] : win[0], wb = z ? win[4] : win[1], wc = z ? win[5] : win[2],
-                           wd = z ? win[6] : win[3], we = z ? win[7] : win[4];
-            uint32_t v[6];
-            csd_premix(wa, wb, wc, wd, we, z ? 0u : win[5], z ? 0u : win[6], z ? 0u : win[7], v);
-            out[2 * done] = make_uint4(klo + done, (uint32_t)s_after, v[0], v[1]);
-            out[2 * done + 1] = make_uint4(v[2], v[3], v[4], v[5]);
-            if (klo + done == 0) { ri->a0 = wa; ri->b0 = wb; ri->c0 = wc; }
-            done++;
-            ready = (tail0 && done == nbk - 1) ? 5u * done + 5u : 5u * done + 8u;
-        }
-    };
-    uint32_t m = m0, o = o0;
-    while (done < nbk) {
-        if (m < N) {
-            uint32_t R[CS_RW];
-            const uint32_t L = record<W>(d, m, row[m], R);
-#pragma unroll
-            for (int i = 0; i < CS_RW; i++) {
-                const uint32_t lo = max(o, 4u * i), hi = min(L, 4u * i + 4u);
-                if (hi > lo) {
-                    const uint32_t nb = hi - lo;
-                    const uint32_t v = R[i] >> (8u * (lo - 4u * i));
-                    const uint32_t vm = nb == 4 ? v : (v & ((1u << (8u * nb)) - 1u));
-                    acc |= (uint64_t)vm << (8u * nacc);
-                    nacc += nb;
-                    if (nacc >= 4) {
-                        push((uint32_t)acc);
-                        acc >>= 32;
-                        nacc -= 4;
-                    }
-                }
-            }
-        } else {                                                    // past the last member: zero bytes
-            push((uint32_t)acc);
-            acc = 0;
-            nacc = 0;
-        }
-        m++;
-        o = 0;
-    }
-}
-
-template <int W>
-__global__ void __launch_bounds__(256) k_csd_scan(DS d, const uint32_t *list, uint32_t n, CsdArgs a) {
-    // CSD_SU chunks of 64 members per pass, their loads in flight together (a row is one 256-KB stream). Chunks with
-    // differing members are staged in LDS, and the pass's diffs are walked by a loop that is not unrolled; runs wait
-    // in LDS for their entries, generated (one lane per run) between passes.
-    constexpr uint32_t CSD_SU = 8, RUNCAP = 128, RUNFLUSH = 64;
-    __shared__ uint32_t runs[4][RUNCAP][6];                         // {klo, khi, m0, o0, s_after, first entry}
-    __shared__ uint32_t stw[4][CSD_SU][64];                         // staged row words of a pass
-    __shared__ uint64_t stm[4][CSD_SU];                             // their diff masks
-    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-    const uint32_t i = blockIdx.x * 4 + wv;
-    if (i >= n) return;
-    const uint32_t id = list[i];
-    const uint32_t *row = csd_row(d, id);
-    CsdRow *ri = a.rinfo + i;
-    uint4 *ent = a.ent + (size_t)i * a.ecap * 2;
-    const uint32_t len = csd_len(d, id);
-    const uint32_t N = d.N;
-    if (len <= 24) {                                                // FarmHash's short-string paths: not ours
-        if (lane == 0) { ri->ecnt = 0; ri->flags = CSD_F_SHORT; ri->smin = 0; ri->smax = 0; ri->phmask = 1; }
-        return;
-    }
-    const uint32_t kl = (len - 1) / 20 - 1;                         // the row's last chain block
-    int32_t s = 0;                                                  // row offset - B offset of the clean bytes here
-    uint32_t rlo = 0, rhi = 0, rm0 = 0, ro0 = 0;                    // the open run (block 0 always begins one)
-    uint32_t nruns = 0, e = 0, flags = 0, phm = 0;
-    int32_t smin = 0x7FFFFFFF, smax = -0x7FFFFFFF - 1;
-    auto wsync = [&]() {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    };
-    auto flush = [&]() {
-        wsync();
-        for (uint32_t q0 = 0; q0 < nruns; q0 += 64) {
-            if (q0 + lane < nruns) {
-                const uint32_t *q = runs[wv][q0 + lane];
-                csd_run_entries<W>(d, row, q[2], q[3], q[0], q[1], kl, (int32_t)q[4], ent + 2 * q[5], ri);
-            }
-        }
-        wsync();
-        nruns = 0;
-    };
-    auto close_run = [&](int32_t s_after) {
-        const uint32_t nb = rhi - rlo + 1;
-        if (e + nb > a.ecap || nruns == RUNCAP) { flags |= CSD_F_ECAP; return; }
-        if (lane == 0) {
-            uint32_t *q = runs[wv][nruns];
-            q[0] = rlo; q[1] = rhi; q[2] = rm0; q[3] = ro0; q[4] = (uint32_t)s_after; q[5] = e;
-        }
-        if (rhi < kl) {                                             // clean blocks follow at this shift
-            smin = min(smin, s_after);
-            smax = max(smax, s_after);
-            phm |= 1u << csd_phase(s_after);
-        }
-        e += nb;
-        nruns++;
-    };
-    auto diff = [&](uint32_t mm, uint32_t wm, uint32_t bm) {
-        const int32_t Lr = (int32_t)csd_reclen(d, wm), Lbm = (int32_t)csd_reclen(d, bm);
-        const int32_t x = (int32_t)a.OB[mm] + s, y = x + Lr;        // the record's bytes in the row: [x, y)
-        // blocks whose 32 bytes [20k, 20k + 32) meet [x, y) (or straddle x when the record is empty)
-        const int32_t klo = x >= 32 ? (x - 32) / 20 + 1 : 0;
-        int32_t khi = y >= 1 ? (y - 1) / 20 : -1;
-        if (khi > (int32_t)kl) khi = (int32_t)kl;
-        if (klo <= (int32_t)kl && khi >= klo) {
-            if ((uint32_t)klo <= rhi + 1) {
-                rhi = max(rhi, (uint32_t)khi);
-            } else {
-                close_run(s);
-                // the new run starts at row byte p = 20 klo, in the clean bytes before mm (shift s): the record
-                // holding B offset t = p - s is the last member below mm with O_B <= t
-                const uint32_t t = (uint32_t)(20 * klo - s);
-                uint32_t m0 = mm - 1;
-                while (m0 > 0 && a.OB[m0] > t) m0--;
-                rlo = (uint32_t)klo; rhi = (uint32_t)khi; rm0 = m0; ro0 = t - a.OB[m0];
-            }
-        }
-        s += Lr - Lbm;
-    };
-    for (uint32_t c00 = 0; c00 < N && !flags; c00 += 64 * CSD_SU) {
-        uint32_t wv_[CSD_SU], bv_[CSD_SU];
-#pragma unroll
-        for (uint32_t k = 0; k < CSD_SU; k++) {
-            const uint32_t m = c00 + 64 * k + lane;
-            wv_[k] = m < N ? row[m] : 0u;
-            bv_[k] = m < N ? a.B[m] : 0u;
-        }
-        uint32_t any = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < CSD_SU; k++) {
-            const uint64_t mk = __ballot(c00 + 64 * k + lane < N && !csd_same(wv_[k], bv_[k]));
-            if (mk) stw[wv][k][lane] = wv_[k];
-            if (lane == 0) stm[wv][k] = mk;
-            any |= mk ? 1u : 0u;
-        }
-        if (!any) continue;
-        wsync();
-        for (uint32_t k = 0; k < CSD_SU && !flags; k++) {
-            uint64_t mask = stm[wv][k];
-            while (mask && !flags) {                                // the chunk's differing members, in order
-                const uint32_t l = (uint32_t)__builtin_ctzll(mask);
-                mask &= mask - 1;
-                const uint32_t mm = c00 + 64 * k + l;
-                diff(mm, stw[wv][k][l], a.B[mm]);
-            }
-        }
-        wsync();
-        if (nruns >= RUNFLUSH) flush();
-    }
-    if (!flags) {
-        if (rhi + 1 >= kl) {
-            rhi = kl;
-        } else {                                                    // the last block: a run of its own
-            close_run(s);
-            const uint32_t t = (uint32_t)(20 * (int32_t)kl - s);
-            uint32_t m0 = N - 1;
-            while (m0 > 0 && a.OB[m0] > t) m0--;
-            rlo = kl; rhi = kl; rm0 = m0; ro0 = t - a.OB[m0];
-        }
-        close_run(s);
-    }
-    if (!flags && nruns) flush();
-    if (lane == 0) {
-        ri->ecnt = e;
-        ri->flags = flags;
-        ri->smin = phm ? smin : 0;
-        ri->smax = phm ? smax : 0;
-        ri->phmask = phm ? phm : 1u;
-    }
-}
-
-// ---------------------------------------------------------------------------------------------------------------
-// k_cs_delta: the chains
-// ---------------------------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t csd_alignbyte(uint32_t hi, uint32_t lo, uint32_t sh) {
-    return __builtin_amdgcn_alignbyte(hi, lo, sh);
-}
-
-// one block of the coupled g and f lanes in carried-sum form, the two lanes' instructions interleaved (a wave issues in
-// order: each of a pair's dependent successors then waits one instruction less)
-__device__ __forceinline__ void csd_gf_step(uint32_t &Xg, uint32_t &Xf, uint32_t mg, uint32_t dd, uint32_t mf, uint32_t pf) {
-    uint32_t tg, tf;
-    asm volatile("v_xor_b32 %2, %0, %4\n\t"
-                 "v_xor_b32 %3, %1, %6\n\t"
-                 "v_alignbit_b32 %2, %2, %2, 19\n\t"
-                 "v_alignbit_b32 %3, %3, %3, 19\n\t"
-                 "v_lshl_add_u32 %2, %2, 2, %2\n\t"
-                 "v_lshl_add_u32 %3, %3, 2, %3\n\t"
-                 "v_add3_u32 %1, %3, %2, %7\n\t"
-                 "v_add3_u32 %0, %2, %1, %5"
-                 : "+v"(Xg), "+v"(Xf), "=&v"(tg), "=&v"(tf)
-                 : "v"(mg), "v"(dd), "v"(mf), "v"(pf));
-}
-// one block of the h lane: Xh' = 5 ror(Xh ^ Mh, 19) + KH
-__device__ __forceinline__ void csd_h_step(uint32_t &Xh, uint32_t mh, uint32_t kh) {
-    asm volatile("v_xor_b32 %0, %0, %1\n\t"
-                 "v_alignbit_b32 %0, %0, %0, 19\n\t"
-                 "v_lshl_add_u32 %0, %0, 2, %0\n\t"
-                 "v_add_u32 %0, %0, %2"
-                 : "+v"(Xh)
-                 : "v"(mh), "v"(kh));
-}
 
 template <int W, int G>
 __global__ void __launch_bounds__(CsdGeo<G>::THREADS) k_cs_delta(DS d, const uint32_t *list, const uint32_t *count, CsdArgs a) {
