@@ -31,6 +31,7 @@ constexpr int CSR_EXW = 128;           // exception entries per wave per buffer
 constexpr int CSR_ENT = CSR_WINMAX + 4 * CSR_EXW;   // entries per buffer
 constexpr int CSR_TBLW = 18;           // u32 words per row of the code table (32 u16 codes + pad: b64 reads conflict-free)
 constexpr int CSR_EREG = 4;            // exception entries of a record prefetched with it
+constexpr int CSR_PF = 4;              // blocks the chain's LDS reads run ahead of its arithmetic
 constexpr uint32_t CSR_EXC = 0x8000u;  // code flag: exception entry (low bits: ordinal in the super step)
 constexpr uint32_t CSR_F_PLAN = 128, CSR_F_SLOTS = 256, CSR_F_RCAP = 512;   // flags beyond k_csd_scan's
 
@@ -117,7 +118,7 @@ __global__ void __launch_bounds__(CSR_ROWS) k_csr_plan(DS d, const uint32_t *lis
         uint32_t phm = ph;
         if (phm == 0) { phm = 1; smin = 0; smax = 0; }
         p.cmax = csr_ceil20(smax);
-        p.Wn = (uint32_t)(CSR_SB + (p.cmax - csr_ceil20(smin)) + 1);
+        p.Wn = ((uint32_t)(CSR_SB + (p.cmax - csr_ceil20(smin)) + 1) + 30u) / 32u * 32u + 1u;   // = 1 mod 32 (k_csr)
         p.phm = phm;
         p.nph = (uint32_t)__popc(phm);
         p.maxit = mi;
@@ -126,9 +127,14 @@ __global__ void __launch_bounds__(CSR_ROWS) k_csr_plan(DS d, const uint32_t *lis
     }
 }
 
-// records of one row (one thread per listed row): its exception entries grouped by super step
-__global__ void k_csr_rec(DS d, const uint32_t *list, uint32_t n, CsrArgs a) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+// records of one row per wave (4 rows per workgroup): the row's entries in chunks of 64 (lane q holds entry c0 + q's
+// block and shift, staged in LDS), and every lane that begins a super step's group of entries builds that group's
+// record. A group that runs past the chunk's end is left to the next chunk, which starts at its first entry (a group
+// holds at most CSR_SB entries, so every chunk completes at least one group).
+__global__ void __launch_bounds__(256) k_csr_rec(DS d, const uint32_t *list, uint32_t n, CsrArgs a) {
+    __shared__ uint2 hd[4][64];
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t i = blockIdx.x * 4 + wv;
     if (i >= n) return;
     const CsdRow ri = a.rinfo[i];
     const CsrPlan p = a.plan[i / CSR_ROWS];
@@ -138,38 +144,65 @@ __global__ void k_csr_rec(DS d, const uint32_t *list, uint32_t n, CsrArgs a) {
         const uint32_t iters = len > 24 ? (len - 1) / 20 : 0u;
         const uint4 *ent = a.ent + (size_t)i * a.ecap * 2;
         CsrRec *rec = a.rec + (size_t)i * a.rcap;
-        int32_t s = 0;
-        uint32_t e = 0;
-        while (e < ri.ecnt) {
-            const uint32_t k0 = ent[2 * e].x;
-            const uint32_t t = k0 / CSR_SB, K0 = t * CSR_SB;
-            if (nr == a.rcap) { nr = 0xFFFFFFFFu; break; }
-            CsrRec r;
-            r.t = t;
-            r.e0 = e;
-            uint32_t ne = 0;
-            uint32_t kn = k0;                                       // block of entry e + ne
-            for (uint32_t q = 0; q < (uint32_t)CSR_SB; q++) {
-                const uint32_t j = K0 + q;
-                uint32_t c;
-                if (e + ne < ri.ecnt && kn == j) {
-                    c = CSR_EXC | ne;
-                    s = (int32_t)ent[2 * (e + ne)].y;
-                    ne++;
-                    kn = e + ne < ri.ecnt ? ent[2 * (e + ne)].x : 0xFFFFFFFFu;
-                } else {
-                    c = j < iters ? csr_base(p, s) + q : 0u;
+        int32_t s_prev = 0;                                          // the shift before entry c0
+        uint32_t c0 = 0;
+        while (c0 < ri.ecnt) {
+            const uint32_t nin = min(64u, ri.ecnt - c0);
+            const bool in = lane < nin;
+            const uint2 h = in ? *(const uint2 *)(ent + 2 * (c0 + lane)) : make_uint2(0xFFFFFFFFu, 0u);   // {k, s after}
+            hd[wv][lane] = h;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const uint32_t t = h.x / CSR_SB;
+            const bool head = in && (lane == 0 || hd[wv][lane - 1].x / CSR_SB != t);
+            const uint64_t heads = __ballot(head);
+            const uint64_t after = lane < 63 ? heads & ~((2ull << lane) - 1ull) : 0ull;
+            const uint32_t gend = after ? (uint32_t)__builtin_ctzll(after) : nin;   // one past the group's last entry
+            const bool complete = after != 0 || c0 + nin == ri.ecnt;
+            const bool build = head && complete;
+            const uint64_t built = __ballot(build);
+            if (build) {
+                const uint32_t slot = nr + (uint32_t)__popcll(built & ((1ull << lane) - 1ull));
+                if (slot < a.rcap) {
+                    CsrRec r;
+                    int32_t s = lane ? (int32_t)hd[wv][lane - 1].y : s_prev;
+                    const uint32_t K0 = t * CSR_SB;
+                    uint32_t q = lane, kn = h.x;
+                    for (uint32_t b = 0; b < (uint32_t)CSR_SB; b++) {
+                        const uint32_t j = K0 + b;
+                        uint32_t c;
+                        if (q < gend && kn == j) {
+                            c = CSR_EXC | (q - lane);
+                            s = (int32_t)hd[wv][q].y;
+                            q++;
+                            kn = q < gend ? hd[wv][q].x : 0xFFFFFFFFu;
+                        } else {
+                            c = j < iters ? csr_base(p, s) + b : 0u;
+                        }
+                        if (b & 1u) r.code[b >> 1] |= c << 16;
+                        else r.code[b >> 1] = c;
+                    }
+                    r.t = t;
+                    r.s_end = s;
+                    r.e0 = c0 + lane;
+                    r.ne = gend - lane;
+                    rec[slot] = r;
                 }
-                if (q & 1u) r.code[q >> 1] |= c << 16;
-                else r.code[q >> 1] = c;
             }
-            r.s_end = s;
-            r.ne = ne;
-            rec[nr++] = r;
-            e += ne;
+            nr += (uint32_t)__popcll(built);
+            // the next chunk begins at the first group left incomplete
+            const uint64_t open = heads & ~built;
+            const uint32_t adv = open ? (uint32_t)__builtin_ctzll(open) : nin;
+            s_prev = adv ? (int32_t)hd[wv][adv - 1].y : s_prev;
+            c0 += adv;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
+        if (nr > a.rcap) nr = 0xFFFFFFFFu;
     }
-    a.nrec[i] = nr;
+    if (lane == 0) a.nrec[i] = nr;
 }
 
 // one block of the coupled g and f lanes and of the h lane in carried-sum form (swimsim_checksum_ref.hip)
@@ -180,7 +213,12 @@ __device__ __forceinline__ void csr_block(uint32_t &Xg, uint32_t &Xf, uint32_t &
 
 template <int W>
 __global__ void __launch_bounds__(CSR_ROWS) k_csr(DS d, const uint32_t *list, const uint32_t *count, CsrArgs a) {
-    __shared__ uint4 E[2][CSR_ENT * 2];                 // per buffer: window entries, then each wave's exception entries
+    // per buffer: window entries, then each wave's exception entries, split into {Mg, D} (EA) and {Mf, PF, Mh, KH} (EB):
+    // a lane reads EA[e] (8 B) and EB[e] (16 B). With Wn = 1 mod 32 the entries of the different phases that the rows of
+    // a wave read at one block fall into different LDS banks (a 32-B entry put every entry's halves on the same 8 of 16
+    // 16-B slots: 2.4e9 bank-conflict cycles per launch, half the kernel's time)
+    __shared__ uint2 EA[2][CSR_ENT];
+    __shared__ uint4 EB[2][CSR_ENT];
     __shared__ uint2 T[2][CSR_ROWS * CSR_TBLW / 2];     // per buffer: each row's 32 codes (tables of record super steps)
     __shared__ uint32_t phs[20];
     const uint32_t cnt = *count;
@@ -200,6 +238,7 @@ __global__ void __launch_bounds__(CSR_ROWS) k_csr(DS d, const uint32_t *list, co
     uint32_t fl = !valid ? 0u : ri.flags ? ri.flags : !p.feasible ? CSR_F_PLAN : nrec == 0xFFFFFFFFu ? CSR_F_RCAP : 0u;
     if (valid && !fl && iters == 0) fl = CSD_F_SHORT;
     if (tid < 20 && ((p.phm >> tid) & 1u)) phs[__popc(p.phm & ((1u << tid) - 1u))] = tid;   // phase slot -> phase
+    __syncthreads();
     const bool live = valid && fl == 0;
     const uint32_t myit = live ? iters : 0u;
     const uint32_t T_ = p.feasible ? (p.maxit + CSR_SB - 1) / CSR_SB : 0u;
@@ -233,32 +272,39 @@ __global__ void __launch_bounds__(CSR_ROWS) k_csr(DS d, const uint32_t *list, co
 
     // window staging: entries u = tid + 256 v of the next super step's window, through registers
     constexpr int WV = CSR_WINMAX / CSR_ROWS;
-    uint4 wst[WV][2];
+    // two staging sets: super step u's window goes through set u & 1, loaded two super steps ahead (the window rows of
+    // P miss in L2 at their first touch: one HBM round trip, longer than a super step's chain)
+    uint4 wA[WV][2], wB[WV][2];
     const uint32_t nwin = p.nph * p.Wn;
-    auto wload = [&](uint32_t t) {
+    // (each thread's window entries keep their phase and position from super step to super step: their source rows
+    // in P are fixed, the S_B block advances by CSR_SB)
+    const uint4 *wsrc[WV];
+    int32_t wk0[WV];
+#pragma unroll
+    for (int v = 0; v < WV; v++) {
+        const uint32_t u = tid + (uint32_t)CSR_ROWS * v;
+        const uint32_t ps = u < nwin ? u / p.Wn : 0u, w = u < nwin ? u - ps * p.Wn : 0u;
+        wsrc[v] = a.P + 2 * (size_t)phs[min(ps, 19u)] * a.KP;
+        wk0[v] = u < nwin ? (int32_t)w - p.cmax : 0x40000000;
+    }
+    auto wload = [&](uint4 (&wst)[WV][2], uint32_t t) {
 #pragma unroll
         for (int v = 0; v < WV; v++) {
-            const uint32_t u = tid + (uint32_t)CSR_ROWS * v;
-            wst[v][0] = make_uint4(0, 0, 0, 0);
-            wst[v][1] = make_uint4(0, 0, 0, 0);
-            if (u < nwin) {
-                const uint32_t ps = u / p.Wn, w = u - ps * p.Wn;
-                const int32_t k = (int32_t)(t * CSR_SB) - p.cmax + (int32_t)w;
-                if (k >= 0 && (uint32_t)k < a.KP) {
-                    const uint4 *src = a.P + 2 * ((size_t)phs[ps] * a.KP + (uint32_t)k);
-                    wst[v][0] = src[0];
-                    wst[v][1] = src[1];
-                }
-            }
+            const int32_t k = wk0[v] + (int32_t)(t * CSR_SB);
+            const bool in = k >= 0 && (uint32_t)k < a.KP;
+            const uint4 *src = wsrc[v] + 2 * (in ? (uint32_t)k : 0u);
+            const uint4 x0 = src[0], x1 = src[1];
+            wst[v][0] = in ? x0 : make_uint4(0, 0, 0, 0);
+            wst[v][1] = in ? x1 : make_uint4(0, 0, 0, 0);
         }
     };
-    auto wstore = [&](uint32_t b) {
+    auto wstore = [&](const uint4 (&wst)[WV][2], uint32_t b) {
 #pragma unroll
         for (int v = 0; v < WV; v++) {
             const uint32_t u = tid + (uint32_t)CSR_ROWS * v;
             if (u < nwin) {
-                E[b][2 * u] = wst[v][0];
-                E[b][2 * u + 1] = wst[v][1];
+                EA[b][u] = make_uint2(wst[v][0].z, wst[v][0].w);
+                EB[b][u] = wst[v][1];
             }
         }
     };
@@ -287,14 +333,16 @@ __global__ void __launch_bounds__(CSR_ROWS) k_csr(DS d, const uint32_t *list, co
                 tr[q] = make_uint2(lo0 | (hi0 << 16), lo1 | (hi1 << 16));
             }
             if (!(fl & CSR_F_SLOTS)) {
-                uint4 *xe = E[b] + 2 * xb;
-                if (ne > 0) { xe[0] = RE0a; xe[1] = RE0b; }
-                if (ne > 1) { xe[2] = RE1a; xe[3] = RE1b; }
-                if (ne > 2) { xe[4] = RE2a; xe[5] = RE2b; }
-                if (ne > 3) { xe[6] = RE3a; xe[7] = RE3b; }
+                uint2 *xa = EA[b] + xb;
+                uint4 *xf = EB[b] + xb;
+                if (ne > 0) { xa[0] = make_uint2(RE0a.z, RE0a.w); xf[0] = RE0b; }
+                if (ne > 1) { xa[1] = make_uint2(RE1a.z, RE1a.w); xf[1] = RE1b; }
+                if (ne > 2) { xa[2] = make_uint2(RE2a.z, RE2a.w); xf[2] = RE2b; }
+                if (ne > 3) { xa[3] = make_uint2(RE3a.z, RE3a.w); xf[3] = RE3b; }
                 for (uint32_t k = CSR_EREG; k < ne; k++) {          // more than CSR_EREG: synchronous loads (rare)
-                    E[b][2 * (xb + k)] = ent[2 * (R.e0 + k)];
-                    E[b][2 * (xb + k) + 1] = ent[2 * (R.e0 + k) + 1];
+                    const uint4 x0 = ent[2 * (R.e0 + k)];
+                    EA[b][xb + k] = make_uint2(x0.z, x0.w);
+                    EB[b][xb + k] = ent[2 * (R.e0 + k) + 1];
                 }
             }
             s = R.s_end;
@@ -309,48 +357,77 @@ __global__ void __launch_bounds__(CSR_ROWS) k_csr(DS d, const uint32_t *list, co
     };
 
     // super step 0
-    wload(0);
-    wstore(0);
+    wload(wA, 0);
+    wstore(wA, 0);
+    if (T_ > 1) wload(wB, 1);
     bool tab = prep(0, 0);
     if (live && R.t == 0) { base = csr_base(p, s); rcur++; load_rec(rcur); }
     __syncthreads();
     for (uint32_t t = 0; t < T_; t++) {
         const uint32_t b = t & 1u, K0 = t * CSR_SB;
-        if (t + 1 < T_) wload(t + 1);
+        if (t + 2 < T_) {                                          // set t & 1 is free: super step t is in LDS
+            if (b) wload(wB, t + 2);
+            else wload(wA, t + 2);
+        }
         // ---- the chain over blocks K0 .. K0 + 31 ----
+        // The block loop is straight-line code per variant (FULL: every row's chain covers the whole super step, no
+        // predication; TAB: codes from the row's table instead of base + i), and each block's two LDS reads are
+        // issued CSR_PF blocks ahead of its arithmetic: a read followed at once by its use waits the whole LDS latency
+        // (about 120 cycles with four waves reading), twice the chain's own cost of a block.
         const bool full = __all(myit == 0u || K0 + CSR_SB <= myit);
-        const uint4 *EB = E[b];
-        auto step = [&](uint32_t i, uint32_t c) {
-            const uint4 *q = EB + 2 * c;
-            const uint4 x = q[0], y = q[1];
-            if (full) {
-                csr_block(Xg, Xf, Xh, make_uint2(x.z, x.w), y);
-            } else {
-                uint32_t ng = Xg, nf = Xf, nh = Xh;
-                csr_block(ng, nf, nh, make_uint2(x.z, x.w), y);
-                const bool act = K0 + i < myit;
-                Xg = act ? ng : Xg;
-                Xf = act ? nf : Xf;
-                Xh = act ? nh : Xh;
+        const uint2 *EAb = EA[b];
+        const uint4 *EBb = EB[b];
+        auto run = [&](auto FULLC, auto TABC) {
+            constexpr bool FULL = decltype(FULLC)::value;
+            constexpr bool TAB = decltype(TABC)::value;
+            uint32_t code[CSR_SB];
+            if (TAB) {
+                const uint2 *tr = T[b] + (size_t)tid * (CSR_TBLW / 2);
+#pragma unroll
+                for (int q = 0; q < 8; q++) {
+                    const uint2 cc = tr[q];
+                    code[4 * q + 0] = cc.x & 0xFFFFu;
+                    code[4 * q + 1] = cc.x >> 16;
+                    code[4 * q + 2] = cc.y & 0xFFFFu;
+                    code[4 * q + 3] = cc.y >> 16;
+                }
+            }
+            uint2 vg[CSR_PF + 1];
+            uint4 vf[CSR_PF + 1];
+            auto fetch = [&](int i) {
+                const uint32_t e = TAB ? code[i] : base + (uint32_t)i;
+                vg[i % (CSR_PF + 1)] = EAb[e];
+                vf[i % (CSR_PF + 1)] = EBb[e];
+            };
+#pragma unroll
+            for (int i = 0; i < CSR_PF; i++) fetch(i);
+#pragma unroll
+            for (int i = 0; i < CSR_SB; i++) {
+                if (i + CSR_PF < CSR_SB) fetch(i + CSR_PF);
+                const uint2 g = vg[i % (CSR_PF + 1)];
+                const uint4 f = vf[i % (CSR_PF + 1)];
+                if (FULL) {
+                    csr_block(Xg, Xf, Xh, g, f);
+                } else {
+                    uint32_t ng = Xg, nf = Xf, nh = Xh;
+                    csr_block(ng, nf, nh, g, f);
+                    const bool act = K0 + (uint32_t)i < myit;
+                    Xg = act ? ng : Xg;
+                    Xf = act ? nf : Xf;
+                    Xh = act ? nh : Xh;
+                }
             }
         };
-        if (!tab) {
-#pragma unroll
-            for (uint32_t i = 0; i < (uint32_t)CSR_SB; i++) step(i, base + i);
-        } else {
-            const uint2 *tr = T[b] + (size_t)tid * (CSR_TBLW / 2);
-#pragma unroll
-            for (int q = 0; q < 8; q++) {
-                const uint2 cc = tr[q];
-                step(4 * q + 0, cc.x & 0xFFFFu);
-                step(4 * q + 1, cc.x >> 16);
-                step(4 * q + 2, cc.y & 0xFFFFu);
-                step(4 * q + 3, cc.y >> 16);
-            }
-        }
+        using TT = std::integral_constant<bool, true>;
+        using FF = std::integral_constant<bool, false>;
+        if (full && !tab) run(TT{}, FF{});
+        else if (full) run(TT{}, TT{});
+        else if (!tab) run(FF{}, FF{});
+        else run(FF{}, TT{});
         // ---- the next super step's window, rows and entries into the other buffer ----
         if (t + 1 < T_) {
-            wstore(b ^ 1u);
+            if (b) wstore(wA, 0u);                                  // super step t + 1 (even) -> buffer 0
+            else wstore(wB, 1u);
             tab = prep(t + 1, b ^ 1u);
             if (live && R.t == t + 1) { base = csr_base(p, s); rcur++; load_rec(rcur); }
         }
@@ -388,7 +465,7 @@ void launch_csr_w(const DS &d, const uint32_t *list, uint32_t n, const uint32_t 
         hipLaunchKernelGGL((k_csd_scan<W>), dim3((n + 3) / 4), dim3(256), 0, s, d, list, n, ca);
     } else if (part == 3) {
         hipLaunchKernelGGL(k_csr_plan, dim3((n + CSR_ROWS - 1) / CSR_ROWS), dim3(CSR_ROWS), 0, s, d, list, n, a);
-        hipLaunchKernelGGL(k_csr_rec, dim3((n + 255) / 256), dim3(256), 0, s, d, list, n, a);
+        hipLaunchKernelGGL(k_csr_rec, dim3((n + 3) / 4), dim3(256), 0, s, d, list, n, a);
     } else {
         hipLaunchKernelGGL((k_csr<W>), dim3((n + CSR_ROWS - 1) / CSR_ROWS), dim3(CSR_ROWS), 0, s, d, list, count, a);
     }

@@ -47,6 +47,8 @@ struct CsdArgs {
     CsdRow *rinfo;            // [rows]
     uint32_t ecap;
     uint32_t *fb_list, *fb_cnt; // rows left to the production kernels; fb_cnt[1 + b]: rows with flag bit b
+    const uint32_t *ulist;    // divergent columns in member order (DS::colx), or null: k_csd_scan reads every column
+    const uint32_t *ucnt;     // their number
     uint32_t dmode;           // diagnostics library only (swimsim_bench_checksum modes 31..46 = dmode + 30, garbage
                               // checksums): 1 helpers alone, 2 chains alone, 3 helpers without the exception work; bit 8:
                               // no barrier between super steps. Ignored by the product library (CSD_DMODE)
@@ -113,6 +115,37 @@ __global__ void __launch_bounds__(256) k_csd_sample(DS d, const uint32_t *list, 
     for (uint32_t m = threadIdx.x; m < d.N; m += 256u) c += csd_same(row[m], B[m]) ? 0u : 1u;
     for (int off = 32; off > 0; off >>= 1) c += (uint32_t)__shfl_xor((int)c, off, 64);
     if ((threadIdx.x & 63u) == 0 && c) atomicAdd(out, c);
+}
+
+// the divergent columns in member order (one workgroup of 1024 threads: each thread a run of bitmap words, a block
+// prefix sum of their bit counts)
+__global__ void __launch_bounds__(1024) k_csr_ulist(DS d, uint32_t *ulist, uint32_t *ucnt) {
+    __shared__ uint32_t part[1024];
+    const uint32_t t = threadIdx.x, per = (d.NBIT + 1023) / 1024, w0 = t * per;
+    auto bitsof = [&](uint32_t w) -> uint32_t {                    // (bits of members >= N masked off)
+        const uint32_t x = d.colx[w], lo = w * 32;
+        return lo + 32 <= d.N ? x : lo >= d.N ? 0u : x & ((1u << (d.N - lo)) - 1u);
+    };
+    uint32_t c = 0;
+    for (uint32_t w = w0; w < min(w0 + per, d.NBIT); w++) c += (uint32_t)__popc(bitsof(w));
+    part[t] = c;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024; off <<= 1) {              // inclusive Hillis-Steele scan
+        const uint32_t v = t >= off ? part[t - off] : 0u;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint32_t at = part[t] - c;
+    for (uint32_t w = w0; w < min(w0 + per, d.NBIT); w++) {
+        uint32_t bits = bitsof(w);
+        while (bits) {
+            const uint32_t b = (uint32_t)__builtin_ctz(bits);
+            bits &= bits - 1;
+            ulist[at++] = w * 32 + b;
+        }
+    }
+    if (t == 1023) *ucnt = part[1023];
 }
 
 template <int W>
@@ -204,6 +237,7 @@ __global__ void __launch_bounds__(256) k_csd_scan(DS d, const uint32_t *list, ui
     __shared__ uint32_t runs[4][RUNCAP][6];                         // {klo, khi, m0, o0, s_after, first entry}
     __shared__ uint32_t stw[4][CSD_SU][64];                         // staged row words of a pass
     __shared__ uint64_t stm[4][CSD_SU];                             // their diff masks
+    __shared__ uint32_t stmem[4][CSD_SU][64];                       // their members
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
     const uint32_t i = blockIdx.x * 4 + wv;
     if (i >= n) return;
@@ -275,19 +309,26 @@ __global__ void __launch_bounds__(256) k_csd_scan(DS d, const uint32_t *list, ui
         }
         s += Lr - Lbm;
     };
-    for (uint32_t c00 = 0; c00 < N && !flags; c00 += 64 * CSD_SU) {
-        uint32_t wv_[CSD_SU], bv_[CSD_SU];
+    // the columns to compare: every member, or only the divergent columns (DS::colx: outside them every row, and
+    // every snapshot of a row, holds the same word, so it equals the majority B there) when they are few
+    const uint32_t ucnt = a.ulist ? *a.ucnt : N;
+    const bool UL = a.ulist && ucnt <= N / 4;
+    const uint32_t ncol = UL ? ucnt : N;
+    for (uint32_t c00 = 0; c00 < ncol && !flags; c00 += 64 * CSD_SU) {
+        uint32_t wv_[CSD_SU], bv_[CSD_SU], mv_[CSD_SU];
 #pragma unroll
         for (uint32_t k = 0; k < CSD_SU; k++) {
-            const uint32_t m = c00 + 64 * k + lane;
-            wv_[k] = m < N ? row[m] : 0u;
-            bv_[k] = m < N ? a.B[m] : 0u;
+            const uint32_t c = c00 + 64 * k + lane;
+            const uint32_t m = c < ncol ? (UL ? a.ulist[c] : c) : 0u;
+            mv_[k] = m;
+            wv_[k] = c < ncol ? row[m] : 0u;
+            bv_[k] = c < ncol ? a.B[m] : 0u;
         }
         uint32_t any = 0;
 #pragma unroll
         for (uint32_t k = 0; k < CSD_SU; k++) {
-            const uint64_t mk = __ballot(c00 + 64 * k + lane < N && !csd_same(wv_[k], bv_[k]));
-            if (mk) stw[wv][k][lane] = wv_[k];
+            const uint64_t mk = __ballot(c00 + 64 * k + lane < ncol && !csd_same(wv_[k], bv_[k]));
+            if (mk) { stw[wv][k][lane] = wv_[k]; stmem[wv][k][lane] = mv_[k]; }
             if (lane == 0) stm[wv][k] = mk;
             any |= mk ? 1u : 0u;
         }
@@ -298,7 +339,7 @@ __global__ void __launch_bounds__(256) k_csd_scan(DS d, const uint32_t *list, ui
             while (mask && !flags) {                                // the chunk's differing members, in order
                 const uint32_t l = (uint32_t)__builtin_ctzll(mask);
                 mask &= mask - 1;
-                const uint32_t mm = c00 + 64 * k + l;
+                const uint32_t mm = stmem[wv][k][l];
                 diff(mm, stw[wv][k][l], a.B[mm]);
             }
         }

@@ -133,6 +133,8 @@ struct DS {
     uint32_t *hlist;          // [HP] slot -> member
     uint32_t *hmw;            // [NL][HP]
     uint2 *hde;               // [NL][HP]
+    uint32_t *colx;           // [NBIT] columns in which rows may differ: every row-word write since the rows were last
+                              // known equal marks its member (the reference-row scan reads only these columns)
     uint32_t *hotnew;         // [NBIT] members that got a new dissemination entry while not hot
     uint32_t *hot_cnt;        // {slots in use, slots filled}
     uint32_t HP;              // hot slots per row

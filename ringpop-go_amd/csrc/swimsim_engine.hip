@@ -351,6 +351,7 @@ struct swimsim {
     CsrPlan *csr_plan = nullptr;
     CsrRec *csr_rec = nullptr;
     uint32_t csr_ecap = 2048, csr_rcap = 512, csr_KP = 0;
+    uint32_t *csr_ulist = nullptr, *csr_ucnt = nullptr; // the divergent columns (DS::colx) in member order
     uint32_t csr_maxdiff = 0;                     // swimsim_tuning.cs_ref_maxdiff: mean differing members per sampled
                                                   // row above which a launch keeps the production kernels (0: never)
     uint64_t csr_launches = 0, csr_fallback_rows = 0, csr_declined = 0;
@@ -830,7 +831,9 @@ int csr_alloc(swimsim *h) {
         (rc = dalloc(h, &h->csr_ent, (size_t)rows * h->csr_ecap * 2, "csr exception entries")) ||
         (rc = dalloc(h, &h->csr_plan, (size_t)rows / CSR_ROWS + 1, "csr plans")) ||
         (rc = dalloc(h, &h->csr_rec, (size_t)rows * h->csr_rcap, "csr records")) ||
-        (rc = dalloc(h, &h->csr_nrec, (size_t)rows, "csr record counts"))) {
+        (rc = dalloc(h, &h->csr_nrec, (size_t)rows, "csr record counts")) ||
+        (rc = dalloc(h, &h->csr_ulist, (size_t)h->N, "csr divergent columns")) ||
+        (rc = dalloc(h, &h->csr_ucnt, 1, "csr divergent column count"))) {
         h->csr_failed = true;                                      // the production kernels stay in charge
         h->err.clear();
         return rc;
@@ -863,6 +866,8 @@ int csr_hash(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t n, 
     ca.ent = h->csr_ent;
     ca.rinfo = h->csr_rinfo;
     ca.ecap = h->csr_ecap;
+    ca.ulist = h->csr_ulist;
+    ca.ucnt = h->csr_ucnt;
     CsrArgs a{};
     a.P = h->csr_P;
     a.KP = h->csr_KP;
@@ -889,6 +894,7 @@ int csr_hash(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t n, 
         size_t bytes = h->cub_bytes;
         HIPCHK(h, hipcub::DeviceScan::ExclusiveSum(h->cub_tmp, bytes, h->csr_Lb, h->csr_OB, (int)h->N + 1, h->s));
         HIPCHK(h, hipMemsetAsync(h->csr_SBw, 0, h->csr_sbw_words * 4, h->s));
+        hipLaunchKernelGGL(k_csr_ulist, dim3(1), dim3(1024), 0, h->s, h->d, h->csr_ulist, h->csr_ucnt);
         launch_csr(h->d, list, n, cnt, ca, a, h->s, 0);
         launch_csr(h->d, list, n, cnt, ca, a, h->s, 1);
         launch_csr(h->d, list, n, cnt, ca, a, h->s, 2);
@@ -1659,9 +1665,11 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
         (rc = dalloc(h, &d.live, h->N, "live")) || (rc = dalloc(h, &d.part, h->N, "part")) ||
         (rc = dalloc(h, &d.ctr, (size_t)CTR_SHARDS * CTR_STRIDE, "counters")) || (rc = dalloc(h, &d.err, 4, "err")) ||
         (rc = dalloc(h, &d.clen, h->NL, "clen")) || (rc = dalloc(h, &d.clast, h->NL, "clast")) ||
-        (rc = dalloc(h, &d.cpslot, h->NL, "cpslot")) || (rc = dalloc(h, &d.nhe, h->NL, "cold entry counts")))
+        (rc = dalloc(h, &d.cpslot, h->NL, "cpslot")) || (rc = dalloc(h, &d.nhe, h->NL, "cold entry counts")) ||
+        (rc = dalloc(h, &d.colx, d.NBIT, "divergent columns")))
         return bail(rc);
     hipMemset(d.nhe, 0, (size_t)h->NL * 4);
+    hipMemset(d.colx, 0xFF, (size_t)d.NBIT * 4);
     hipMemset(d.cpslot, 0xFF, (size_t)h->NL * 4);
     {
         // hot columns: 2,048 slots per row (1.6 GB at 65,536 rows); swimsim_tuning.hot_slots = 0
@@ -1833,6 +1841,8 @@ int swimsim_destroy(swimsim_t *h) {
 static int init_rows(swimsim_t *h, int mode) {
     hot_reset(h, false);
     hipLaunchKernelGGL(k_init_rows, dim3(blocks_for_waves(h->NL)), dim3(SWIM_WAVE_BLOCK), 0, h->s, h->d, mode, 0u);
+    // converged rows are all equal: no column differs; self-only rows differ everywhere
+    HIPCHK(h, hipMemsetAsync(h->d.colx, mode == 0 ? 0 : 0xFF, (size_t)h->d.NBIT * 4, h->s));
     if (int rc = checksum_dirty(h, 0)) return rc;
     return check_err(h);
 }
@@ -1848,6 +1858,7 @@ int swimsim_set_member(swimsim_t *h, uint32_t o, uint32_t m, int32_t status, int
     if (status != SWIMSIM_UNKNOWN)
         if (int rc = to_e(h, inc_ms, &e)) return rc;
     const uint32_t w = (e << 3) | (uint32_t)status;
+    HIPCHK(h, hipMemsetAsync(h->d.colx, 0xFF, (size_t)h->d.NBIT * 4, h->s));   // raw write: every column may differ
     hot_reset(h, true);
     HIPCHK(h, hipMemcpyAsync(h->d.mw + (size_t)(o - h->lo) * h->NP + m, &w, 4, hipMemcpyHostToDevice, h->s));
     hipLaunchKernelGGL(k_recount, dim3(1), dim3(64), 0, h->s, h->d, o - h->lo);
@@ -1866,6 +1877,7 @@ int swimsim_set_row(swimsim_t *h, uint32_t o, const uint8_t *status, const int64
         if (int rc = to_e(h, inc_ms[m], &e)) return rc;
         row[m] = (e << 3) | (uint32_t)s;
     }
+    HIPCHK(h, hipMemsetAsync(h->d.colx, 0xFF, (size_t)h->d.NBIT * 4, h->s));   // raw write: every column may differ
     hot_reset(h, true);
     HIPCHK(h, hipMemcpyAsync(h->d.mw + (size_t)(o - h->lo) * h->NP, row.data(), (size_t)h->N * 4,
                              hipMemcpyHostToDevice, h->s));

@@ -80,6 +80,14 @@ __device__ __forceinline__ void track_len(const DS &d, uint32_t ol, uint32_t m, 
     else if (os < 4u && (int)m == d.clast[ol]) acc.inval = 1;
 }
 
+// a row word of member m changes: its column may now differ between rows (DS::colx; a relaxed test first, the bit is
+// set once per column and epoch)
+__device__ __forceinline__ void colmark(const DS &d, uint32_t m) {
+    uint32_t *w = d.colx + (m >> 5);
+    const uint32_t bit = 1u << (m & 31);
+    if (!(__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit)) atomicOr(w, bit);
+}
+
 // cur = the row word d.mw[ol][m] (callers batch these loads)
 __device__ __forceinline__ void merge_change_w(const DS &d, uint32_t ol, uint32_t o, uint32_t m, uint32_t cur, uint32_t cst,
                                                uint32_t ce, uint32_t csrc, uint32_t csinc, uint32_t now_e, uint32_t sched_r,
@@ -104,6 +112,7 @@ __device__ __forceinline__ void merge_change_w(const DS &d, uint32_t ol, uint32_
     const size_t hx = (size_t)ol * d.HP + hk;
     d.mw[idx] = nw_;
     if (hk != SRC_NONE) d.hmw[hx] = nw_;
+    colmark(d, m);
     track_len(d, ol, m, cur, nw_, acc);
     acc.dfp += fpmix(m, (ne << 3) | nst) - fpmix(m, cur);
     if (m != o) acc.dping += (int)is_pingable(nst) - (int)is_pingable(cur_st);
@@ -820,6 +829,7 @@ __global__ void k_timers(DS d, uint32_t r) {
                     if ((w & 7u) != ST_UNKNOWN && m != o) {
                         if (is_pingable(w & 7u)) acc.dping--;
                         d.mw[idx] = (w & ~7u) | ST_UNKNOWN;
+                        colmark(d, m);
                         const uint32_t hk = hot_slot(d, m);
                         if (hk != SRC_NONE) d.hmw[(size_t)ol * d.HP + hk] = (w & ~7u) | ST_UNKNOWN;
                         track_len(d, ol, m, w, (w & ~7u) | ST_UNKNOWN, acc);
