@@ -10,7 +10,7 @@
 // launch for all 20 phases (k_csr_ptable: the table P, 32 B per S_B block and phase), and the chain kernel only
 // streams them from LDS: per block 12 VALU instructions and two LDS reads per row.
 //
-//   k_csr_ptable  P[phi][k] = premix of S_B bytes [20 k + phi, 20 k + phi + 32)   {0, 0, Mg, D}, {Mf, PF, Mh, KH}
+//   k_csr_ptable  P[phi][k] = premix of S_B bytes [20 k + phi, 20 k + phi + 32)   {Mg, D, Mf, PF}, {Mh, KH, 0, 0}
 //   k_csr_plan    per workgroup of CSR_ROWS listed rows: the shift range and phases of its clean blocks -> the LDS
 //                 window geometry (Wn positions per phase), or "infeasible" (the workgroup's rows fall back)
 //   k_csr_rec     per row: one record per super step (CSR_SB blocks) that holds exception blocks: the super step's
@@ -56,7 +56,7 @@ struct __attribute__((aligned(16))) CsrRec {
 struct CsrArgs {
     const uint4 *P;        // [20][KP] x 2
     uint32_t KP;
-    const uint4 *ent;      // k_csd_scan's entries [rows][ecap] x 2: {k, s_after, Mg, D}, {Mf, PF, Mh, KH}
+    const uint4 *ent;      // k_csd_scan's entries [rows][ecap] x 2: {Mg, D, Mf, PF}, {Mh, KH, k, s_after}
     const CsdRow *rinfo;   // [rows]
     uint32_t ecap;
     CsrPlan *plan;         // [workgroups]
@@ -65,6 +65,9 @@ struct CsrArgs {
     uint32_t rcap;
     uint32_t *fb_list, *fb_cnt;   // rows left to the production kernels
 };
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ int32_t csr_ceil20(int32_t x) { return x >= 0 ? (x + 19) / 20 : -((-x) / 20); }
 
@@ -91,8 +94,8 @@ __global__ void k_csr_ptable(const uint32_t *__restrict__ SBw, uint32_t sbw_word
     for (int i = 0; i < 8; i++) w[i] = __builtin_amdgcn_alignbyte(x[i + 1], x[i], sh);
     uint32_t v[6];
     csd_premix(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], v);
-    P[2 * q] = make_uint4(0u, 0u, v[0], v[1]);
-    P[2 * q + 1] = make_uint4(v[2], v[3], v[4], v[5]);
+    P[2 * q] = make_uint4(v[0], v[1], v[2], v[3]);
+    P[2 * q + 1] = make_uint4(v[4], v[5], 0u, 0u);
 }
 
 __global__ void __launch_bounds__(CSR_ROWS) k_csr_plan(DS d, const uint32_t *list, uint32_t n, CsrArgs a) {
@@ -149,7 +152,7 @@ __global__ void __launch_bounds__(256) k_csr_rec(DS d, const uint32_t *list, uin
         while (c0 < ri.ecnt) {
             const uint32_t nin = min(64u, ri.ecnt - c0);
             const bool in = lane < nin;
-            const uint2 h = in ? *(const uint2 *)(ent + 2 * (c0 + lane)) : make_uint2(0xFFFFFFFFu, 0u);   // {k, s after}
+            const uint2 h = in ? ((const uint2 *)(ent + 2 * (c0 + lane) + 1))[1] : make_uint2(0xFFFFFFFFu, 0u);   // {k, s after}
             hd[wv][lane] = h;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -255,26 +258,52 @@ __global__ void __launch_bounds__(CSR_ROWS) k_csr(DS d, const uint32_t *list, co
     uint32_t base = csr_base(p, 0);
 
     // the next record and its first exception entries, loaded one record ahead
-    uint32_t rcur = 0;
-    CsrRec R{};
-    uint4 RE0a, RE0b, RE1a, RE1b, RE2a, RE2b, RE3a, RE3b;   // (named registers: an indexed array went to scratch)
+    // (records partition the row's entries in order: record q + 1 begins where record q ends, so the entry loads never
+    // wait for the record itself; nothing here selects on a loaded value, which would wait for the load at once)
+    // (record and entries are held as whole vector registers, each loaded by one instruction into exactly the
+    // registers it lives in: loaded structs split into scalars came out as copies after the loads, each waiting for them)
+    uint32_t rcur = 0, ecur = 0;
+    bool rv = false;
+    u32x4 R0, R1, R2, R3, R4;                                    // CsrRec: {t, s_end, e0, ne}, code[0..15]
+    u32x4 RE0a, RE1a, RE2a, RE3a;                                // entry values {Mg, D, Mf, PF}
+    u32x2 RE0b, RE1b, RE2b, RE3b;                                // {Mh, KH}
     // (unconditional loads from clamped indices: conditionally assigned arrays would live in scratch)
-    auto load_rec = [&](uint32_t q) {
-        R = rec[min(q, a.rcap - 1u)];
-        const uint4 *ep = ent + 2 * min(R.e0, a.ecap - (uint32_t)CSR_EREG);
-        RE0a = ep[0]; RE0b = ep[1]; RE1a = ep[2]; RE1b = ep[3]; RE2a = ep[4]; RE2b = ep[5]; RE3a = ep[6]; RE3b = ep[7];
-        if (q >= nr) {
-            R.t = 0xFFFFFFFFu;
-            R.ne = 0;
-        }
+    auto load_rec = [&](uint32_t q, uint32_t e0) {
+        const u32x4 *rp = (const u32x4 *)(rec + min(q, a.rcap - 1u));
+        R0 = rp[0]; R1 = rp[1]; R2 = rp[2]; R3 = rp[3]; R4 = rp[4];
+        const u32x4 *ep = (const u32x4 *)(ent + 2 * min(e0, a.ecap - (uint32_t)CSR_EREG));
+        RE0a = ep[0]; RE0b = *(const u32x2 *)(ep + 1);
+        RE1a = ep[2]; RE1b = *(const u32x2 *)(ep + 3);
+        RE2a = ep[4]; RE2b = *(const u32x2 *)(ep + 5);
+        RE3a = ep[6]; RE3b = *(const u32x2 *)(ep + 7);
+        rv = q < nr;
     };
-    load_rec(0);
+    load_rec(0, 0);
+#ifdef CSR_DIAG_STAMP
+    // (diagnostic build only: shader-clock stamps around the loop's sections, summed per wave into the diagnostic
+    // counters: 0 chain, 1 staging + preparation, 2 barrier, 3 whole loop; shares only, the stamps drain LDS waits)
+    uint64_t st_[4] = {0, 0, 0, 0};
+    auto stamp = [&]() -> uint64_t {
+        uint64_t tt;
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tt) :: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        return tt;
+    };
+#define CSR_STAMP(v) const uint64_t v = stamp()
+#define CSR_ACC(k, x) st_[k] += (x)
+#else
+#define CSR_STAMP(v)
+#define CSR_ACC(k, x)
+#endif
 
     // window staging: entries u = tid + 256 v of the next super step's window, through registers
     constexpr int WV = CSR_WINMAX / CSR_ROWS;
     // two staging sets: super step u's window goes through set u & 1, loaded two super steps ahead (the window rows of
     // P miss in L2 at their first touch: one HBM round trip, longer than a super step's chain)
-    uint4 wA[WV][2], wB[WV][2];
+    // (vector types: a struct copy of a uint4 is a memcpy, and the compiler promoted the staging arrays to LDS)
+    u32x4 wA0[WV], wB0[WV];
+    u32x2 wA1[WV], wB1[WV];
     const uint32_t nwin = p.nph * p.Wn;
     // (each thread's window entries keep their phase and position from super step to super step: their source rows
     // in P are fixed, the S_B block advances by CSR_SB)
@@ -287,24 +316,24 @@ __global__ void __launch_bounds__(CSR_ROWS) k_csr(DS d, const uint32_t *list, co
         wsrc[v] = a.P + 2 * (size_t)phs[min(ps, 19u)] * a.KP;
         wk0[v] = u < nwin ? (int32_t)w - p.cmax : 0x40000000;
     }
-    auto wload = [&](uint4 (&wst)[WV][2], uint32_t t) {
+    auto wload = [&](u32x4 (&wst0)[WV], u32x2 (&wst1)[WV], uint32_t t) {
 #pragma unroll
         for (int v = 0; v < WV; v++) {
-            const int32_t k = wk0[v] + (int32_t)(t * CSR_SB);
-            const bool in = k >= 0 && (uint32_t)k < a.KP;
-            const uint4 *src = wsrc[v] + 2 * (in ? (uint32_t)k : 0u);
-            const uint4 x0 = src[0], x1 = src[1];
-            wst[v][0] = in ? x0 : make_uint4(0, 0, 0, 0);
-            wst[v][1] = in ? x1 : make_uint4(0, 0, 0, 0);
+            // (positions outside S_B are read only by predicated blocks past a row's chain: any value does; a select on
+            // the loaded value would wait for this load here, one HBM round trip per super step)
+            const int32_t k = min(max(wk0[v] + (int32_t)(t * CSR_SB), 0), (int32_t)a.KP - 1);
+            const uint4 *src = wsrc[v] + 2 * (uint32_t)k;
+            wst0[v] = *(const u32x4 *)src;
+            wst1[v] = *(const u32x2 *)(src + 1);
         }
     };
-    auto wstore = [&](const uint4 (&wst)[WV][2], uint32_t b) {
+    auto wstore = [&](const u32x4 (&wst0)[WV], const u32x2 (&wst1)[WV], uint32_t b) {
 #pragma unroll
         for (int v = 0; v < WV; v++) {
             const uint32_t u = tid + (uint32_t)CSR_ROWS * v;
             if (u < nwin) {
-                EA[b][u] = make_uint2(wst[v][0].z, wst[v][0].w);
-                EB[b][u] = wst[v][1];
+                EA[b][u] = make_uint2(wst0[v].x, wst0[v].y);
+                EB[b][u] = make_uint4(wst0[v].z, wst0[v].w, wst1[v].x, wst1[v].y);
             }
         }
     };
@@ -312,10 +341,10 @@ __global__ void __launch_bounds__(CSR_ROWS) k_csr(DS d, const uint32_t *list, co
     // rebased to the wave's slots) and its entries; the others write base + i when the wave needs tables.
     // Returns whether this wave reads tables in super step t (wave-uniform).
     auto prep = [&](uint32_t t, uint32_t b) -> bool {
-        const bool has = live && R.t == t;
+        const bool has = live && rv && R0.x == t;
         const bool any = __ballot(has) != 0;
         if (!any) return false;
-        uint32_t ne = has ? R.ne : 0u, tot = 0;
+        uint32_t ne = has ? R0.w : 0u, tot = 0;
         const uint32_t sb = wscan_excl(ne, tot);                  // this row's first slot in the wave's area
         const uint32_t xb = (uint32_t)CSR_WINMAX + wave * CSR_EXW + sb;
         uint2 *tr = T[b] + (size_t)tid * (CSR_TBLW / 2);
@@ -324,7 +353,8 @@ __global__ void __launch_bounds__(CSR_ROWS) k_csr(DS d, const uint32_t *list, co
             // codes: exception ordinals + the row's slot base, clean codes as the record has them
 #pragma unroll
             for (int q = 0; q < 8; q++) {
-                uint32_t c0 = R.code[2 * q], c1 = R.code[2 * q + 1];
+                const u32x4 Rq = q < 2 ? R1 : q < 4 ? R2 : q < 6 ? R3 : R4;
+                uint32_t c0 = (q & 1) ? Rq.z : Rq.x, c1 = (q & 1) ? Rq.w : Rq.y;
                 uint32_t lo0 = c0 & 0xFFFFu, hi0 = c0 >> 16, lo1 = c1 & 0xFFFFu, hi1 = c1 >> 16;
                 lo0 = (lo0 & CSR_EXC) ? xb + (lo0 & 0x7FFFu) : lo0;
                 hi0 = (hi0 & CSR_EXC) ? xb + (hi0 & 0x7FFFu) : hi0;
@@ -335,17 +365,17 @@ __global__ void __launch_bounds__(CSR_ROWS) k_csr(DS d, const uint32_t *list, co
             if (!(fl & CSR_F_SLOTS)) {
                 uint2 *xa = EA[b] + xb;
                 uint4 *xf = EB[b] + xb;
-                if (ne > 0) { xa[0] = make_uint2(RE0a.z, RE0a.w); xf[0] = RE0b; }
-                if (ne > 1) { xa[1] = make_uint2(RE1a.z, RE1a.w); xf[1] = RE1b; }
-                if (ne > 2) { xa[2] = make_uint2(RE2a.z, RE2a.w); xf[2] = RE2b; }
-                if (ne > 3) { xa[3] = make_uint2(RE3a.z, RE3a.w); xf[3] = RE3b; }
+                if (ne > 0) { xa[0] = make_uint2(RE0a.x, RE0a.y); xf[0] = make_uint4(RE0a.z, RE0a.w, RE0b.x, RE0b.y); }
+                if (ne > 1) { xa[1] = make_uint2(RE1a.x, RE1a.y); xf[1] = make_uint4(RE1a.z, RE1a.w, RE1b.x, RE1b.y); }
+                if (ne > 2) { xa[2] = make_uint2(RE2a.x, RE2a.y); xf[2] = make_uint4(RE2a.z, RE2a.w, RE2b.x, RE2b.y); }
+                if (ne > 3) { xa[3] = make_uint2(RE3a.x, RE3a.y); xf[3] = make_uint4(RE3a.z, RE3a.w, RE3b.x, RE3b.y); }
                 for (uint32_t k = CSR_EREG; k < ne; k++) {          // more than CSR_EREG: synchronous loads (rare)
-                    const uint4 x0 = ent[2 * (R.e0 + k)];
-                    EA[b][xb + k] = make_uint2(x0.z, x0.w);
-                    EB[b][xb + k] = ent[2 * (R.e0 + k) + 1];
+                    const uint4 x0 = ent[2 * (R0.z + k)], x1 = ent[2 * (R0.z + k) + 1];
+                    EA[b][xb + k] = make_uint2(x0.x, x0.y);
+                    EB[b][xb + k] = make_uint4(x0.z, x0.w, x1.x, x1.y);
                 }
             }
-            s = R.s_end;
+            s = (int32_t)R0.y;
         } else {
 #pragma unroll
             for (int q = 0; q < 8; q++) {
@@ -357,23 +387,29 @@ __global__ void __launch_bounds__(CSR_ROWS) k_csr(DS d, const uint32_t *list, co
     };
 
     // super step 0
-    wload(wA, 0);
-    wstore(wA, 0);
-    if (T_ > 1) wload(wB, 1);
+    wload(wA0, wA1, 0);
+    wstore(wA0, wA1, 0);
+    if (T_ > 1) wload(wB0, wB1, 1);
     bool tab = prep(0, 0);
-    if (live && R.t == 0) { base = csr_base(p, s); rcur++; load_rec(rcur); }
+    if (live && rv && R0.x == 0) { base = csr_base(p, s); rcur++; ecur += R0.w; load_rec(rcur, ecur); }
     __syncthreads();
-    for (uint32_t t = 0; t < T_; t++) {
-        const uint32_t b = t & 1u, K0 = t * CSR_SB;
-        if (t + 2 < T_) {                                          // set t & 1 is free: super step t is in LDS
-            if (b) wload(wB, t + 2);
-            else wload(wA, t + 2);
-        }
+    // (the loop runs two super steps per trip, one per buffer, so that every staging set and LDS buffer is named at
+    // compile time: a buffer chosen at run time made the compiler select between the two sets' addresses and keep
+    // both in scratch)
+    auto iter = [&](uint32_t t, auto BC) {
+        constexpr uint32_t b = decltype(BC)::value;
+        const uint32_t K0 = t * CSR_SB;
+        // set b is free: super step t is in LDS. (Issued even past the last super step, from clamped positions: with
+        // the loads on one path only, the wait before the stores of the other set had to cover the path without them,
+        // i.e. these very loads.)
+        if constexpr (b) wload(wB0, wB1, t + 2);
+        else wload(wA0, wA1, t + 2);
         // ---- the chain over blocks K0 .. K0 + 31 ----
         // The block loop is straight-line code per variant (FULL: every row's chain covers the whole super step, no
         // predication; TAB: codes from the row's table instead of base + i), and each block's two LDS reads are
         // issued CSR_PF blocks ahead of its arithmetic: a read followed at once by its use waits the whole LDS latency
         // (about 120 cycles with four waves reading), twice the chain's own cost of a block.
+        CSR_STAMP(ts0);
         const bool full = __all(myit == 0u || K0 + CSR_SB <= myit);
         const uint2 *EAb = EA[b];
         const uint4 *EBb = EB[b];
@@ -395,7 +431,12 @@ __global__ void __launch_bounds__(CSR_ROWS) k_csr(DS d, const uint32_t *list, co
             uint2 vg[CSR_PF + 1];
             uint4 vf[CSR_PF + 1];
             auto fetch = [&](int i) {
+#ifdef CSR_DIAG_BCAST
+                // (diagnostic build only: every lane reads lane 0's entry, wrong checksums, no bank conflicts)
+                const uint32_t e = (uint32_t)__builtin_amdgcn_readfirstlane((int)(TAB ? code[i] : base + (uint32_t)i));
+#else
                 const uint32_t e = TAB ? code[i] : base + (uint32_t)i;
+#endif
                 vg[i % (CSR_PF + 1)] = EAb[e];
                 vf[i % (CSR_PF + 1)] = EBb[e];
             };
@@ -425,14 +466,40 @@ __global__ void __launch_bounds__(CSR_ROWS) k_csr(DS d, const uint32_t *list, co
         else if (!tab) run(FF{}, FF{});
         else run(FF{}, TT{});
         // ---- the next super step's window, rows and entries into the other buffer ----
+        // (kept after the chain: hoisted above it, the stores of a staging set would wait for its loads there)
+        asm volatile("" ::: "memory");
+        CSR_STAMP(ts1);
+        CSR_ACC(0, ts1 - ts0);
         if (t + 1 < T_) {
-            if (b) wstore(wA, 0u);                                  // super step t + 1 (even) -> buffer 0
-            else wstore(wB, 1u);
+            if constexpr (b) wstore(wA0, wA1, 0u);                  // super step t + 1 (even) -> buffer 0
+            else wstore(wB0, wB1, 1u);
             tab = prep(t + 1, b ^ 1u);
-            if (live && R.t == t + 1) { base = csr_base(p, s); rcur++; load_rec(rcur); }
+            // (the record loads run for the whole wave whenever one of its rows moves on, the others reloading their
+            // current record: a load into only some lanes keeps the old values live in the rest, and the compiler
+            // copies the loaded registers over them, waiting for the loads right here)
+            const bool adv = live && rv && R0.x == t + 1;
+            if (adv) { base = csr_base(p, s); rcur++; ecur += R0.w; }
+            if (__ballot(adv)) load_rec(rcur, ecur);
         }
+        CSR_STAMP(ts2);
         __syncthreads();
+        CSR_STAMP(ts3);
+        CSR_ACC(1, ts2 - ts1);
+        CSR_ACC(2, ts3 - ts2);
+    };
+    CSR_STAMP(tl0);
+    for (uint32_t t = 0; t < T_; t += 2) {
+        iter(t, std::integral_constant<uint32_t, 0>{});
+        if (t + 1 < T_) iter(t + 1, std::integral_constant<uint32_t, 1>{});
     }
+    CSR_STAMP(tl1);
+    CSR_ACC(3, tl1 - tl0);
+#ifdef CSR_DIAG_STAMP
+    if (lane == 0)
+        for (int k = 0; k < 4; k++) ctr_add(d, C_NALL + k, (unsigned long long)st_[k]);
+#endif
+#undef CSR_STAMP
+#undef CSR_ACC
     const bool mine = valid && fl == 0;
     const uint32_t nmine = (uint32_t)__popcll(__ballot(mine));
     if (lane == 0 && nmine) ctr_add(d, C_X_CS_ROWS, (unsigned long long)nmine);   // rows this launch hashed

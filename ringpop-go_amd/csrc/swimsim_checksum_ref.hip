@@ -43,7 +43,7 @@ struct CsdArgs {
     const uint32_t *OB;       // [N+1] reference record offsets, OB[N] = |S_B|
     const uint32_t *SBw;      // S_B as little-endian words, zero padded (sbw_words of them)
     uint32_t sbw_words;
-    uint4 *ent;               // [rows][ecap] exception entries, 2 uint4 each: {k, s_after, Mg, D}, {Mf, PF, Mh, KH}
+    uint4 *ent;               // [rows][ecap] exception entries, 2 uint4 each: {Mg, D, Mf, PF}, {Mh, KH, k, s_after}
     CsdRow *rinfo;            // [rows]
     uint32_t ecap;
     uint32_t *fb_list, *fb_cnt; // rows left to the production kernels; fb_cnt[1 + b]: rows with flag bit b
@@ -190,8 +190,8 @@ __device__ void csd_run_entries(const DS &d, const uint32_t *row, uint32_t m0, u
                            wd = z ? win[6] : win[3], we = z ? win[7] : win[4];
             uint32_t v[6];
             csd_premix(wa, wb, wc, wd, we, z ? 0u : win[5], z ? 0u : win[6], z ? 0u : win[7], v);
-            out[2 * done] = make_uint4(klo + done, (uint32_t)s_after, v[0], v[1]);
-            out[2 * done + 1] = make_uint4(v[2], v[3], v[4], v[5]);
+            out[2 * done] = make_uint4(v[0], v[1], v[2], v[3]);
+            out[2 * done + 1] = make_uint4(v[4], v[5], klo + done, (uint32_t)s_after);
             if (klo + done == 0) { ri->a0 = wa; ri->b0 = wb; ri->c0 = wc; }
             done++;
             ready = (tail0 && done == nbk - 1) ? 5u * done + 5u : 5u * done + 8u;
@@ -230,14 +230,12 @@ __device__ void csd_run_entries(const DS &d, const uint32_t *row, uint32_t m0, u
 
 template <int W>
 __global__ void __launch_bounds__(256) k_csd_scan(DS d, const uint32_t *list, uint32_t n, CsdArgs a) {
-    // CSD_SU chunks of 64 members per pass, their loads in flight together (a row is one 256-KB stream). Chunks with
-    // differing members are staged in LDS, and the pass's diffs are walked by a loop that is not unrolled; runs wait
-    // in LDS for their entries, generated (one lane per run) between passes.
+    // CSD_SU chunks of 64 members per pass, their loads in flight together (a row is one 256-KB stream). The pass's
+    // differing members are walked in order by the whole wave, each one's word, B word and B offsets read from the
+    // lane that loaded them (v_readlane: no LDS staging, no load inside the walk); runs wait in LDS for their
+    // entries, generated (one lane per run) between passes.
     constexpr uint32_t CSD_SU = 8, RUNCAP = 128, RUNFLUSH = 64;
     __shared__ uint32_t runs[4][RUNCAP][6];                         // {klo, khi, m0, o0, s_after, first entry}
-    __shared__ uint32_t stw[4][CSD_SU][64];                         // staged row words of a pass
-    __shared__ uint64_t stm[4][CSD_SU];                             // their diff masks
-    __shared__ uint32_t stmem[4][CSD_SU][64];                       // their members
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
     const uint32_t i = blockIdx.x * 4 + wv;
     if (i >= n) return;
@@ -287,9 +285,10 @@ __global__ void __launch_bounds__(256) k_csd_scan(DS d, const uint32_t *list, ui
         e += nb;
         nruns++;
     };
-    auto diff = [&](uint32_t mm, uint32_t wm, uint32_t bm) {
+    // member mm differs: row word wm, B word bm, B offsets obm = O_B[mm] and ob1 = O_B[mm - 1]
+    auto diff = [&](uint32_t mm, uint32_t wm, uint32_t bm, uint32_t obm, uint32_t ob1) {
         const int32_t Lr = (int32_t)csd_reclen(d, wm), Lbm = (int32_t)csd_reclen(d, bm);
-        const int32_t x = (int32_t)a.OB[mm] + s, y = x + Lr;        // the record's bytes in the row: [x, y)
+        const int32_t x = (int32_t)obm + s, y = x + Lr;             // the record's bytes in the row: [x, y)
         // blocks whose 32 bytes [20k, 20k + 32) meet [x, y) (or straddle x when the record is empty)
         const int32_t klo = x >= 32 ? (x - 32) / 20 + 1 : 0;
         int32_t khi = y >= 1 ? (y - 1) / 20 : -1;
@@ -301,10 +300,11 @@ __global__ void __launch_bounds__(256) k_csd_scan(DS d, const uint32_t *list, ui
                 close_run(s);
                 // the new run starts at row byte p = 20 klo, in the clean bytes before mm (shift s): the record
                 // holding B offset t = p - s is the last member below mm with O_B <= t
+                // (mm >= 1 here: member 0's record meets block 0, which always begins a run)
                 const uint32_t t = (uint32_t)(20 * klo - s);
-                uint32_t m0 = mm - 1;
-                while (m0 > 0 && a.OB[m0] > t) m0--;
-                rlo = (uint32_t)klo; rhi = (uint32_t)khi; rm0 = m0; ro0 = t - a.OB[m0];
+                uint32_t m0 = mm - 1, om = ob1;
+                while (m0 > 0 && om > t) om = a.OB[--m0];
+                rlo = (uint32_t)klo; rhi = (uint32_t)khi; rm0 = m0; ro0 = t - om;
             }
         }
         s += Lr - Lbm;
@@ -324,26 +324,31 @@ __global__ void __launch_bounds__(256) k_csd_scan(DS d, const uint32_t *list, ui
             wv_[k] = c < ncol ? row[m] : 0u;
             bv_[k] = c < ncol ? a.B[m] : 0u;
         }
-        uint32_t any = 0;
+        uint64_t mk[CSD_SU];
+        uint64_t any = 0;
 #pragma unroll
         for (uint32_t k = 0; k < CSD_SU; k++) {
-            const uint64_t mk = __ballot(c00 + 64 * k + lane < ncol && !csd_same(wv_[k], bv_[k]));
-            if (mk) { stw[wv][k][lane] = wv_[k]; stmem[wv][k][lane] = mv_[k]; }
-            if (lane == 0) stm[wv][k] = mk;
-            any |= mk ? 1u : 0u;
+            mk[k] = __ballot(c00 + 64 * k + lane < ncol && !csd_same(wv_[k], bv_[k]));
+            any |= mk[k];
         }
         if (!any) continue;
-        wsync();
-        for (uint32_t k = 0; k < CSD_SU && !flags; k++) {
-            uint64_t mask = stm[wv][k];
+        uint32_t ov_[CSD_SU], o1_[CSD_SU];
+#pragma unroll
+        for (uint32_t k = 0; k < CSD_SU; k++) {
+            ov_[k] = a.OB[mv_[k]];
+            o1_[k] = a.OB[mv_[k] ? mv_[k] - 1u : 0u];
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < CSD_SU; k++) {
+            uint64_t mask = mk[k];
             while (mask && !flags) {                                // the chunk's differing members, in order
                 const uint32_t l = (uint32_t)__builtin_ctzll(mask);
                 mask &= mask - 1;
-                const uint32_t mm = stmem[wv][k][l];
-                diff(mm, stw[wv][k][l], a.B[mm]);
+                diff((uint32_t)__builtin_amdgcn_readlane((int)mv_[k], (int)l), (uint32_t)__builtin_amdgcn_readlane((int)wv_[k], (int)l),
+                     (uint32_t)__builtin_amdgcn_readlane((int)bv_[k], (int)l), (uint32_t)__builtin_amdgcn_readlane((int)ov_[k], (int)l),
+                     (uint32_t)__builtin_amdgcn_readlane((int)o1_[k], (int)l));
             }
         }
-        wsync();
         if (nruns >= RUNFLUSH) flush();
     }
     if (!flags) {

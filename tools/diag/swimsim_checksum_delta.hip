@@ -134,8 +134,8 @@ __global__ void __launch_bounds__(CsdGeo<G>::THREADS) k_cs_delta(DS d, const uin
             for (int q = 0; q < CSD_E; q++) {
                 if (cur + q < ecnt) {
                     const uint4 x = ent[2 * (cur + q)], y = ent[2 * (cur + q) + 1];
-                    bk[q] = x.x; bs[q] = (int32_t)x.y;
-                    bv[q][0] = make_uint2(x.z, x.w); bv[q][1] = make_uint2(y.x, y.y); bv[q][2] = make_uint2(y.z, y.w);
+                    bk[q] = y.z; bs[q] = (int32_t)y.w;
+                    bv[q][0] = make_uint2(x.x, x.y); bv[q][1] = make_uint2(x.z, x.w); bv[q][2] = make_uint2(y.x, y.y);
                 } else {
                     bk[q] = 0xFFFFFFFFu; bs[q] = 0;
                     bv[q][0] = bv[q][1] = bv[q][2] = make_uint2(0u, 0u);
@@ -221,7 +221,7 @@ __global__ void __launch_bounds__(CsdGeo<G>::THREADS) k_cs_delta(DS d, const uin
             // more exception blocks in this super step than the batch holds (a run of adjacent differing records):
             // the rest are counted and read with synchronous loads (rare)
             const bool ovf = ne == (uint32_t)CSD_E && cur + CSD_E < ecnt;
-            auto kat = [&](uint32_t e) -> uint32_t { return ((const uint32_t *)(ent + 2 * e))[0]; };
+            auto kat = [&](uint32_t e) -> uint32_t { return ((const uint32_t *)(ent + 2 * e + 1))[2]; };
             if (__builtin_expect(__ballot(ovf) != 0, 0)) {
                 if (ovf)
                     while (cur + ne < ecnt && kat(cur + ne) < K0 + CSD_SB) ne++;
@@ -279,7 +279,7 @@ __global__ void __launch_bounds__(CsdGeo<G>::THREADS) k_cs_delta(DS d, const uin
                     }
                     for (uint32_t q = CSD_E; q < ne; q++) {                // the overflow, from global memory
                         const uint4 x = ent[2 * (cur + q)], y = ent[2 * (cur + q) + 1];
-                        place(q, x.x, (int32_t)x.y, make_uint2(x.z, x.w), make_uint2(y.x, y.y), make_uint2(y.z, y.w),
+                        place(q, y.z, (int32_t)y.w, make_uint2(x.x, x.y), make_uint2(x.z, x.w), make_uint2(y.x, y.y),
                               kat(cur + q - 1), q + 1 < ne ? kat(cur + q + 1) : 0u);
                     }
                     if (nj > (uint32_t)CSD_NJ) fl |= CSD_F_JUMPS;
