@@ -290,6 +290,8 @@ def main():
     # diagnostics: every rank on cuda:0, shards exchanging through the gloo host transport instead of
     # RCCL (lets the multi-process path run on a one-GPU machine); never used for reported numbers
     ap.add_argument("--host-transport", action="store_true")
+    # the reference-row checksum path (swimsim_tuning.cs_ref: 0 off, 1 wide launches; default: the library's)
+    ap.add_argument("--cs-ref", type=int, default=-1)
     # test hook: the ranks report (rank, world size) and exit before any GPU call
     ap.add_argument("--launch-check", action="store_true")
     args = ap.parse_args()
@@ -334,17 +336,18 @@ def main():
 
     n = args.members
     total_rounds = args.warmup + args.steps
+    tuning = {"cs_ref": args.cs_ref} if args.cs_ref >= 0 else None
     wl = W.config3(n=n, rounds=max(total_rounds, KILL_ROUND + 1), kill_round=KILL_ROUND)
     nkilled = sum(1 for e in wl.events if e[1] == W.EV_KILL)
     if ws > 1:
         from swimsim import dist as sd
 
         if args.host_transport:
-            eng = swimsim.Cluster(n, device=0, comm=(ws, rank, sd.GlooTransport()))
+            eng = swimsim.Cluster(n, device=0, comm=(ws, rank, sd.GlooTransport()), tuning=tuning)
         else:
-            eng = sd.sharded_cluster(n, device=local)
+            eng = sd.sharded_cluster(n, device=local, tuning=tuning)
     else:
-        eng = swimsim.Cluster(n, device=local)
+        eng = swimsim.Cluster(n, device=local, tuning=tuning)
 
     def barrier():
         if ws > 1:

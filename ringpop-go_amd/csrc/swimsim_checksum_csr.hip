@@ -8,28 +8,30 @@
 // shifted by the row's accumulated record-length difference s (swimsim_checksum_ref.hip), so the premixed values of
 // every clean block are a function of (phase = -s mod 20, S_B block index) alone. Here they are computed once per
 // launch for all 20 phases (k_csr_ptable: the table P, 32 B per S_B block and phase), and the chain kernel only
-// streams them from LDS: per block 12 VALU instructions and two LDS reads per row.
+// streams them from LDS: per block 12 VALU instructions and three LDS reads per row, no address arithmetic.
 //
 //   k_csr_ptable  P[phi][k] = premix of S_B bytes [20 k + phi, 20 k + phi + 32)   {Mg, D, Mf, PF}, {Mh, KH, 0, 0}
 //   k_csr_plan    per workgroup of CSR_ROWS listed rows: the shift range and phases of its clean blocks -> the LDS
 //                 window geometry (Wn positions per phase), or "infeasible" (the workgroup's rows fall back)
 //   k_csr_rec     per row: one record per super step (CSR_SB blocks) that holds exception blocks: the super step's
-//                 32 window codes (u16; an exception block's code = CSR_EXC | its ordinal in the super step), the
-//                 shift after it and its first entry (k_csd_scan's entries, sorted by block)
+//                 32 codes (u16: a clean block's window entry as an LDS byte address, CSR_EXC | ordinal for an
+//                 exception block), the shift after it and where its first exceptions are
 //   k_csr         the chains. 256 rows per workgroup (4 waves, lane = row, one wave per SIMD at one workgroup per CU).
 //                 Per super step the waves stage the next super step's window (every phase in use, Wn positions)
 //                 from P and the rows' exception entries into the other LDS buffer while the chain of this one
-//                 runs: a super step without records in a wave reads entry base(s) + i at block i (no table, no
-//                 address arithmetic); otherwise each row's 32 codes come from its record or from its shift.
+//                 runs. Each row reads its 32 blocks' entries at the byte addresses in its own LDS table, which its
+//                 lane rewrites only when the codes change: from a record (exception codes patched to the wave's
+//                 slots), and back to base(s) + i in the super step after one.
 // Rows the path cannot take (scan flags, an infeasible window, a super step with more exception entries than a
 // wave's slots) are listed and hashed by the production kernels (k_checksum3 / k_checksum_q16): bit-exact either way.
 
 constexpr int CSR_ROWS = 256;          // rows per workgroup (4 waves)
 constexpr int CSR_SB = 32;             // blocks per super step
-constexpr int CSR_WINMAX = 1024;       // window entries (32 B) per buffer: phases in use x Wn
+constexpr int CSR_WINMAX = 1024;       // window entries per buffer: phases in use x Wn
 constexpr int CSR_EXW = 128;           // exception entries per wave per buffer
 constexpr int CSR_ENT = CSR_WINMAX + 4 * CSR_EXW;   // entries per buffer
-constexpr int CSR_TBLW = 18;           // u32 words per row of the code table (32 u16 codes + pad: b64 reads conflict-free)
+constexpr int CSR_TW = 36;             // u32 words per row of the code table (32 codes + pad: ds_read_b128 conflict-free)
+constexpr uint32_t CSR_ESZ = 16;       // a code's unit: an entry's byte offset in each of the two entry arrays
 constexpr int CSR_EREG = 4;            // exception entries of a record prefetched with it
 constexpr int CSR_PF = 4;              // blocks the chain's LDS reads run ahead of its arithmetic
 constexpr uint32_t CSR_EXC = 0x8000u;  // code flag: exception entry (low bits: ordinal in the super step)
@@ -49,8 +51,9 @@ struct CsrPlan {
 struct __attribute__((aligned(16))) CsrRec {
     uint32_t t;            // super step
     int32_t s_end;         // the row's shift after the super step
-    uint32_t e0, ne;       // its exception entries: ent[e0 .. e0 + ne)
-    uint32_t code[16];     // 32 u16 codes, block i in the low half of code[i / 2] for even i
+    uint32_t pos4, ne;     // the blocks (bytes 0-3) of its first exception entries (ne <= 4), their number
+    uint32_t code[16];     // 32 u16 codes, block i in the low half of code[i / 2] for even i: the byte address of a
+                           // clean block's window entry, CSR_EXC | ordinal for an exception block
 };
 
 struct CsrArgs {
@@ -171,24 +174,26 @@ __global__ void __launch_bounds__(256) k_csr_rec(DS d, const uint32_t *list, uin
                     CsrRec r;
                     int32_t s = lane ? (int32_t)hd[wv][lane - 1].y : s_prev;
                     const uint32_t K0 = t * CSR_SB;
-                    uint32_t q = lane, kn = h.x;
+                    uint32_t q = lane, kn = h.x, pos = 0;
                     for (uint32_t b = 0; b < (uint32_t)CSR_SB; b++) {
                         const uint32_t j = K0 + b;
                         uint32_t c;
                         if (q < gend && kn == j) {
-                            c = CSR_EXC | (q - lane);
+                            const uint32_t o = q - lane;
+                            c = CSR_EXC | o;
+                            if (o < 4) pos |= b << (8 * o);
                             s = (int32_t)hd[wv][q].y;
                             q++;
                             kn = q < gend ? hd[wv][q].x : 0xFFFFFFFFu;
                         } else {
-                            c = j < iters ? csr_base(p, s) + b : 0u;
+                            c = j < iters ? (csr_base(p, s) + b) * CSR_ESZ : 0u;
                         }
                         if (b & 1u) r.code[b >> 1] |= c << 16;
                         else r.code[b >> 1] = c;
                     }
                     r.t = t;
                     r.s_end = s;
-                    r.e0 = c0 + lane;
+                    r.pos4 = pos;
                     r.ne = gend - lane;
                     rec[slot] = r;
                 }
@@ -208,21 +213,19 @@ __global__ void __launch_bounds__(256) k_csr_rec(DS d, const uint32_t *list, uin
     if (lane == 0) a.nrec[i] = nr;
 }
 
-// one block of the coupled g and f lanes and of the h lane in carried-sum form (swimsim_checksum_ref.hip)
-__device__ __forceinline__ void csr_block(uint32_t &Xg, uint32_t &Xf, uint32_t &Xh, uint2 gd, uint4 fh) {
-    csd_gf_step(Xg, Xf, gd.x, gd.y, fh.x, fh.y);
-    csd_h_step(Xh, fh.z, fh.w);
-}
-
 template <int W>
 __global__ void __launch_bounds__(CSR_ROWS) k_csr(DS d, const uint32_t *list, const uint32_t *count, CsrArgs a) {
-    // per buffer: window entries, then each wave's exception entries, split into {Mg, D} (EA) and {Mf, PF, Mh, KH} (EB):
-    // a lane reads EA[e] (8 B) and EB[e] (16 B). With Wn = 1 mod 32 the entries of the different phases that the rows of
-    // a wave read at one block fall into different LDS banks (a 32-B entry put every entry's halves on the same 8 of 16
-    // 16-B slots: 2.4e9 bank-conflict cycles per launch, half the kernel's time)
-    __shared__ uint2 EA[2][CSR_ENT];
+    // per buffer: window entries, then each wave's exception entries, in two arrays of 16-B entries, EA {Mg, D, Mf, PF}
+    // and EB {Mh, KH, -, -}: a block is two ds_read_b128 at one byte address (the row's code, 16 e) plus each array's
+    // base as the immediate offset. ds_read_b128 runs at the LDS array's full rate with one wave per SIMD; 8-byte
+    // reads do not (three ds_read_b64 per block of 24-B entries: 10.3 ms per launch against 8.5 for one b64 + one b128).
+    // Two rows of a 16-lane group conflict when their entries are 16 apart; with Wn = 1 mod 32 the phases' windows
+    // start at different residues.
+    __shared__ uint4 EA[2][CSR_ENT];
     __shared__ uint4 EB[2][CSR_ENT];
-    __shared__ uint2 T[2][CSR_ROWS * CSR_TBLW / 2];     // per buffer: each row's 32 codes (tables of record super steps)
+    // per row: the byte addresses of its 32 blocks' entries in the super step (one table, not one per buffer: a row's
+    // table is read and written only by its own lane, and rewritten only when its codes change)
+    __shared__ uint32_t T[CSR_ROWS * CSR_TW];
     __shared__ uint32_t phs[20];
     const uint32_t cnt = *count;
     const uint32_t g0 = blockIdx.x * CSR_ROWS;
@@ -248,6 +251,7 @@ __global__ void __launch_bounds__(CSR_ROWS) k_csr(DS d, const uint32_t *list, co
     const CsrRec *rec = a.rec + (size_t)(valid ? gi : g0) * a.rcap;
     const uint4 *ent = a.ent + (size_t)(valid ? gi : g0) * a.ecap * 2;
     const uint32_t nr = live ? nrec : 0u;
+    uint32_t *trow = T + (size_t)tid * CSR_TW;
 
     // chain state (FarmHash-mk prologue, then X = state + the string's first words)
     FH fh{0, 0, 0};
@@ -264,7 +268,7 @@ __global__ void __launch_bounds__(CSR_ROWS) k_csr(DS d, const uint32_t *list, co
     // registers it lives in: loaded structs split into scalars came out as copies after the loads, each waiting for them)
     uint32_t rcur = 0, ecur = 0;
     bool rv = false;
-    u32x4 R0, R1, R2, R3, R4;                                    // CsrRec: {t, s_end, e0, ne}, code[0..15]
+    u32x4 R0, R1, R2, R3, R4;                                    // CsrRec: {t, s_end, pos4, ne}, code[0..15]
     u32x4 RE0a, RE1a, RE2a, RE3a;                                // entry values {Mg, D, Mf, PF}
     u32x2 RE0b, RE1b, RE2b, RE3b;                                // {Mh, KH}
     // (unconditional loads from clamped indices: conditionally assigned arrays would live in scratch)
@@ -327,72 +331,107 @@ __global__ void __launch_bounds__(CSR_ROWS) k_csr(DS d, const uint32_t *list, co
             wst1[v] = *(const u32x2 *)(src + 1);
         }
     };
+    auto put_entry = [&](uint32_t b, uint32_t e, uint2 x, uint2 y, uint2 z) {
+        EA[b][e] = make_uint4(x.x, x.y, y.x, y.y);
+        *(uint2 *)&EB[b][e] = z;
+    };
     auto wstore = [&](const u32x4 (&wst0)[WV], const u32x2 (&wst1)[WV], uint32_t b) {
 #pragma unroll
         for (int v = 0; v < WV; v++) {
+            // (every thread stores all its entries, those past the window into unused window slots: a store on some
+            // paths only left its loads pending on the others, and the loop head waited for them)
             const uint32_t u = tid + (uint32_t)CSR_ROWS * v;
-            if (u < nwin) {
-                EA[b][u] = make_uint2(wst0[v].x, wst0[v].y);
-                EB[b][u] = make_uint4(wst0[v].z, wst0[v].w, wst1[v].x, wst1[v].y);
-            }
+            put_entry(b, u, make_uint2(wst0[v].x, wst0[v].y), make_uint2(wst0[v].z, wst0[v].w),
+                      make_uint2(wst1[v].x, wst1[v].y));
         }
     };
-    // a super step's row preparation in buffer b: a row with a record for t writes its codes (exception codes
-    // rebased to the wave's slots) and its entries; the others write base + i when the wave needs tables.
-    // Returns whether this wave reads tables in super step t (wave-uniform).
-    auto prep = [&](uint32_t t, uint32_t b) -> bool {
+    // a row's codes at shift s with no exception block: the window entries base + i
+    auto write_base = [&]() {
+        const uint32_t ba = base * CSR_ESZ;
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            u32x4 v;
+            v.x = ba + (4u * q + 0u) * CSR_ESZ;
+            v.y = ba + (4u * q + 1u) * CSR_ESZ;
+            v.z = ba + (4u * q + 2u) * CSR_ESZ;
+            v.w = ba + (4u * q + 3u) * CSR_ESZ;
+            *(u32x4 *)(trow + 4 * q) = v;
+        }
+    };
+    // (every lane's table starts valid: a row that is not hashed reads entry 0)
+    if (live) {
+        write_base();
+    } else {
+#pragma unroll
+        for (int q = 0; q < 8; q++) *(u32x4 *)(trow + 4 * q) = u32x4{0u, 0u, 0u, 0u};
+    }
+    bool was = false;                                              // the row's codes are a record's
+    // a super step's row preparation in buffer b: a row with a record for t writes its codes and its exception
+    // entries (exception codes patched to the wave's slots); a row whose last super step had a record writes base + i
+    auto prep = [&](uint32_t t, uint32_t b) {
         const bool has = live && rv && R0.x == t;
-        const bool any = __ballot(has) != 0;
-        if (!any) return false;
-        uint32_t ne = has ? R0.w : 0u, tot = 0;
-        const uint32_t sb = wscan_excl(ne, tot);                  // this row's first slot in the wave's area
-        const uint32_t xb = (uint32_t)CSR_WINMAX + wave * CSR_EXW + sb;
-        uint2 *tr = T[b] + (size_t)tid * (CSR_TBLW / 2);
-        if (has && sb + ne > (uint32_t)CSR_EXW) fl |= CSR_F_SLOTS;
-        if (has) {
-            // codes: exception ordinals + the row's slot base, clean codes as the record has them
+        if (__ballot(has)) {
+            uint32_t ne = has ? R0.w : 0u, tot = 0;
+            const uint32_t sb = wscan_excl(ne, tot);              // this row's first slot in the wave's area
+            const uint32_t xb = (uint32_t)CSR_WINMAX + wave * CSR_EXW + sb;
+            if (has && sb + ne > (uint32_t)CSR_EXW) fl |= CSR_F_SLOTS;
+            if (has) {
 #pragma unroll
-            for (int q = 0; q < 8; q++) {
-                const u32x4 Rq = q < 2 ? R1 : q < 4 ? R2 : q < 6 ? R3 : R4;
-                uint32_t c0 = (q & 1) ? Rq.z : Rq.x, c1 = (q & 1) ? Rq.w : Rq.y;
-                uint32_t lo0 = c0 & 0xFFFFu, hi0 = c0 >> 16, lo1 = c1 & 0xFFFFu, hi1 = c1 >> 16;
-                lo0 = (lo0 & CSR_EXC) ? xb + (lo0 & 0x7FFFu) : lo0;
-                hi0 = (hi0 & CSR_EXC) ? xb + (hi0 & 0x7FFFu) : hi0;
-                lo1 = (lo1 & CSR_EXC) ? xb + (lo1 & 0x7FFFu) : lo1;
-                hi1 = (hi1 & CSR_EXC) ? xb + (hi1 & 0x7FFFu) : hi1;
-                tr[q] = make_uint2(lo0 | (hi0 << 16), lo1 | (hi1 << 16));
-            }
-            if (!(fl & CSR_F_SLOTS)) {
-                uint2 *xa = EA[b] + xb;
-                uint4 *xf = EB[b] + xb;
-                if (ne > 0) { xa[0] = make_uint2(RE0a.x, RE0a.y); xf[0] = make_uint4(RE0a.z, RE0a.w, RE0b.x, RE0b.y); }
-                if (ne > 1) { xa[1] = make_uint2(RE1a.x, RE1a.y); xf[1] = make_uint4(RE1a.z, RE1a.w, RE1b.x, RE1b.y); }
-                if (ne > 2) { xa[2] = make_uint2(RE2a.x, RE2a.y); xf[2] = make_uint4(RE2a.z, RE2a.w, RE2b.x, RE2b.y); }
-                if (ne > 3) { xa[3] = make_uint2(RE3a.x, RE3a.y); xf[3] = make_uint4(RE3a.z, RE3a.w, RE3b.x, RE3b.y); }
-                for (uint32_t k = CSR_EREG; k < ne; k++) {          // more than CSR_EREG: synchronous loads (rare)
-                    const uint4 x0 = ent[2 * (R0.z + k)], x1 = ent[2 * (R0.z + k) + 1];
-                    EA[b][xb + k] = make_uint2(x0.x, x0.y);
-                    EB[b][xb + k] = make_uint4(x0.z, x0.w, x1.x, x1.y);
+                for (int q = 0; q < 4; q++) {                      // the record's 32 u16 codes
+                    const u32x4 Rq = q == 0 ? R1 : q == 1 ? R2 : q == 2 ? R3 : R4;
+                    *(u32x4 *)(trow + 8 * q) = u32x4{Rq.x & 0xFFFFu, Rq.x >> 16, Rq.y & 0xFFFFu, Rq.y >> 16};
+                    *(u32x4 *)(trow + 8 * q + 4) = u32x4{Rq.z & 0xFFFFu, Rq.z >> 16, Rq.w & 0xFFFFu, Rq.w >> 16};
                 }
-            }
-            s = (int32_t)R0.y;
-        } else {
-#pragma unroll
-            for (int q = 0; q < 8; q++) {
-                const uint32_t c = base + 4u * q;
-                tr[q] = make_uint2(c | ((c + 1u) << 16), (c + 2u) | ((c + 3u) << 16));
+                const uint32_t xa = xb * CSR_ESZ;
+                if (ne <= (uint32_t)CSR_EREG) {                    // exception codes: positions from the record
+                    const uint32_t pos = R0.z;
+                    if (ne > 0) trow[pos & 31u] = xa;
+                    if (ne > 1) trow[(pos >> 8) & 31u] = xa + CSR_ESZ;
+                    if (ne > 2) trow[(pos >> 16) & 31u] = xa + 2u * CSR_ESZ;
+                    if (ne > 3) trow[(pos >> 24) & 31u] = xa + 3u * CSR_ESZ;
+                } else {                                           // (rare) from the codes' flags
+                    for (int q = 0; q < CSR_SB; q++) {
+                        const uint32_t c = trow[q];
+                        if (c & CSR_EXC) trow[q] = xa + (c & 0x7FFFu) * CSR_ESZ;
+                    }
+                }
+                if (!(fl & CSR_F_SLOTS)) {
+                    if (ne > 0) put_entry(b, xb + 0, make_uint2(RE0a.x, RE0a.y), make_uint2(RE0a.z, RE0a.w), make_uint2(RE0b.x, RE0b.y));
+                    if (ne > 1) put_entry(b, xb + 1, make_uint2(RE1a.x, RE1a.y), make_uint2(RE1a.z, RE1a.w), make_uint2(RE1b.x, RE1b.y));
+                    if (ne > 2) put_entry(b, xb + 2, make_uint2(RE2a.x, RE2a.y), make_uint2(RE2a.z, RE2a.w), make_uint2(RE2b.x, RE2b.y));
+                    if (ne > 3) put_entry(b, xb + 3, make_uint2(RE3a.x, RE3a.y), make_uint2(RE3a.z, RE3a.w), make_uint2(RE3b.x, RE3b.y));
+                    for (uint32_t k = CSR_EREG; k < ne; k++) {      // more than CSR_EREG: synchronous loads (rare)
+                        const uint4 x0 = ent[2 * (ecur + k)], x1 = ent[2 * (ecur + k) + 1];
+                        put_entry(b, xb + k, make_uint2(x0.x, x0.y), make_uint2(x0.z, x0.w), make_uint2(x1.x, x1.y));
+                    }
+                }
+                s = (int32_t)R0.y;
             }
         }
-        return true;
+        if (was && !has) write_base();
+        was = has;
+    };
+
+    // the chain's codes for the super step: read from the row's table after its preparation (the reads complete
+    // while the waves meet at the barrier)
+    uint32_t code[CSR_SB];
+    auto load_codes = [&]() {
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const u32x4 v = *(const u32x4 *)(trow + 4 * q);
+            code[4 * q] = v.x; code[4 * q + 1] = v.y; code[4 * q + 2] = v.z; code[4 * q + 3] = v.w;
+        }
     };
 
     // super step 0
     wload(wA0, wA1, 0);
     wstore(wA0, wA1, 0);
-    if (T_ > 1) wload(wB0, wB1, 1);
-    bool tab = prep(0, 0);
+    wload(wB0, wB1, 1);
+    prep(0, 0);
     if (live && rv && R0.x == 0) { base = csr_base(p, s); rcur++; ecur += R0.w; load_rec(rcur, ecur); }
+    load_codes();
     __syncthreads();
+    CSR_STAMP(tl0);
     // (the loop runs two super steps per trip, one per buffer, so that every staging set and LDS buffer is named at
     // compile time: a buffer chosen at run time made the compiler select between the two sets' addresses and keep
     // both in scratch)
@@ -406,52 +445,30 @@ __global__ void __launch_bounds__(CSR_ROWS) k_csr(DS d, const uint32_t *list, co
         else wload(wA0, wA1, t + 2);
         // ---- the chain over blocks K0 .. K0 + 31 ----
         // The block loop is straight-line code per variant (FULL: every row's chain covers the whole super step, no
-        // predication; TAB: codes from the row's table instead of base + i), and each block's two LDS reads are
-        // issued CSR_PF blocks ahead of its arithmetic: a read followed at once by its use waits the whole LDS latency
-        // (about 120 cycles with four waves reading), twice the chain's own cost of a block.
+        // predication), and each block's three LDS reads are issued CSR_PF blocks ahead of its arithmetic: a read
+        // followed at once by its use waits the whole LDS latency (about 120 cycles with four waves reading), twice
+        // the chain's own cost of a block.
         CSR_STAMP(ts0);
         const bool full = __all(myit == 0u || K0 + CSR_SB <= myit);
-        const uint2 *EAb = EA[b];
-        const uint4 *EBb = EB[b];
-        auto run = [&](auto FULLC, auto TABC) {
+        const char *EAb = (const char *)EA[b], *EBb = (const char *)EB[b];
+        auto run = [&](auto FULLC) {
             constexpr bool FULL = decltype(FULLC)::value;
-            constexpr bool TAB = decltype(TABC)::value;
-            uint32_t code[CSR_SB];
-            if (TAB) {
-                const uint2 *tr = T[b] + (size_t)tid * (CSR_TBLW / 2);
-#pragma unroll
-                for (int q = 0; q < 8; q++) {
-                    const uint2 cc = tr[q];
-                    code[4 * q + 0] = cc.x & 0xFFFFu;
-                    code[4 * q + 1] = cc.x >> 16;
-                    code[4 * q + 2] = cc.y & 0xFFFFu;
-                    code[4 * q + 3] = cc.y >> 16;
-                }
-            }
-            uint2 vg[CSR_PF + 1];
-            uint4 vf[CSR_PF + 1];
+            u32x4 va[CSR_PF + 1], vb[CSR_PF + 1];
             auto fetch = [&](int i) {
-#ifdef CSR_DIAG_BCAST
-                // (diagnostic build only: every lane reads lane 0's entry, wrong checksums, no bank conflicts)
-                const uint32_t e = (uint32_t)__builtin_amdgcn_readfirstlane((int)(TAB ? code[i] : base + (uint32_t)i));
-#else
-                const uint32_t e = TAB ? code[i] : base + (uint32_t)i;
-#endif
-                vg[i % (CSR_PF + 1)] = EAb[e];
-                vf[i % (CSR_PF + 1)] = EBb[e];
+                va[i % (CSR_PF + 1)] = *(const u32x4 *)(EAb + code[i]);
+                vb[i % (CSR_PF + 1)] = *(const u32x4 *)(EBb + code[i]);
             };
 #pragma unroll
             for (int i = 0; i < CSR_PF; i++) fetch(i);
 #pragma unroll
             for (int i = 0; i < CSR_SB; i++) {
                 if (i + CSR_PF < CSR_SB) fetch(i + CSR_PF);
-                const uint2 g = vg[i % (CSR_PF + 1)];
-                const uint4 f = vf[i % (CSR_PF + 1)];
+                const u32x4 A = va[i % (CSR_PF + 1)], B = vb[i % (CSR_PF + 1)];
                 if (FULL) {
-                    csr_block(Xg, Xf, Xh, g, f);
+                    csd_block3(Xg, Xf, Xh, A.x, A.y, A.z, A.w, B.x, B.y);
                 } else {
                     uint32_t ng = Xg, nf = Xf, nh = Xh;
-                    csr_block(ng, nf, nh, g, f);
+                    csd_block3(ng, nf, nh, A.x, A.y, A.z, A.w, B.x, B.y);
                     const bool act = K0 + (uint32_t)i < myit;
                     Xg = act ? ng : Xg;
                     Xf = act ? nf : Xf;
@@ -459,39 +476,39 @@ __global__ void __launch_bounds__(CSR_ROWS) k_csr(DS d, const uint32_t *list, co
                 }
             }
         };
-        using TT = std::integral_constant<bool, true>;
-        using FF = std::integral_constant<bool, false>;
-        if (full && !tab) run(TT{}, FF{});
-        else if (full) run(TT{}, TT{});
-        else if (!tab) run(FF{}, FF{});
-        else run(FF{}, TT{});
+        if (full) run(std::integral_constant<bool, true>{});
+        else run(std::integral_constant<bool, false>{});
         // ---- the next super step's window, rows and entries into the other buffer ----
         // (kept after the chain: hoisted above it, the stores of a staging set would wait for its loads there)
         asm volatile("" ::: "memory");
         CSR_STAMP(ts1);
         CSR_ACC(0, ts1 - ts0);
-        if (t + 1 < T_) {
-            if constexpr (b) wstore(wA0, wA1, 0u);                  // super step t + 1 (even) -> buffer 0
-            else wstore(wB0, wB1, 1u);
-            tab = prep(t + 1, b ^ 1u);
-            // (the record loads run for the whole wave whenever one of its rows moves on, the others reloading their
-            // current record: a load into only some lanes keeps the old values live in the rest, and the compiler
-            // copies the loaded registers over them, waiting for the loads right here)
-            const bool adv = live && rv && R0.x == t + 1;
-            if (adv) { base = csr_base(p, s); rcur++; ecur += R0.w; }
-            if (__ballot(adv)) load_rec(rcur, ecur);
-        }
+        // (run after the last super step too, into a buffer nobody reads: skipped on one path, the staging set's loads
+        // stay pending on it, and the compiler waits for every load at the loop head before reusing their registers)
+        if constexpr (b) wstore(wA0, wA1, 0u);                      // super step t + 1 (even) -> buffer 0
+        else wstore(wB0, wB1, 1u);
+        prep(t + 1, b ^ 1u);
+        // (the record loads run for the whole wave whenever one of its rows moves on, the others reloading their
+        // current record: a load into only some lanes keeps the old values live in the rest, and the compiler
+        // copies the loaded registers over them, waiting for the loads right here)
+        const bool adv = live && rv && R0.x == t + 1;
+        if (adv) { base = csr_base(p, s); rcur++; ecur += R0.w; }
+        if (__ballot(adv)) load_rec(rcur, ecur);
+        load_codes();
         CSR_STAMP(ts2);
         __syncthreads();
         CSR_STAMP(ts3);
         CSR_ACC(1, ts2 - ts1);
         CSR_ACC(2, ts3 - ts2);
     };
-    CSR_STAMP(tl0);
-    for (uint32_t t = 0; t < T_; t += 2) {
+    // (both super steps of a trip always run, the odd last one after the loop: the loop head is then reached from
+    // one kind of trip only, and the loads in flight there are always the same)
+    uint32_t t = 0;
+    for (; t + 1 < T_; t += 2) {
         iter(t, std::integral_constant<uint32_t, 0>{});
-        if (t + 1 < T_) iter(t + 1, std::integral_constant<uint32_t, 1>{});
+        iter(t + 1, std::integral_constant<uint32_t, 1>{});
     }
+    if (t < T_) iter(t, std::integral_constant<uint32_t, 0>{});
     CSR_STAMP(tl1);
     CSR_ACC(3, tl1 - tl0);
 #ifdef CSR_DIAG_STAMP

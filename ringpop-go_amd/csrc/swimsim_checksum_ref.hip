@@ -49,6 +49,7 @@ struct CsdArgs {
     uint32_t *fb_list, *fb_cnt; // rows left to the production kernels; fb_cnt[1 + b]: rows with flag bit b
     const uint32_t *ulist;    // divergent columns in member order (DS::colx), or null: k_csd_scan reads every column
     const uint32_t *ucnt;     // their number
+    const uint4 *ucol;        // per divergent column c: {m, B[m], O_B[m], O_B[m - 1]} (k_csr_ucol)
     uint32_t dmode;           // diagnostics library only (swimsim_bench_checksum modes 31..46 = dmode + 30, garbage
                               // checksums): 1 helpers alone, 2 chains alone, 3 helpers without the exception work; bit 8:
                               // no barrier between super steps. Ignored by the product library (CSD_DMODE)
@@ -146,6 +147,14 @@ __global__ void __launch_bounds__(1024) k_csr_ulist(DS d, uint32_t *ulist, uint3
         }
     }
     if (t == 1023) *ucnt = part[1023];
+}
+
+// the divergent columns' scan table: what k_csd_scan needs of B at each, in one 16-B load
+__global__ void k_csr_ucol(const uint32_t *ulist, const uint32_t *ucnt, const uint32_t *B, const uint32_t *OB, uint4 *ucol) {
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= *ucnt) return;
+    const uint32_t m = ulist[c];
+    ucol[c] = make_uint4(m, B[m], OB[m], OB[m ? m - 1u : 0u]);
 }
 
 template <int W>
@@ -314,15 +323,28 @@ __global__ void __launch_bounds__(256) k_csd_scan(DS d, const uint32_t *list, ui
     const uint32_t ucnt = a.ulist ? *a.ucnt : N;
     const bool UL = a.ulist && ucnt <= N / 4;
     const uint32_t ncol = UL ? ucnt : N;
+    // (divergent columns come with their B word and offsets from the column table: one dependent load less)
+    const bool ULc = UL && a.ucol;
     for (uint32_t c00 = 0; c00 < ncol && !flags; c00 += 64 * CSD_SU) {
-        uint32_t wv_[CSD_SU], bv_[CSD_SU], mv_[CSD_SU];
+        uint32_t wv_[CSD_SU], bv_[CSD_SU], mv_[CSD_SU], ov_[CSD_SU], o1_[CSD_SU];
+        if (ULc) {
 #pragma unroll
-        for (uint32_t k = 0; k < CSD_SU; k++) {
-            const uint32_t c = c00 + 64 * k + lane;
-            const uint32_t m = c < ncol ? (UL ? a.ulist[c] : c) : 0u;
-            mv_[k] = m;
-            wv_[k] = c < ncol ? row[m] : 0u;
-            bv_[k] = c < ncol ? a.B[m] : 0u;
+            for (uint32_t k = 0; k < CSD_SU; k++) {
+                const uint32_t c = c00 + 64 * k + lane;
+                const uint4 u = a.ucol[c < ncol ? c : 0u];
+                mv_[k] = u.x; bv_[k] = u.y; ov_[k] = u.z; o1_[k] = u.w;
+                wv_[k] = row[u.x];
+                if (c >= ncol) bv_[k] = wv_[k];                    // (past the list: equal, no diff)
+            }
+        } else {
+#pragma unroll
+            for (uint32_t k = 0; k < CSD_SU; k++) {
+                const uint32_t c = c00 + 64 * k + lane;
+                const uint32_t m = c < ncol ? (UL ? a.ulist[c] : c) : 0u;
+                mv_[k] = m;
+                wv_[k] = c < ncol ? row[m] : 0u;
+                bv_[k] = c < ncol ? a.B[m] : 0u;
+            }
         }
         uint64_t mk[CSD_SU];
         uint64_t any = 0;
@@ -332,11 +354,12 @@ __global__ void __launch_bounds__(256) k_csd_scan(DS d, const uint32_t *list, ui
             any |= mk[k];
         }
         if (!any) continue;
-        uint32_t ov_[CSD_SU], o1_[CSD_SU];
+        if (!ULc) {
 #pragma unroll
-        for (uint32_t k = 0; k < CSD_SU; k++) {
-            ov_[k] = a.OB[mv_[k]];
-            o1_[k] = a.OB[mv_[k] ? mv_[k] - 1u : 0u];
+            for (uint32_t k = 0; k < CSD_SU; k++) {
+                ov_[k] = a.OB[mv_[k]];
+                o1_[k] = a.OB[mv_[k] ? mv_[k] - 1u : 0u];
+            }
         }
 #pragma unroll
         for (uint32_t k = 0; k < CSD_SU; k++) {
@@ -394,6 +417,29 @@ __device__ __forceinline__ void csd_gf_step(uint32_t &Xg, uint32_t &Xf, uint32_t
                  "v_add3_u32 %0, %2, %1, %5"
                  : "+v"(Xg), "+v"(Xf), "=&v"(tg), "=&v"(tf)
                  : "v"(mg), "v"(dd), "v"(mf), "v"(pf));
+}
+// one block of all three lanes as one sequence, the g, f and h instructions interleaved so that every instruction's
+// operands were produced at least two instructions earlier (also across consecutive blocks): a dependent integer VALU
+// instruction issues about 10 cycles after its producer, an independent one every 5, so the block runs at the issue
+// rate, 12 instructions. (csd_gf_step followed by csd_h_step leaves the four h instructions back to back: the compiler
+// does not interleave separate asm statements.)
+__device__ __forceinline__ void csd_block3(uint32_t &Xg, uint32_t &Xf, uint32_t &Xh, uint32_t mg, uint32_t dd, uint32_t mf,
+                                           uint32_t pf, uint32_t mh, uint32_t kh) {
+    uint32_t tg, tf;
+    asm volatile("v_xor_b32 %4, %1, %7\n\t"
+                 "v_xor_b32 %3, %0, %5\n\t"
+                 "v_xor_b32 %2, %2, %9\n\t"
+                 "v_alignbit_b32 %4, %4, %4, 19\n\t"
+                 "v_alignbit_b32 %3, %3, %3, 19\n\t"
+                 "v_alignbit_b32 %2, %2, %2, 19\n\t"
+                 "v_lshl_add_u32 %3, %3, 2, %3\n\t"
+                 "v_lshl_add_u32 %4, %4, 2, %4\n\t"
+                 "v_lshl_add_u32 %2, %2, 2, %2\n\t"
+                 "v_add3_u32 %1, %4, %3, %8\n\t"
+                 "v_add_u32 %2, %2, %10\n\t"
+                 "v_add3_u32 %0, %3, %1, %6"
+                 : "+v"(Xg), "+v"(Xf), "+v"(Xh), "=&v"(tg), "=&v"(tf)
+                 : "v"(mg), "v"(dd), "v"(mf), "v"(pf), "v"(mh), "v"(kh));
 }
 // one block of the h lane: Xh' = 5 ror(Xh ^ Mh, 19) + KH
 __device__ __forceinline__ void csd_h_step(uint32_t &Xh, uint32_t mh, uint32_t kh) {

@@ -352,6 +352,7 @@ struct swimsim {
     CsrRec *csr_rec = nullptr;
     uint32_t csr_ecap = 2048, csr_rcap = 512, csr_KP = 0;
     uint32_t *csr_ulist = nullptr, *csr_ucnt = nullptr; // the divergent columns (DS::colx) in member order
+    uint4 *csr_ucol = nullptr;                          // and their scan table (k_csr_ucol)
     uint32_t csr_maxdiff = 0;                     // swimsim_tuning.cs_ref_maxdiff: mean differing members per sampled
                                                   // row above which a launch keeps the production kernels (0: never)
     uint64_t csr_launches = 0, csr_fallback_rows = 0, csr_declined = 0;
@@ -833,7 +834,8 @@ int csr_alloc(swimsim *h) {
         (rc = dalloc(h, &h->csr_rec, (size_t)rows * h->csr_rcap, "csr records")) ||
         (rc = dalloc(h, &h->csr_nrec, (size_t)rows, "csr record counts")) ||
         (rc = dalloc(h, &h->csr_ulist, (size_t)h->N, "csr divergent columns")) ||
-        (rc = dalloc(h, &h->csr_ucnt, 1, "csr divergent column count"))) {
+        (rc = dalloc(h, &h->csr_ucnt, 1, "csr divergent column count")) ||
+        (rc = dalloc(h, &h->csr_ucol, (size_t)h->N, "csr divergent column table"))) {
         h->csr_failed = true;                                      // the production kernels stay in charge
         h->err.clear();
         return rc;
@@ -868,6 +870,7 @@ int csr_hash(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t n, 
     ca.ecap = h->csr_ecap;
     ca.ulist = h->csr_ulist;
     ca.ucnt = h->csr_ucnt;
+    ca.ucol = h->csr_ucol;
     CsrArgs a{};
     a.P = h->csr_P;
     a.KP = h->csr_KP;
@@ -895,6 +898,8 @@ int csr_hash(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t n, 
         HIPCHK(h, hipcub::DeviceScan::ExclusiveSum(h->cub_tmp, bytes, h->csr_Lb, h->csr_OB, (int)h->N + 1, h->s));
         HIPCHK(h, hipMemsetAsync(h->csr_SBw, 0, h->csr_sbw_words * 4, h->s));
         hipLaunchKernelGGL(k_csr_ulist, dim3(1), dim3(1024), 0, h->s, h->d, h->csr_ulist, h->csr_ucnt);
+        hipLaunchKernelGGL(k_csr_ucol, dim3((h->N + 255) / 256), dim3(256), 0, h->s, h->csr_ulist, h->csr_ucnt, h->csr_B,
+                           h->csr_OB, h->csr_ucol);
         launch_csr(h->d, list, n, cnt, ca, a, h->s, 0);
         launch_csr(h->d, list, n, cnt, ca, a, h->s, 1);
         launch_csr(h->d, list, n, cnt, ca, a, h->s, 2);
