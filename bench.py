@@ -292,6 +292,7 @@ def main():
     ap.add_argument("--host-transport", action="store_true")
     # the reference-row checksum path (swimsim_tuning.cs_ref: 0 off, 1 wide launches; default: the library's)
     ap.add_argument("--cs-ref", type=int, default=-1)
+    ap.add_argument("--cs-ref-maxdiff", type=int, default=-1)
     # test hook: the ranks report (rank, world size) and exit before any GPU call
     ap.add_argument("--launch-check", action="store_true")
     args = ap.parse_args()
@@ -336,7 +337,7 @@ def main():
 
     n = args.members
     total_rounds = args.warmup + args.steps
-    tuning = {"cs_ref": args.cs_ref} if args.cs_ref >= 0 else None
+    tuning = {k: v for k, v in (("cs_ref", args.cs_ref), ("cs_ref_maxdiff", args.cs_ref_maxdiff)) if v >= 0} or None
     wl = W.config3(n=n, rounds=max(total_rounds, KILL_ROUND + 1), kill_round=KILL_ROUND)
     nkilled = sum(1 for e in wl.events if e[1] == W.EV_KILL)
     if ws > 1:
@@ -418,6 +419,7 @@ def main():
                          "merge_kernel": entries.get("recv_merge")},
             "kernel_ms": {k: round(v["avg_ms"] * v["launches"], 3) for k, v in kt.items()},
             "counters": counters,
+            "checksum_paths": eng.checksum_path_stats(),
         }
         if line["roofline"]["bound"] == "valu":
             line["roofline"]["bound_frac"] = (dom.get("valu") or {}).get("frac")

@@ -75,10 +75,10 @@ typedef struct swimsim_tuning {
     int32_t cs_async_rows;    /* phase-C launches of at most this many rows go to the side stream; default 12,288 */
     int32_t cs_narrow_rows;   /* launches of at most this many rows use the narrow checksum kernel; 0 = the wide
                                  kernel only; default 8,192 */
-    int32_t cs_ref;           /* the reference-row checksum path: 0 off, 1 wide launches, 2 every launch
-                                 of at least 1,024 rows */
+    int32_t cs_ref;           /* the reference-row checksum path: 0 off, 1 wide launches (default), 2
+                                 every launch of at least 1,024 rows */
     int32_t cs_ref_maxdiff;   /* the path declines a launch whose sampled rows differ from the reference in more than
-                                 this many members on average; 0 = never declines */
+                                 this many members on average; 0 = never declines (default) */
 } swimsim_tuning;
 
 /* Events applied in phase E of a round (docs/ROUND_SEMANTICS.md §4). */

@@ -28,7 +28,9 @@
 constexpr int CSR_ROWS = 256;          // rows per workgroup (4 waves)
 constexpr int CSR_SB = 32;             // blocks per super step
 constexpr int CSR_WINMAX = 1024;       // window entries per buffer: phases in use x Wn
-constexpr int CSR_EXW = 128;           // exception entries per wave per buffer
+constexpr int CSR_EXW = 384;           // exception entries per wave per buffer (128: a third of the rows of heavy cascade
+                                       // rounds fell back, a differing column giving every row of a wave exceptions;
+                                       // 192: still an eighth in the heaviest)
 constexpr int CSR_ENT = CSR_WINMAX + 4 * CSR_EXW;   // entries per buffer
 constexpr int CSR_TW = 36;             // u32 words per row of the code table (32 codes + pad: ds_read_b128 conflict-free)
 constexpr uint32_t CSR_ESZ = 16;       // a code's unit: an entry's byte offset in each of the two entry arrays
@@ -221,8 +223,10 @@ __global__ void __launch_bounds__(CSR_ROWS) k_csr(DS d, const uint32_t *list, co
     // reads do not (three ds_read_b64 per block of 24-B entries: 10.3 ms per launch against 8.5 for one b64 + one b128).
     // Two rows of a 16-lane group conflict when their entries are 16 apart; with Wn = 1 mod 32 the phases' windows
     // start at different residues.
+    // (EB holds both buffers in each 16-B entry, buffer b in bytes 8b..8b+7: a ds_read_b128 of the whole entry and
+    // the compile-time buffer's half, with 16 KB more for exception slots)
     __shared__ uint4 EA[2][CSR_ENT];
-    __shared__ uint4 EB[2][CSR_ENT];
+    __shared__ uint4 EB[CSR_ENT];
     // per row: the byte addresses of its 32 blocks' entries in the super step (one table, not one per buffer: a row's
     // table is read and written only by its own lane, and rewritten only when its codes change)
     __shared__ uint32_t T[CSR_ROWS * CSR_TW];
@@ -333,7 +337,7 @@ __global__ void __launch_bounds__(CSR_ROWS) k_csr(DS d, const uint32_t *list, co
     };
     auto put_entry = [&](uint32_t b, uint32_t e, uint2 x, uint2 y, uint2 z) {
         EA[b][e] = make_uint4(x.x, x.y, y.x, y.y);
-        *(uint2 *)&EB[b][e] = z;
+        ((uint2 *)&EB[e])[b] = z;
     };
     auto wstore = [&](const u32x4 (&wst0)[WV], const u32x2 (&wst1)[WV], uint32_t b) {
 #pragma unroll
@@ -450,7 +454,7 @@ __global__ void __launch_bounds__(CSR_ROWS) k_csr(DS d, const uint32_t *list, co
         // the chain's own cost of a block.
         CSR_STAMP(ts0);
         const bool full = __all(myit == 0u || K0 + CSR_SB <= myit);
-        const char *EAb = (const char *)EA[b], *EBb = (const char *)EB[b];
+        const char *EAb = (const char *)EA[b], *EBb = (const char *)EB;
         auto run = [&](auto FULLC) {
             constexpr bool FULL = decltype(FULLC)::value;
             u32x4 va[CSR_PF + 1], vb[CSR_PF + 1];
@@ -465,10 +469,10 @@ __global__ void __launch_bounds__(CSR_ROWS) k_csr(DS d, const uint32_t *list, co
                 if (i + CSR_PF < CSR_SB) fetch(i + CSR_PF);
                 const u32x4 A = va[i % (CSR_PF + 1)], B = vb[i % (CSR_PF + 1)];
                 if (FULL) {
-                    csd_block3(Xg, Xf, Xh, A.x, A.y, A.z, A.w, B.x, B.y);
+                    csd_block3(Xg, Xf, Xh, A.x, A.y, A.z, A.w, b ? B.z : B.x, b ? B.w : B.y);
                 } else {
                     uint32_t ng = Xg, nf = Xf, nh = Xh;
-                    csd_block3(ng, nf, nh, A.x, A.y, A.z, A.w, B.x, B.y);
+                    csd_block3(ng, nf, nh, A.x, A.y, A.z, A.w, b ? B.z : B.x, b ? B.w : B.y);
                     const bool act = K0 + (uint32_t)i < myit;
                     Xg = act ? ng : Xg;
                     Xf = act ? nf : Xf;
@@ -524,6 +528,10 @@ __global__ void __launch_bounds__(CSR_ROWS) k_csr(DS d, const uint32_t *list, co
     if (!mine) {                                                    // left to the production kernels
         const uint32_t at = atomicAdd(a.fb_cnt, 1u);
         a.fb_list[at] = id;
+        // by reason (swimsim_checksum_path_stats): short, entry/run capacity, window plan, record capacity, slots
+        const uint32_t r = (fl & CSD_F_SHORT) ? 0u : (fl & CSD_F_ECAP) ? 1u : (fl & CSR_F_PLAN) ? 2u : (fl & CSR_F_RCAP) ? 3u
+                         : (fl & CSR_F_SLOTS) ? 4u : 6u;
+        atomicAdd(a.fb_cnt + 1 + r, 1u);
         return;
     }
     fh.h = Xh; fh.g = Xg; fh.f = Xf;

@@ -239,11 +239,14 @@ __device__ void csd_run_entries(const DS &d, const uint32_t *row, uint32_t m0, u
 
 template <int W>
 __global__ void __launch_bounds__(256) k_csd_scan(DS d, const uint32_t *list, uint32_t n, CsdArgs a) {
-    // CSD_SU chunks of 64 members per pass, their loads in flight together (a row is one 256-KB stream). The pass's
-    // differing members are walked in order by the whole wave, each one's word, B word and B offsets read from the
-    // lane that loaded them (v_readlane: no LDS staging, no load inside the walk); runs wait in LDS for their
+    // CSD_SU chunks of 64 members per pass, their loads in flight together (a row is one 256-KB stream). A chunk's
+    // differing members are taken together, one per lane: the shift before each is a wave prefix sum of the record
+    // length differences, a member starts a new run of exception blocks when its first block lies past the previous
+    // differing member's last block + 1 (their last blocks grow with the member), and each run start closes the run
+    // before it (prefix sums place the closed runs and their entries). Round 4's first version walked the members one
+    // at a time (the whole wave, scalar): 5.9 ms per launch on a heavy cascade round. Runs wait in LDS for their
     // entries, generated (one lane per run) between passes.
-    constexpr uint32_t CSD_SU = 8, RUNCAP = 128, RUNFLUSH = 64;
+    constexpr uint32_t CSD_SU = 8, RUNCAP = 256, RUNFLUSH = 128;
     __shared__ uint32_t runs[4][RUNCAP][6];                         // {klo, khi, m0, o0, s_after, first entry}
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
     const uint32_t i = blockIdx.x * 4 + wv;
@@ -268,7 +271,8 @@ __global__ void __launch_bounds__(256) k_csd_scan(DS d, const uint32_t *list, ui
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
-    auto flush = [&]() {
+    // (forced inline: called from more than one place, the compiler made it a call that copies the DS block to scratch)
+    auto flush = [&]() __attribute__((always_inline)) {
         wsync();
         for (uint32_t q0 = 0; q0 < nruns; q0 += 64) {
             if (q0 + lane < nruns) {
@@ -281,7 +285,8 @@ __global__ void __launch_bounds__(256) k_csd_scan(DS d, const uint32_t *list, ui
     };
     auto close_run = [&](int32_t s_after) {
         const uint32_t nb = rhi - rlo + 1;
-        if (e + nb > a.ecap || nruns == RUNCAP) { flags |= CSD_F_ECAP; return; }
+        if (nruns == RUNCAP) flush();                               // (wave-uniform here: the walk is the whole wave's)
+        if (e + nb > a.ecap) { flags |= CSD_F_ECAP; return; }
         if (lane == 0) {
             uint32_t *q = runs[wv][nruns];
             q[0] = rlo; q[1] = rhi; q[2] = rm0; q[3] = ro0; q[4] = (uint32_t)s_after; q[5] = e;
@@ -294,29 +299,80 @@ __global__ void __launch_bounds__(256) k_csd_scan(DS d, const uint32_t *list, ui
         e += nb;
         nruns++;
     };
-    // member mm differs: row word wm, B word bm, B offsets obm = O_B[mm] and ob1 = O_B[mm - 1]
-    auto diff = [&](uint32_t mm, uint32_t wm, uint32_t bm, uint32_t obm, uint32_t ob1) {
-        const int32_t Lr = (int32_t)csd_reclen(d, wm), Lbm = (int32_t)csd_reclen(d, bm);
-        const int32_t x = (int32_t)obm + s, y = x + Lr;             // the record's bytes in the row: [x, y)
+    auto wred = [&](int32_t v, int op) -> int32_t {                 // wave min (0), max (1) or or (2)
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const int32_t y = __shfl_xor(v, off, 64);
+            v = op == 0 ? min(v, y) : op == 1 ? max(v, y) : (v | y);
+        }
+        return v;
+    };
+    // one chunk: m = its differing lanes; this lane's member mm, row word wm, B word bm, O_B[mm], O_B[mm - 1]
+    auto chunk = [&](uint64_t m, uint32_t mm, uint32_t wm, uint32_t bm, uint32_t obm, uint32_t ob1) {
+        const bool dl = (m >> lane) & 1ull;
+        const int32_t Lr = dl ? (int32_t)csd_reclen(d, wm) : 0, Lbm = dl ? (int32_t)csd_reclen(d, bm) : 0;
+        uint32_t tot;
+        const int32_t sb = s + (int32_t)wscan_excl((uint32_t)(Lr - Lbm), tot);   // the shift before this member
+        const int32_t x = (int32_t)obm + sb, y = x + Lr;            // the record's bytes in the row: [x, y)
         // blocks whose 32 bytes [20k, 20k + 32) meet [x, y) (or straddle x when the record is empty)
         const int32_t klo = x >= 32 ? (x - 32) / 20 + 1 : 0;
         int32_t khi = y >= 1 ? (y - 1) / 20 : -1;
         if (khi > (int32_t)kl) khi = (int32_t)kl;
-        if (klo <= (int32_t)kl && khi >= klo) {
-            if ((uint32_t)klo <= rhi + 1) {
-                rhi = max(rhi, (uint32_t)khi);
-            } else {
-                close_run(s);
-                // the new run starts at row byte p = 20 klo, in the clean bytes before mm (shift s): the record
-                // holding B offset t = p - s is the last member below mm with O_B <= t
-                // (mm >= 1 here: member 0's record meets block 0, which always begins a run)
-                const uint32_t t = (uint32_t)(20 * klo - s);
-                uint32_t m0 = mm - 1, om = ob1;
-                while (m0 > 0 && om > t) om = a.OB[--m0];
-                rlo = (uint32_t)klo; rhi = (uint32_t)khi; rm0 = m0; ro0 = t - om;
-            }
+        const bool vd = dl && klo <= (int32_t)kl && khi >= klo;
+        // the last block of every run before this member: the open run's, or the previous valid member's (a prefix max)
+        int32_t px = vd ? khi : (-0x7FFFFFFF - 1);
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int32_t yv = __shfl_up(px, off, 64);
+            if (lane >= (uint32_t)off) px = max(px, yv);
         }
-        s += Lr - Lbm;
+        const int32_t pxe = __shfl_up(px, 1, 64);                   // (exclusive: the lanes below this one)
+        const int32_t pk = lane ? max(pxe, (int32_t)rhi) : (int32_t)rhi;
+        const bool st = vd && klo > pk + 1;                         // this member begins a new run
+        const uint64_t sm = __ballot(st);
+        if (sm == 0) {                                              // every valid member extends the open run
+            rhi = (uint32_t)max((int32_t)rhi, wred(vd ? khi : (-0x7FFFFFFF - 1), 1));
+            s += (int32_t)tot;
+            return;
+        }
+        // a new run starts at row byte p = 20 klo, in the clean bytes before mm (shift sb): the record holding B offset
+        // t = p - sb is the last member below mm with O_B <= t (mm >= 1: member 0's record meets block 0, which always
+        // begins a run)
+        uint32_t m0 = 0, o0 = 0;
+        if (st) {
+            const uint32_t t = (uint32_t)(20 * klo - sb);
+            uint32_t q = mm - 1, om = ob1;
+            while (q > 0 && om > t) om = a.OB[--q];
+            m0 = q;
+            o0 = t - om;
+        }
+        // each start closes the run before it: the previous start's, or the open run
+        const uint64_t below = sm & ((1ull << lane) - 1ull);
+        const uint32_t src = below ? 63u - (uint32_t)__builtin_clzll(below) : 0u;
+        const uint32_t plo = (uint32_t)__shfl(klo, (int)src, 64), pm0 = (uint32_t)__shfl((int)m0, (int)src, 64),
+                       po0 = (uint32_t)__shfl((int)o0, (int)src, 64);
+        const uint32_t clo = below ? plo : rlo, cm0 = below ? pm0 : rm0, co0 = below ? po0 : ro0, chi = (uint32_t)pk;
+        uint32_t ntot;
+        const uint32_t eo = wscan_excl(st ? chi - clo + 1 : 0u, ntot);
+        const uint32_t K = (uint32_t)__popcll(sm);
+        if (e + ntot > a.ecap) { flags |= CSD_F_ECAP; return; }
+        if (st) {
+            uint32_t *q = runs[wv][nruns + (uint32_t)__popcll(below)];
+            q[0] = clo; q[1] = chi; q[2] = cm0; q[3] = co0; q[4] = (uint32_t)sb; q[5] = e + eo;
+        }
+        const bool cs = st && chi < kl;                             // clean blocks follow the closed run at shift sb
+        smin = min(smin, wred(cs ? sb : 0x7FFFFFFF, 0));
+        smax = max(smax, wred(cs ? sb : (-0x7FFFFFFF - 1), 1));
+        phm |= (uint32_t)wred(cs ? (int32_t)(1u << csd_phase(sb)) : 0, 2);
+        e += ntot;
+        nruns += K;
+        // the last start's run stays open
+        const uint32_t ll = 63u - (uint32_t)__builtin_clzll(sm);
+        rlo = (uint32_t)__shfl(klo, (int)ll, 64);
+        rm0 = (uint32_t)__shfl((int)m0, (int)ll, 64);
+        ro0 = (uint32_t)__shfl((int)o0, (int)ll, 64);
+        rhi = (uint32_t)wred(vd && lane >= ll ? khi : (-0x7FFFFFFF - 1), 1);
+        s += (int32_t)tot;
     };
     // the columns to compare: every member, or only the divergent columns (DS::colx: outside them every row, and
     // every snapshot of a row, holds the same word, so it equals the majority B there) when they are few
@@ -361,15 +417,12 @@ __global__ void __launch_bounds__(256) k_csd_scan(DS d, const uint32_t *list, ui
                 o1_[k] = a.OB[mv_[k] ? mv_[k] - 1u : 0u];
             }
         }
+        // (unrolled: the pass's values stay in registers; picked by a run-time chunk index, they went to memory)
 #pragma unroll
         for (uint32_t k = 0; k < CSD_SU; k++) {
-            uint64_t mask = mk[k];
-            while (mask && !flags) {                                // the chunk's differing members, in order
-                const uint32_t l = (uint32_t)__builtin_ctzll(mask);
-                mask &= mask - 1;
-                diff((uint32_t)__builtin_amdgcn_readlane((int)mv_[k], (int)l), (uint32_t)__builtin_amdgcn_readlane((int)wv_[k], (int)l),
-                     (uint32_t)__builtin_amdgcn_readlane((int)bv_[k], (int)l), (uint32_t)__builtin_amdgcn_readlane((int)ov_[k], (int)l),
-                     (uint32_t)__builtin_amdgcn_readlane((int)o1_[k], (int)l));
+            if (mk[k] && !flags) {
+                if (nruns + 64 > RUNCAP) flush();                   // (a chunk closes at most 64 runs)
+                chunk(mk[k], mv_[k], wv_[k], bv_[k], ov_[k], o1_[k]);
             }
         }
         if (nruns >= RUNFLUSH) flush();

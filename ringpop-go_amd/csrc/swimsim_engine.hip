@@ -340,7 +340,8 @@ struct swimsim {
     uint4 *wout = nullptr;
     uint32_t *winfo = nullptr;
     // reference-row checksum path (swimsim_checksum_ref.hip + swimsim_checksum_csr.hip), allocated at its first launch
-    int csr_mode = 0;                             // swimsim_tuning.cs_ref: 0 off, 1 wide launches, 2 every launch of
+    // (on for wide launches by default: the bench window runs 9.51 against 10.48 ms per round)
+    int csr_mode = 1;                             // swimsim_tuning.cs_ref: 0 off, 1 wide launches, 2 every launch of
                                                   // at least CSD_MIN_ROWS rows
     bool csr_ready = false, csr_failed = false;
     uint32_t *csr_B = nullptr, *csr_Lb = nullptr, *csr_OB = nullptr, *csr_SBw = nullptr, *csr_fb = nullptr,
@@ -350,12 +351,14 @@ struct swimsim {
     CsdRow *csr_rinfo = nullptr;
     CsrPlan *csr_plan = nullptr;
     CsrRec *csr_rec = nullptr;
-    uint32_t csr_ecap = 2048, csr_rcap = 512, csr_KP = 0;
+    uint32_t csr_ecap = 4096, csr_rcap = 512, csr_KP = 0;    // (2,048 entries: rows far from the reference fell back)
     uint32_t *csr_ulist = nullptr, *csr_ucnt = nullptr; // the divergent columns (DS::colx) in member order
     uint4 *csr_ucol = nullptr;                          // and their scan table (k_csr_ucol)
     uint32_t csr_maxdiff = 0;                     // swimsim_tuning.cs_ref_maxdiff: mean differing members per sampled
-                                                  // row above which a launch keeps the production kernels (0: never)
-    uint64_t csr_launches = 0, csr_fallback_rows = 0, csr_declined = 0;
+                                                  // row above which a launch keeps the production kernels (0: never;
+                                                  // the default: a decline costs a host synchronisation mid-round, and
+                                                  // the path no longer loses on heavy rounds)
+    uint64_t csr_launches = 0, csr_fallback_rows = 0, csr_declined = 0, csr_reasons[7] = {0};
 #ifdef SWIMSIM_DIAG
     // reference-row checksum path (swimsim_checksum_delta.hip), allocated at its first launch
     int csd_mode = 0;                             // SWIMSIM_CS_DELTA: 0 off, 1 wide launches, 2 every launch >= 1024 rows
@@ -817,7 +820,9 @@ bool csr_wanted(swimsim *h, uint32_t n, CsKind kind) {
 
 int csr_alloc(swimsim *h) {
     if (h->csr_ready) return 0;
-    const uint32_t rows = h->NL + h->d.dense_cap;                    // a launch lists rows and dense snapshots
+    // (per listed row of one launch: sized for NL rows; the few launches that list more rows and dense snapshots
+    // together keep the production kernels, csr_hash)
+    const uint32_t rows = h->NL;
     h->csr_sbw_words = ((size_t)h->N * (h->W + 32) + 256) / 4;
     h->csr_KP = (uint32_t)(h->csr_sbw_words * 4 / 20 + 2);
     int rc = 0;
@@ -827,7 +832,7 @@ int csr_alloc(swimsim *h) {
         (rc = dalloc(h, &h->csr_SBw, h->csr_sbw_words, "csr reference string")) ||
         (rc = dalloc(h, &h->csr_P, (size_t)20 * h->csr_KP * 2, "csr premix table")) ||
         (rc = dalloc(h, &h->csr_fb, (size_t)rows, "csr fallback list")) ||
-        (rc = dalloc(h, &h->csr_fbcnt, 1, "csr fallback count")) ||
+        (rc = dalloc(h, &h->csr_fbcnt, 8, "csr fallback count and reasons")) ||
         (rc = dalloc(h, &h->csr_rinfo, (size_t)rows, "csr row info")) ||
         (rc = dalloc(h, &h->csr_ent, (size_t)rows * h->csr_ecap * 2, "csr exception entries")) ||
         (rc = dalloc(h, &h->csr_plan, (size_t)rows / CSR_ROWS + 1, "csr plans")) ||
@@ -858,7 +863,7 @@ int csr_alloc(swimsim *h) {
 // path leaves go to the production kernels here), 1 when the path is unavailable or declined (the caller hashes them),
 // < 0 on a HIP error (h->err set)
 int csr_hash(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t n, bool force = false) {
-    if (n > h->NL + h->d.dense_cap) return 1;
+    if (n > h->NL) return 1;
     if (csr_alloc(h)) return 1;
     CsdArgs ca{};
     ca.B = h->csr_B;
@@ -904,7 +909,7 @@ int csr_hash(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t n, 
         launch_csr(h->d, list, n, cnt, ca, a, h->s, 1);
         launch_csr(h->d, list, n, cnt, ca, a, h->s, 2);
         launch_csr(h->d, list, n, cnt, ca, a, h->s, 3);
-        HIPCHK(h, hipMemsetAsync(h->csr_fbcnt, 0, 4, h->s));
+        HIPCHK(h, hipMemsetAsync(h->csr_fbcnt, 0, 32, h->s));
         hipLaunchKernelGGL(k_ctr_add, dim3(1), dim3(1), 0, h->s, h->d, (int)C_X_CSD_SCANNED, (unsigned long long)n);
     }
     {
@@ -913,9 +918,10 @@ int csr_hash(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t n, 
     }
     h->csr_launches++;
     uint32_t nf = 0;
-    HIPCHK(h, hipMemcpyAsync(h->hinfo + 16, h->csr_fbcnt, 4, hipMemcpyDeviceToHost, h->s));
+    HIPCHK(h, hipMemcpyAsync(h->hinfo + 16, h->csr_fbcnt, 32, hipMemcpyDeviceToHost, h->s));
     HIPCHK(h, hipStreamSynchronize(h->s));
     nf = h->hinfo[16];
+    for (int b = 0; b < 7; b++) h->csr_reasons[b] += h->hinfo[17 + b];
     if (nf) {                                                      // rows the path left: the production kernels
         h->csr_fallback_rows += nf;
         const CsKind k2 = cs_kind(nf, h->cs_narrow_rows);
@@ -2739,7 +2745,7 @@ int swimsim_checksum_path_stats(swimsim_t *h, uint64_t *delta_launches, uint64_t
     if (delta_launches) *delta_launches = h->csr_launches;
     if (fallback_rows) *fallback_rows = h->csr_fallback_rows;
     if (reasons) {
-        for (uint32_t b = 0; b < 8; b++) reasons[b] = 0;
+        for (uint32_t b = 0; b < 7; b++) reasons[b] = h->csr_reasons[b];
         reasons[7] = h->csr_declined;
     }
 #endif

@@ -561,7 +561,9 @@ class Cluster:
         return {"shards": g.value, "rank": r.value, "lo": lo.value, "hi": hi.value, "exchanged_bytes": xb.value,
                 "exchanges": xc.value, "exchange_host_syncs": xs.value}
 
-    CSD_REASONS = ("short", "entry_cap", "window_plan", "entry_batch", "exception_slots", "jump_slots", "window_miss",
+    # (rows the reference-row path left to the production kernels, by reason; "record_cap" is the diagnostics
+    # library's entry-batch reason, "jump_slots" and "window_miss" exist only there)
+    CSD_REASONS = ("short", "entry_cap", "window_plan", "record_cap", "exception_slots", "jump_slots", "window_miss",
                    "declined_launches")
 
     def checksum_path_stats(self):

@@ -28,8 +28,9 @@ for rows in rows_list:
     for mode in modes:
         out[f"rows{rows}_mode{mode}_ms"] = round(c.bench_checksum(rows, mode, reps=reps), 3)
         out[f"rows{rows}_mode{mode}_mismatch"] = int((c.checksums()[:rows] != ref[:rows]).sum())
+        if mode in (3, 5):
+            out[f"rows{rows}_mode{mode}_path"] = c.checksum_path_stats()
         if mode == 3:
-            out[f"rows{rows}_mode3_path"] = c.checksum_path_stats()
             ku = c.kernel_units()
             out["diag"] = [hex(int(ku.get(f"diag_stamp{i}", 0))) for i in range(4)]
         print(json.dumps(out), flush=True)
