@@ -1866,8 +1866,10 @@ int swimsim_set_member(swimsim_t *h, uint32_t o, uint32_t m, int32_t status, int
     if (!h || !own(h, o) || m >= h->N) return SWIMSIM_EINVAL;
     if (!(status >= 0 && status <= 4) && status != SWIMSIM_UNKNOWN) return SWIMSIM_EINVAL;
     uint32_t e = 0;
-    if (status != SWIMSIM_UNKNOWN)
+    if (status != SWIMSIM_UNKNOWN) {
         if (int rc = to_e(h, inc_ms, &e)) return rc;
+        if (int rc = ensure_ecap(h, e)) return rc;              // the checksum tables cover the new incarnation
+    }
     const uint32_t w = (e << 3) | (uint32_t)status;
     HIPCHK(h, hipMemsetAsync(h->d.colx, 0xFF, (size_t)h->d.NBIT * 4, h->s));   // raw write: every column may differ
     hot_reset(h, true);
@@ -1880,6 +1882,7 @@ int swimsim_set_member(swimsim_t *h, uint32_t o, uint32_t m, int32_t status, int
 int swimsim_set_row(swimsim_t *h, uint32_t o, const uint8_t *status, const int64_t *inc_ms) {
     if (!h || !own(h, o) || !status || !inc_ms) return SWIMSIM_EINVAL;
     std::vector<uint32_t> row(h->NP, (uint32_t)SWIMSIM_UNKNOWN);
+    uint32_t emax = 0;
     for (uint32_t m = 0; m < h->N; m++) {
         const int32_t s = status[m];
         if (s == SWIMSIM_UNKNOWN) continue;
@@ -1887,7 +1890,9 @@ int swimsim_set_row(swimsim_t *h, uint32_t o, const uint8_t *status, const int64
         uint32_t e;
         if (int rc = to_e(h, inc_ms[m], &e)) return rc;
         row[m] = (e << 3) | (uint32_t)s;
+        emax = std::max(emax, e);
     }
+    if (int rc = ensure_ecap(h, emax)) return rc;                  // the checksum tables cover every incarnation
     HIPCHK(h, hipMemsetAsync(h->d.colx, 0xFF, (size_t)h->d.NBIT * 4, h->s));   // raw write: every column may differ
     hot_reset(h, true);
     HIPCHK(h, hipMemcpyAsync(h->d.mw + (size_t)(o - h->lo) * h->NP, row.data(), (size_t)h->N * 4,
