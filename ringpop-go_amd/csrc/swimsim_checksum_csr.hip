@@ -349,25 +349,20 @@ __global__ void __launch_bounds__(CSR_ROWS) k_csr(DS d, const uint32_t *list, co
                       make_uint2(wst1[v].x, wst1[v].y));
         }
     };
-    // a row's codes at shift s with no exception block: the window entries base + i
-    auto write_base = [&]() {
+    // the chain's codes for the super step, per lane in registers: base(s) + i for a row without exception blocks
+    // (set in registers when the row's shift changes), a record's codes (through the row's LDS table row, where the
+    // exception codes are patched to the wave's slots) otherwise
+    uint32_t code[CSR_SB];
+    auto set_base = [&]() {
         const uint32_t ba = base * CSR_ESZ;
 #pragma unroll
-        for (int q = 0; q < 8; q++) {
-            u32x4 v;
-            v.x = ba + (4u * q + 0u) * CSR_ESZ;
-            v.y = ba + (4u * q + 1u) * CSR_ESZ;
-            v.z = ba + (4u * q + 2u) * CSR_ESZ;
-            v.w = ba + (4u * q + 3u) * CSR_ESZ;
-            *(u32x4 *)(trow + 4 * q) = v;
-        }
+        for (int i = 0; i < CSR_SB; i++) code[i] = ba + (uint32_t)i * CSR_ESZ;
     };
-    // (every lane's table starts valid: a row that is not hashed reads entry 0)
-    if (live) {
-        write_base();
-    } else {
+    // (a row that is not hashed reads entry 0)
+    if (live) set_base();
+    else {
 #pragma unroll
-        for (int q = 0; q < 8; q++) *(u32x4 *)(trow + 4 * q) = u32x4{0u, 0u, 0u, 0u};
+        for (int i = 0; i < CSR_SB; i++) code[i] = 0u;
     }
     bool was = false;                                              // the row's codes are a record's
     // a super step's row preparation in buffer b: a row with a record for t writes its codes and its exception
@@ -410,21 +405,15 @@ __global__ void __launch_bounds__(CSR_ROWS) k_csr(DS d, const uint32_t *list, co
                     }
                 }
                 s = (int32_t)R0.y;
+#pragma unroll
+                for (int q = 0; q < 8; q++) {                      // the codes back (this lane's own writes)
+                    const u32x4 v = *(const u32x4 *)(trow + 4 * q);
+                    code[4 * q] = v.x; code[4 * q + 1] = v.y; code[4 * q + 2] = v.z; code[4 * q + 3] = v.w;
+                }
             }
         }
-        if (was && !has) write_base();
+        if (was && !has) set_base();
         was = has;
-    };
-
-    // the chain's codes for the super step: read from the row's table after its preparation (the reads complete
-    // while the waves meet at the barrier)
-    uint32_t code[CSR_SB];
-    auto load_codes = [&]() {
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-            const u32x4 v = *(const u32x4 *)(trow + 4 * q);
-            code[4 * q] = v.x; code[4 * q + 1] = v.y; code[4 * q + 2] = v.z; code[4 * q + 3] = v.w;
-        }
     };
 
     // super step 0
@@ -433,7 +422,6 @@ __global__ void __launch_bounds__(CSR_ROWS) k_csr(DS d, const uint32_t *list, co
     wload(wB0, wB1, 1);
     prep(0, 0);
     if (live && rv && R0.x == 0) { base = csr_base(p, s); rcur++; ecur += R0.w; load_rec(rcur, ecur); }
-    load_codes();
     __syncthreads();
     CSR_STAMP(tl0);
     // (the loop runs two super steps per trip, one per buffer, so that every staging set and LDS buffer is named at
@@ -459,8 +447,14 @@ __global__ void __launch_bounds__(CSR_ROWS) k_csr(DS d, const uint32_t *list, co
             constexpr bool FULL = decltype(FULLC)::value;
             u32x4 va[CSR_PF + 1], vb[CSR_PF + 1];
             auto fetch = [&](int i) {
-                va[i % (CSR_PF + 1)] = *(const u32x4 *)(EAb + code[i]);
-                vb[i % (CSR_PF + 1)] = *(const u32x4 *)(EBb + code[i]);
+#ifdef CSR_DIAG_BCAST
+                // (diagnostic build only: every lane reads lane 0's entries: wrong checksums, no bank conflicts)
+                const uint32_t c = (uint32_t)__builtin_amdgcn_readfirstlane((int)code[i]);
+#else
+                const uint32_t c = code[i];
+#endif
+                va[i % (CSR_PF + 1)] = *(const u32x4 *)(EAb + c);
+                vb[i % (CSR_PF + 1)] = *(const u32x4 *)(EBb + c);
             };
 #pragma unroll
             for (int i = 0; i < CSR_PF; i++) fetch(i);
@@ -498,7 +492,6 @@ __global__ void __launch_bounds__(CSR_ROWS) k_csr(DS d, const uint32_t *list, co
         const bool adv = live && rv && R0.x == t + 1;
         if (adv) { base = csr_base(p, s); rcur++; ecur += R0.w; }
         if (__ballot(adv)) load_rec(rcur, ecur);
-        load_codes();
         CSR_STAMP(ts2);
         __syncthreads();
         CSR_STAMP(ts3);
