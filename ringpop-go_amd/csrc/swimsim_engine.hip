@@ -1824,6 +1824,11 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
     h->live.assign(h->N, 1);
     h->part.assign(h->N, 0);
     if (upload_topology(h) || hipStreamSynchronize(h->s) != hipSuccess) return bail(SWIMSIM_EHIP);
+    // the reference-row path's buffers (about 180 KB per owned row) now, when this handle can launch it at all (a
+    // wide launch needs more than cs_narrow_rows rows): allocated at the first wide launch they put a hipMalloc of
+    // several GB inside a round, which sometimes took over a second (3 of 12 bench runs at 77-92 ms per round).
+    // Failure is not an error: the production kernels stay in charge.
+    if (h->csr_mode != 0 && h->N >= 1024 && h->NL > h->cs_narrow_rows && h->NL >= CSD_MIN_ROWS) (void)csr_alloc(h);
     if (hipGetLastError() != hipSuccess) return bail(SWIMSIM_EHIP);
     *out = h;
     return SWIMSIM_OK;

@@ -55,11 +55,16 @@ def test_config5_shard_allocates_on_one_mi355x():
     state_transitions.go:52); here they are dense cells, and this checks on hardware that the budget fits with at
     least 10 % headroom, and that a 262,144-member row's checksum (a 10 MB string) equals Fingerprint32 of the
     reference's string rebuilt from the row (memberlist.go:106-128)."""
-    import torch
+    import ctypes
 
     from oracle_ffi import fingerprint32
 
-    total = torch.cuda.get_device_properties(0).total_memory
+    # (the device's memory through the HIP runtime the engine uses: torch's own runtime may refuse the GPU once the
+    # engine's has initialised it in this process)
+    hip = ctypes.CDLL("libamdhip64.so")
+    free_b, total_b = ctypes.c_size_t(), ctypes.c_size_t()
+    assert hip.hipMemGetInfo(ctypes.byref(free_b), ctypes.byref(total_b)) == 0
+    total = total_b.value
     if total < 280e9:
         pytest.skip(f"needs a 288 GB MI355X ({total / 1e9:.0f} GB visible)")
     n, shard = 262144, (0, 32768)
