@@ -35,7 +35,11 @@ constexpr int CSR_ENT = CSR_WINMAX + 4 * CSR_EXW;   // entries per buffer
 constexpr int CSR_TW = 36;             // u32 words per row of the code table (32 codes + pad: ds_read_b128 conflict-free)
 constexpr uint32_t CSR_ESZ = 16;       // a code's unit: an entry's byte offset in each of the two entry arrays
 constexpr int CSR_EREG = 4;            // exception entries of a record prefetched with it
-constexpr int CSR_PF = 4;              // blocks the chain's LDS reads run ahead of its arithmetic
+#ifndef CSR_PF_DEF
+#define CSR_PF_DEF 6
+#endif
+constexpr int CSR_PF = CSR_PF_DEF;     // blocks the chain's LDS reads run ahead of its arithmetic (6: 7.37 / 11.52 ms
+                                       // on rounds 14 / 18 against 7.48 / 11.69 with 4 and 8.00 / 12.00 with 2)
 constexpr uint32_t CSR_EXC = 0x8000u;  // code flag: exception entry (low bits: ordinal in the super step)
 constexpr uint32_t CSR_F_PLAN = 128, CSR_F_SLOTS = 256, CSR_F_RCAP = 512;   // flags beyond k_csd_scan's
 
