@@ -125,6 +125,23 @@ def test_config3_n65536_eight_shards_vs_oracle_fixture():
     assert all(x > 0 for x in per_round[20])
 
 
+def test_config3_n65536_two_shards_reference_row_path_vs_oracle_fixture():
+    """Two shards of 32,768 rows: each shard's wide checksum launches run the reference-row path (a shard's reference
+    row, divergent columns and exception records over its own rows), every round against the oracle fixture. Dense
+    snapshot slots and message pools are sized explicitly so that both shards fit one GPU."""
+    fx = load_fixture("config3_n65536.json")
+    wl = W.config3(n=65536, rounds=fx["rounds"], kill_round=10)
+    launches = []
+
+    def paths(eng, r):
+        launches.append(sum(s.checksum_path_stats()["delta_launches"] for s in eng.shards))
+
+    c, rec = compare_with_fixture(wl, fx, shards=2, on_round=paths, message_pool_bytes=16 << 30,
+                                  tuning={"dense_slots": 8192})
+    assert rec["round"] == 99 and c["timers_fired"] > 0
+    assert launches[-1] > 0, "no launch took the reference-row path"
+
+
 def test_selfstart_n16384_full_syncs_vs_oracle_fixture():
     """Full syncs and reverse full syncs at size (disseminator.go:156-181, 257-304): 16,384 nodes that start knowing
     only themselves and two seeded members, 40 rounds, every round against the oracle fixture."""
