@@ -50,7 +50,8 @@ struct CsrPlan {
     uint32_t nph;          // popcount(phm)
     uint32_t maxit;        // the workgroup's longest chain (blocks)
     uint32_t feasible;
-    uint32_t pad0, pad1;
+    uint32_t ecmax;        // rows with more exception entries than this are not in the plan (production kernels)
+    uint32_t pad1;
 };
 
 // one record per (row, super step with exception blocks), 80 B
@@ -107,34 +108,45 @@ __global__ void k_csr_ptable(const uint32_t *__restrict__ SBw, uint32_t sbw_word
     P[2 * q + 1] = make_uint4(v[4], v[5], 0u, 0u);
 }
 
+// (a workgroup whose window would not fit plans again without its far rows, those with more than CSR_NEAR exception
+// entries: many differences from the reference bring many shifts and phases, and one such row used to send all 256 rows
+// of its workgroup to the production kernels; the far rows alone go there now)
+constexpr uint32_t CSR_NEAR = 1024;
 __global__ void __launch_bounds__(CSR_ROWS) k_csr_plan(DS d, const uint32_t *list, uint32_t n, CsrArgs a) {
-    __shared__ int32_t sm[2];
-    __shared__ uint32_t ph, mi;
+    __shared__ int32_t sm[2][2];
+    __shared__ uint32_t ph[2], mi[2];
     const uint32_t gi = blockIdx.x * CSR_ROWS + threadIdx.x;
-    if (threadIdx.x == 0) { sm[0] = 0x7FFFFFFF; sm[1] = -0x7FFFFFFF - 1; ph = 0; mi = 0; }
+    if (threadIdx.x < 2) { sm[threadIdx.x][0] = 0x7FFFFFFF; sm[threadIdx.x][1] = -0x7FFFFFFF - 1; ph[threadIdx.x] = 0; mi[threadIdx.x] = 0; }
     __syncthreads();
     if (gi < n) {
         const CsdRow ri = a.rinfo[gi];
         const uint32_t len = csd_len(d, list[gi]);
         if (ri.flags == 0 && len > 24) {
-            atomicMin(&sm[0], ri.smin);
-            atomicMax(&sm[1], ri.smax);
-            atomicOr(&ph, ri.phmask);
-            atomicMax(&mi, (len - 1) / 20);
+            for (int k = 0; k < 2; k++) {                          // 0: every row, 1: the near rows
+                if (k == 1 && ri.ecnt > CSR_NEAR) break;
+                atomicMin(&sm[k][0], ri.smin);
+                atomicMax(&sm[k][1], ri.smax);
+                atomicOr(&ph[k], ri.phmask);
+                atomicMax(&mi[k], (len - 1) / 20);
+            }
         }
     }
     __syncthreads();
     if (threadIdx.x == 0) {
         CsrPlan p{};
-        int32_t smin = sm[0], smax = sm[1];
-        uint32_t phm = ph;
-        if (phm == 0) { phm = 1; smin = 0; smax = 0; }
-        p.cmax = csr_ceil20(smax);
-        p.Wn = ((uint32_t)(CSR_SB + (p.cmax - csr_ceil20(smin)) + 1) + 30u) / 32u * 32u + 1u;   // = 1 mod 32 (k_csr)
-        p.phm = phm;
-        p.nph = (uint32_t)__popc(phm);
-        p.maxit = mi;
-        p.feasible = p.nph * p.Wn <= (uint32_t)CSR_WINMAX && p.Wn < 0x7000u ? 1u : 0u;
+        for (int k = 0; k < 2; k++) {
+            int32_t smin = sm[k][0], smax = sm[k][1];
+            uint32_t phm = ph[k];
+            if (phm == 0) { phm = 1; smin = 0; smax = 0; }
+            p.cmax = csr_ceil20(smax);
+            p.Wn = ((uint32_t)(CSR_SB + (p.cmax - csr_ceil20(smin)) + 1) + 30u) / 32u * 32u + 1u;   // = 1 mod 32 (k_csr)
+            p.phm = phm;
+            p.nph = (uint32_t)__popc(phm);
+            p.maxit = mi[k];
+            p.feasible = p.nph * p.Wn <= (uint32_t)CSR_WINMAX && p.Wn < 0x7000u ? 1u : 0u;
+            p.ecmax = k == 0 ? 0xFFFFFFFFu : CSR_NEAR;
+            if (p.feasible) break;
+        }
         a.plan[blockIdx.x] = p;
     }
 }
@@ -151,7 +163,7 @@ __global__ void __launch_bounds__(256) k_csr_rec(DS d, const uint32_t *list, uin
     const CsdRow ri = a.rinfo[i];
     const CsrPlan p = a.plan[i / CSR_ROWS];
     uint32_t nr = 0;
-    if (ri.flags == 0 && p.feasible) {
+    if (ri.flags == 0 && p.feasible && ri.ecnt <= p.ecmax) {
         const uint32_t len = csd_len(d, list[i]);
         const uint32_t iters = len > 24 ? (len - 1) / 20 : 0u;
         const uint4 *ent = a.ent + (size_t)i * a.ecap * 2;
@@ -249,7 +261,8 @@ __global__ void __launch_bounds__(CSR_ROWS) k_csr(DS d, const uint32_t *list, co
     const uint32_t nrec = valid ? a.nrec[gi] : 0u;
     const uint32_t len = csd_len(d, id);
     const uint32_t iters = len > 24 ? (len - 1) / 20 : 0u;
-    uint32_t fl = !valid ? 0u : ri.flags ? ri.flags : !p.feasible ? CSR_F_PLAN : nrec == 0xFFFFFFFFu ? CSR_F_RCAP : 0u;
+    uint32_t fl = !valid ? 0u : ri.flags ? ri.flags : !p.feasible || ri.ecnt > p.ecmax ? CSR_F_PLAN
+                : nrec == 0xFFFFFFFFu ? CSR_F_RCAP : 0u;
     if (valid && !fl && iters == 0) fl = CSD_F_SHORT;
     if (tid < 20 && ((p.phm >> tid) & 1u)) phs[__popc(p.phm & ((1u << tid) - 1u))] = tid;   // phase slot -> phase
     __syncthreads();
