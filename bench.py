@@ -294,7 +294,6 @@ def main():
     ap.add_argument("--host-transport", action="store_true")
     # the reference-row checksum path (swimsim_tuning.cs_ref: 0 off, 1 wide launches; default: the library's)
     ap.add_argument("--cs-ref", type=int, default=-1)
-    ap.add_argument("--cs-ref-maxdiff", type=int, default=-1)
     ap.add_argument("--cs-async-rows", type=int, default=-1)   # side-stream checksum launches up to this many rows
     # test hook: the ranks report (rank, world size) and exit before any GPU call
     ap.add_argument("--launch-check", action="store_true")
@@ -340,8 +339,7 @@ def main():
 
     n = args.members
     total_rounds = args.warmup + args.steps
-    tuning = {k: v for k, v in (("cs_ref", args.cs_ref), ("cs_ref_maxdiff", args.cs_ref_maxdiff),
-                                ("cs_async_rows", args.cs_async_rows)) if v >= 0} or None
+    tuning = {k: v for k, v in (("cs_ref", args.cs_ref), ("cs_async_rows", args.cs_async_rows)) if v >= 0} or None
     wl = W.config3(n=n, rounds=max(total_rounds, KILL_ROUND + 1), kill_round=KILL_ROUND)
     nkilled = sum(1 for e in wl.events if e[1] == W.EV_KILL)
     if ws > 1:

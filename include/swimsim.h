@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SWIMSIM_ABI_VERSION 4
+#define SWIMSIM_ABI_VERSION 5
 
 enum {
     SWIMSIM_OK = 0,
@@ -62,7 +62,8 @@ typedef struct swimsim_config {
     uint32_t max_rounds;               /* incarnation table capacity (default 65536 rounds) */
     uint64_t message_pool_bytes;       /* change-record pool; 0 = automatic */
     uint32_t observer_begin, observer_end; /* shard of observer rows held by this handle; 0,0 = all */
-    const struct swimsim_tuning *tuning;   /* NULL: the production engine; else variants for tests (below) */
+    const struct swimsim_tuning *tuning;   /* NULL: the production engine; else variants for tests (below). Callers
+                                              zero-initialise the struct (memset), so a field added later reads 0 */
 } swimsim_config;
 
 /* Engine variants the tests and diagnostics select per handle (results are identical in every variant; only where
@@ -77,8 +78,9 @@ typedef struct swimsim_tuning {
                                  kernel only; default 8,192 */
     int32_t cs_ref;           /* the reference-row checksum path: 0 off, 1 wide launches (default), 2
                                  every launch of at least 1,024 rows */
-    int32_t cs_ref_maxdiff;   /* the path declines a launch whose sampled rows differ from the reference in more than
-                                 this many members on average; 0 = never declines (default) */
+    int32_t fault_inject;     /* tests only: 1 = the reference-row path's buffers fail to allocate (the production kernels
+                                 stay in charge, create and step succeed); 2 = the next reference-row launch fails with
+                                 SWIMSIM_EHIP (the step returns it; the handle stays usable); default 0 */
 } swimsim_tuning;
 
 /* Events applied in phase E of a round (docs/ROUND_SEMANTICS.md §4). */
@@ -242,15 +244,16 @@ int swimsim_kernel_units(swimsim_t *h, const char **names, double *values, size_
 /* profiler window marker: one tiny kernel (k_profile_mark) on the engine's stream, after the side stream drained */
 int swimsim_profile_mark(swimsim_t *h, uint32_t id);
 /* time the checksum kernel alone on the first nrows rows — average ms per launch. mode 0: the production choice for
- * nrows rows, 1: the wide kernel (k_checksum3), 2: the narrow kernel (k_checksum_q16), 3: the reference-row path
- * (reference row, k_csd_scan, k_cs_delta and the fallback launch for the rows it leaves); other modes (diagnostic
- * variants) only in the diagnostics library tools/libswimsim_diag.so */
+ * nrows rows, 1: the wide kernel (k_checksum3), 2: the narrow kernel (k_checksum_q16), 4: k_checksum3 with four row
+ * groups per workgroup, 5: the reference-row path forced (reference row, k_csd_scan, k_csr_rec, k_csr and the
+ * fallback launches for the rows it leaves); other modes (diagnostic variants) only in the diagnostics library
+ * tools/libswimsim_diag.so */
 int swimsim_bench_checksum(swimsim_t *h, uint32_t nrows, int32_t mode, int32_t reps, double *ms);
-/* the reference-row checksum path so far (swimsim_checksum_delta.hip; SWIMSIM_CS_DELTA = 0 off, 1 wide launches,
- * 2 every launch of >= 1024 rows): its launches, the rows it left to the production kernels and, per reason (8
- * entries: short string, entry capacity, workgroup window, entry batch, exception slots, jump slots, window miss),
- * how many of those rows had it; reasons[7]: launches it declined (sampled rows further from the reference row than
- * SWIMSIM_CS_DELTA_MAXDIFF members on average) */
+/* the reference-row checksum path so far (swimsim_checksum_ref.hip + swimsim_checksum_csr.hip; swimsim_tuning.cs_ref =
+ * 0 off, 1 wide launches, 2 every launch of >= 1024 rows): its launches, the rows it left to the production kernels
+ * and, per reason (8 entries: short string, exception-entry capacity, workgroup window plan, record capacity,
+ * exception slots of a wave, 5..7 reserved = 0), how many of those rows had it. The counts are kept on the device and
+ * read here (no host synchronisation inside a round). */
 int swimsim_checksum_path_stats(swimsim_t *h, uint64_t *delta_launches, uint64_t *fallback_rows, uint64_t *reasons);
 /* diagnostics library only: the 32-bit words of every 20-byte block the checksum kernel hashes for row o (W = 19) */
 int swimsim_debug_cs_stream(swimsim_t *h, uint32_t o, uint32_t *out, size_t cap_words);

@@ -50,6 +50,7 @@ struct CsdArgs {
     const uint32_t *ulist;    // divergent columns in member order (DS::colx), or null: k_csd_scan reads every column
     const uint32_t *ucnt;     // their number
     const uint4 *ucol;        // per divergent column c: {m, B[m], O_B[m], O_B[m - 1]} (k_csr_ucol)
+    const uint32_t *uhk;      // per divergent column c: the hot slot of its member, or SRC_NONE (DS::uhk)
     uint32_t dmode;           // diagnostics library only (swimsim_bench_checksum modes 31..46 = dmode + 30, garbage
                               // checksums): 1 helpers alone, 2 chains alone, 3 helpers without the exception work; bit 8:
                               // no barrier between super steps. Ignored by the product library (CSD_DMODE)
@@ -106,6 +107,8 @@ __global__ void k_csd_ref(DS d, const uint32_t *list, uint32_t n, uint32_t *B, u
     Lb[m] = csd_reclen(d, cand);
 }
 
+#ifdef SWIMSIM_DIAG
+// (diagnostics library only: round 3's path declines launches on a sample; the product's path never declines)
 // the launch's mean distance from B, on CSD_NSAMPLE rows sampled evenly from the list: differing members counted
 // into *out (one workgroup per sampled row). Decides whether the reference-row path pays for this launch.
 constexpr uint32_t CSD_NSAMPLE = 64;
@@ -117,37 +120,7 @@ __global__ void __launch_bounds__(256) k_csd_sample(DS d, const uint32_t *list, 
     for (int off = 32; off > 0; off >>= 1) c += (uint32_t)__shfl_xor((int)c, off, 64);
     if ((threadIdx.x & 63u) == 0 && c) atomicAdd(out, c);
 }
-
-// the divergent columns in member order (one workgroup of 1024 threads: each thread a run of bitmap words, a block
-// prefix sum of their bit counts)
-__global__ void __launch_bounds__(1024) k_csr_ulist(DS d, uint32_t *ulist, uint32_t *ucnt) {
-    __shared__ uint32_t part[1024];
-    const uint32_t t = threadIdx.x, per = (d.NBIT + 1023) / 1024, w0 = t * per;
-    auto bitsof = [&](uint32_t w) -> uint32_t {                    // (bits of members >= N masked off)
-        const uint32_t x = d.colx[w], lo = w * 32;
-        return lo + 32 <= d.N ? x : lo >= d.N ? 0u : x & ((1u << (d.N - lo)) - 1u);
-    };
-    uint32_t c = 0;
-    for (uint32_t w = w0; w < min(w0 + per, d.NBIT); w++) c += (uint32_t)__popc(bitsof(w));
-    part[t] = c;
-    __syncthreads();
-    for (uint32_t off = 1; off < 1024; off <<= 1) {              // inclusive Hillis-Steele scan
-        const uint32_t v = t >= off ? part[t - off] : 0u;
-        __syncthreads();
-        part[t] += v;
-        __syncthreads();
-    }
-    uint32_t at = part[t] - c;
-    for (uint32_t w = w0; w < min(w0 + per, d.NBIT); w++) {
-        uint32_t bits = bitsof(w);
-        while (bits) {
-            const uint32_t b = (uint32_t)__builtin_ctz(bits);
-            bits &= bits - 1;
-            ulist[at++] = w * 32 + b;
-        }
-    }
-    if (t == 1023) *ucnt = part[1023];
-}
+#endif
 
 // the divergent columns' scan table: what k_csd_scan needs of B at each, in one 16-B load
 __global__ void k_csr_ucol(const uint32_t *ulist, const uint32_t *ucnt, const uint32_t *B, const uint32_t *OB, uint4 *ucol) {
@@ -381,6 +354,9 @@ __global__ void __launch_bounds__(256) k_csd_scan(DS d, const uint32_t *list, ui
     const uint32_t ncol = UL ? ucnt : N;
     // (divergent columns come with their B word and offsets from the column table: one dependent load less)
     const bool ULc = UL && a.ucol;
+    // (a listed observer row reads its hot members' words from the row's compact hot copy, a few KB, instead of one
+    // 64-B sector per word of the 256-KB row; snapshots and cold members from the row)
+    const uint32_t *hrow = (ULc && a.uhk && d.hidx && id < d.NL) ? d.hmw + (size_t)id * d.HP : nullptr;
     for (uint32_t c00 = 0; c00 < ncol && !flags; c00 += 64 * CSD_SU) {
         uint32_t wv_[CSD_SU], bv_[CSD_SU], mv_[CSD_SU], ov_[CSD_SU], o1_[CSD_SU];
         if (ULc) {
@@ -388,8 +364,9 @@ __global__ void __launch_bounds__(256) k_csd_scan(DS d, const uint32_t *list, ui
             for (uint32_t k = 0; k < CSD_SU; k++) {
                 const uint32_t c = c00 + 64 * k + lane;
                 const uint4 u = a.ucol[c < ncol ? c : 0u];
+                const uint32_t hk = hrow ? a.uhk[c < ncol ? c : 0u] : SRC_NONE;
                 mv_[k] = u.x; bv_[k] = u.y; ov_[k] = u.z; o1_[k] = u.w;
-                wv_[k] = row[u.x];
+                wv_[k] = *(hk != SRC_NONE ? hrow + hk : row + u.x);
                 if (c >= ncol) bv_[k] = wv_[k];                    // (past the list: equal, no diff)
             }
         } else {

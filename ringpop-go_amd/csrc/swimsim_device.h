@@ -140,6 +140,10 @@ struct DS {
     uint32_t HP;              // hot slots per row
     int32_t *nhe;             // [NL] dissemination entries of members WITHOUT a hot slot; 0: every buffered member of
                               // the row is hot, so issue walks the hot slots instead of the presence bitmap
+    // the divergent columns (colx) as lists, rebuilt by k_ucols before every kernel that compares or scans rows by
+    // them: ucl = every colx column in member order (ucnt[0] of them) with its hot slot uhk (SRC_NONE: none), ucold =
+    // the colx columns without a hot slot (ucnt[1], any order). Rows are equal iff equal at the hot slots and ucold.
+    uint32_t *ucl, *uhk, *ucold, *ucnt;
 };
 
 // hot slot of member m, SRC_NONE when m has none (or hot columns are off)

@@ -352,13 +352,11 @@ struct swimsim {
     CsrPlan *csr_plan = nullptr;
     CsrRec *csr_rec = nullptr;
     uint32_t csr_ecap = 4096, csr_rcap = 512, csr_KP = 0;    // (2,048 entries: rows far from the reference fell back)
-    uint32_t *csr_ulist = nullptr, *csr_ucnt = nullptr; // the divergent columns (DS::colx) in member order
-    uint4 *csr_ucol = nullptr;                          // and their scan table (k_csr_ucol)
-    uint32_t csr_maxdiff = 0;                     // swimsim_tuning.cs_ref_maxdiff: mean differing members per sampled
-                                                  // row above which a launch keeps the production kernels (0: never;
-                                                  // the default: a decline costs a host synchronisation mid-round, and
-                                                  // the path no longer loses on heavy rounds)
-    uint64_t csr_launches = 0, csr_fallback_rows = 0, csr_declined = 0, csr_reasons[7] = {0};
+    uint4 *csr_ucol = nullptr;                    // the divergent columns' scan table (k_csr_ucol)
+    uint32_t *csr_fbsplit = nullptr;              // fallback rows per production launch (k_csr_fbsplit)
+    unsigned long long *csr_acc = nullptr;        // [8] fallback rows so far, then per reason (read by path stats)
+    uint64_t csr_launches = 0;
+    int fault_inject = 0;                         // swimsim_tuning.fault_inject (tests)
 #ifdef SWIMSIM_DIAG
     // reference-row checksum path (swimsim_checksum_delta.hip), allocated at its first launch
     int csd_mode = 0;                             // SWIMSIM_CS_DELTA: 0 off, 1 wide launches, 2 every launch >= 1024 rows
@@ -820,11 +818,25 @@ bool csr_wanted(swimsim *h, uint32_t n, CsKind kind) {
 
 int csr_alloc(swimsim *h) {
     if (h->csr_ready) return 0;
+    if (h->csr_failed) return 1;
     // (per listed row of one launch: sized for NL rows; the few launches that list more rows and dense snapshots
     // together keep the production kernels, csr_hash)
     const uint32_t rows = h->NL;
     h->csr_sbw_words = ((size_t)h->N * (h->W + 32) + 256) / 4;
     h->csr_KP = (uint32_t)(h->csr_sbw_words * 4 / 20 + 2);
+    const size_t nalloc0 = h->allocs.size();
+    const uint64_t bytes0 = h->alloc_bytes;
+    // a failure frees what this call allocated and clears HIP's last error (a failed hipMalloc leaves it set, and
+    // swimsim_create / step_one test it): the production kernels stay in charge, nothing else changes
+    auto undo = [&](int rc) {
+        for (size_t i = nalloc0; i < h->allocs.size(); i++) hipFree(h->allocs[i]);
+        h->allocs.resize(nalloc0);
+        h->alloc_bytes = bytes0;
+        (void)hipGetLastError();
+        h->csr_failed = true;
+        h->err.clear();
+        return rc;
+    };
     int rc = 0;
     if ((rc = dalloc(h, &h->csr_B, (size_t)h->NP, "csr reference row")) ||
         (rc = dalloc(h, &h->csr_Lb, (size_t)h->N + 1, "csr reference lengths")) ||
@@ -838,20 +850,17 @@ int csr_alloc(swimsim *h) {
         (rc = dalloc(h, &h->csr_plan, (size_t)rows / CSR_ROWS + 1, "csr plans")) ||
         (rc = dalloc(h, &h->csr_rec, (size_t)rows * h->csr_rcap, "csr records")) ||
         (rc = dalloc(h, &h->csr_nrec, (size_t)rows, "csr record counts")) ||
-        (rc = dalloc(h, &h->csr_ulist, (size_t)h->N, "csr divergent columns")) ||
-        (rc = dalloc(h, &h->csr_ucnt, 1, "csr divergent column count")) ||
-        (rc = dalloc(h, &h->csr_ucol, (size_t)h->N, "csr divergent column table"))) {
-        h->csr_failed = true;                                      // the production kernels stay in charge
-        h->err.clear();
-        return rc;
-    }
+        (rc = dalloc(h, &h->csr_ucol, (size_t)h->N, "csr divergent column table")) ||
+        (rc = (h->fault_inject & 1) ? h->fail(SWIMSIM_ENOMEM, "injected allocation failure") : 0) ||
+        (rc = dalloc(h, &h->csr_fbsplit, 4, "csr fallback split")) ||
+        (rc = dalloc(h, &h->csr_acc, 8, "csr path statistics")))
+        return undo(rc);
     size_t need = 0;
     hipcub::DeviceScan::ExclusiveSum(nullptr, need, h->csr_Lb, h->csr_OB, (int)h->N + 1, h->s);
-    if (need > h->cub_bytes) {
-        void *p = nullptr;
-        if (hipMalloc(&p, need) != hipSuccess) { h->csr_failed = true; return SWIMSIM_ENOMEM; }
-        h->allocs.push_back(p);
-        h->alloc_bytes += need;
+    void *p = nullptr;
+    if (need > h->cub_bytes && (rc = dalloc(h, (uint8_t **)&p, need, "cub temp (csr)"))) return undo(rc);
+    if (hipMemsetAsync(h->csr_acc, 0, 8 * sizeof(unsigned long long), h->s) != hipSuccess) return undo(SWIMSIM_EHIP);
+    if (p) {                                                       // (committed only here: undo frees p)
         h->cub_tmp = p;
         h->cub_bytes = need;
     }
@@ -859,12 +868,30 @@ int csr_alloc(swimsim *h) {
     return 0;
 }
 
+// rows k_csr left (csr_fbcnt[0], reasons in [1..7]): the production launches' counts (<= 4,096 rows: the narrow kernel
+// at 16 records per step; the next 8,192: at 8; the rest: the wide kernel) and the running statistics, on the device
+__global__ void k_csr_fbsplit(uint32_t *fbcnt, uint32_t *split, unsigned long long *acc) {
+    const uint32_t t = threadIdx.x;
+    const uint32_t nf = fbcnt[0];
+    if (t == 0) {
+        split[0] = min(nf, 4096u);
+        split[1] = nf > 4096u ? min(nf - 4096u, 8192u) : 0u;
+        split[2] = nf > 12288u ? nf - 12288u : 0u;
+    }
+    if (t < 8 && nf) acc[t] += fbcnt[t];
+}
+
 // hash the n listed rows (count on the device) by the reference-row path. Returns 0 when every row is hashed (rows the
-// path leaves go to the production kernels here), 1 when the path is unavailable or declined (the caller hashes them),
-// < 0 on a HIP error (h->err set)
-int csr_hash(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t n, bool force = false) {
+// path leaves go to the production kernels here), 1 when the path is unavailable (the caller hashes them), < 0 on a
+// HIP error (h->err set). Nothing here waits for the device: the rows the chains leave are counted on the device and
+// the production launches take their counts from there.
+int csr_hash(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t n, int chains = 4) {
     if (n > h->NL) return 1;
     if (csr_alloc(h)) return 1;
+    if (h->fault_inject & 2) {                                     // tests: one injected HIP failure
+        h->fault_inject &= ~2;
+        return h->fail(SWIMSIM_EHIP, "csr_hash: injected HIP error");
+    }
     CsdArgs ca{};
     ca.B = h->csr_B;
     ca.OB = h->csr_OB;
@@ -873,9 +900,10 @@ int csr_hash(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t n, 
     ca.ent = h->csr_ent;
     ca.rinfo = h->csr_rinfo;
     ca.ecap = h->csr_ecap;
-    ca.ulist = h->csr_ulist;
-    ca.ucnt = h->csr_ucnt;
+    ca.ulist = h->d.ucl;
+    ca.ucnt = h->d.ucnt;
     ca.ucol = h->csr_ucol;
+    ca.uhk = h->d.uhk;
     CsrArgs a{};
     a.P = h->csr_P;
     a.KP = h->csr_KP;
@@ -891,19 +919,11 @@ int csr_hash(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t n, 
     {
         Scope sc(h, F_CSD_SCAN);
         hipLaunchKernelGGL(k_csd_ref, dim3((h->N + 256) / 256), dim3(256), 0, h->s, h->d, list, n, h->csr_B, h->csr_Lb);
-        if (h->csr_maxdiff && !force) {
-            // rows far from the majority make many exception blocks: decide on a sample
-            HIPCHK(h, hipMemsetAsync(h->csr_fbcnt, 0, 4, h->s));
-            hipLaunchKernelGGL(k_csd_sample, dim3(CSD_NSAMPLE), dim3(256), 0, h->s, h->d, list, n, h->csr_B, h->csr_fbcnt);
-            HIPCHK(h, hipMemcpyAsync(h->hinfo + 16, h->csr_fbcnt, 4, hipMemcpyDeviceToHost, h->s));
-            HIPCHK(h, hipStreamSynchronize(h->s));
-            if ((double)h->hinfo[16] / CSD_NSAMPLE > (double)h->csr_maxdiff) { h->csr_declined++; return 1; }
-        }
         size_t bytes = h->cub_bytes;
         HIPCHK(h, hipcub::DeviceScan::ExclusiveSum(h->cub_tmp, bytes, h->csr_Lb, h->csr_OB, (int)h->N + 1, h->s));
         HIPCHK(h, hipMemsetAsync(h->csr_SBw, 0, h->csr_sbw_words * 4, h->s));
-        hipLaunchKernelGGL(k_csr_ulist, dim3(1), dim3(1024), 0, h->s, h->d, h->csr_ulist, h->csr_ucnt);
-        hipLaunchKernelGGL(k_csr_ucol, dim3((h->N + 255) / 256), dim3(256), 0, h->s, h->csr_ulist, h->csr_ucnt, h->csr_B,
+        hipLaunchKernelGGL(k_ucols, dim3(1), dim3(1024), 0, h->s, h->d);
+        hipLaunchKernelGGL(k_csr_ucol, dim3((h->N + 255) / 256), dim3(256), 0, h->s, h->d.ucl, h->d.ucnt, h->csr_B,
                            h->csr_OB, h->csr_ucol);
         launch_csr(h->d, list, n, cnt, ca, a, h->s, 0);
         launch_csr(h->d, list, n, cnt, ca, a, h->s, 1);
@@ -914,20 +934,16 @@ int csr_hash(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t n, 
     }
     {
         Scope sc(h, F_CS_WIDE);
-        launch_csr(h->d, list, n, cnt, ca, a, h->s, 4);
+        launch_csr(h->d, list, n, cnt, ca, a, h->s, chains);
     }
     h->csr_launches++;
-    uint32_t nf = 0;
-    HIPCHK(h, hipMemcpyAsync(h->hinfo + 16, h->csr_fbcnt, 32, hipMemcpyDeviceToHost, h->s));
-    HIPCHK(h, hipStreamSynchronize(h->s));
-    nf = h->hinfo[16];
-    for (int b = 0; b < 7; b++) h->csr_reasons[b] += h->hinfo[17 + b];
-    if (nf) {                                                      // rows the path left: the production kernels
-        h->csr_fallback_rows += nf;
-        const CsKind k2 = cs_kind(nf, h->cs_narrow_rows);
-        Scope sc(h, k2 == CS_WIDE ? F_CS_WIDE : F_CS_NARROW);
-        launch_checksum_kind(h->d, h->csr_fb, h->csr_fbcnt, nf, k2, h->s);
-    }
+    // rows the path left: the production kernels, counts from the device (a launch with nothing to hash exits at
+    // once; timed with the preparation so that the checksum families' launch counts stay those of real work)
+    Scope sc(h, F_CSPREP);
+    hipLaunchKernelGGL(k_csr_fbsplit, dim3(1), dim3(64), 0, h->s, h->csr_fbcnt, h->csr_fbsplit, h->csr_acc);
+    launch_checksum_kind(h->d, h->csr_fb, h->csr_fbsplit, std::min(n, 4096u), CS_NARROW, h->s);
+    if (n > 4096u) launch_checksum_kind(h->d, h->csr_fb + 4096, h->csr_fbsplit + 1, std::min(n - 4096u, 8192u), CS_NARROW, h->s);
+    if (n > 12288u) launch_checksum_kind(h->d, h->csr_fb + 12288, h->csr_fbsplit + 2, n - 12288u, CS_WIDE, h->s);
     return 0;
 }
 
@@ -938,9 +954,10 @@ int csr_hash(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t n, 
 // over the snapshot pool) touches as many distant pages per load, so address translation, not bandwidth or issue,
 // sets the pace (the wide launch in the cascade: 18.3 -> 15.3 ms). The sorted copy goes to whichever of
 // list / fplist the caller is not using; neither is read again in its old order.
-void hash_rows(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t maxn, uint32_t nrows,
-               hipStream_t st = nullptr) {
-    if (std::min(maxn, nrows) == 0) return;
+// Returns 0 or a negative SWIMSIM_E* code (h->err set); every caller passes it on.
+int hash_rows(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t maxn, uint32_t nrows,
+              hipStream_t st = nullptr) {
+    if (std::min(maxn, nrows) == 0) return 0;
     if (!st && nrows != ~0u && nrows >= 64 && nrows <= h->NL && (list == h->list || list == h->fplist)) {
         Scope sc(h, F_CSPREP);
         uint32_t *out = list == h->list ? h->fplist : h->list;
@@ -954,16 +971,17 @@ void hash_rows(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t m
     const CsKind kind = cs_kind(n, h->cs_narrow_rows);
     if (!st && nrows != ~0u && csr_wanted(h, n, kind)) {          // the reference-row path (swimsim_checksum_csr.hip)
         const int rc = csr_hash(h, list, cnt, n);
-        if (rc <= 0) return;                                       // done (or failed loudly: h->err)
+        if (rc <= 0) return rc;                                    // done, or failed (h->err)
     }
 #ifdef SWIMSIM_DIAG
     if (!st && nrows != ~0u && csd_wanted(h, n, kind)) {          // diagnostics library: round 3's reference-row path
         const int rc = csd_hash(h, list, cnt, n);
-        if (rc <= 0) return;                                       // done (or failed loudly: h->err)
+        if (rc <= 0) return rc;                                    // done, or failed (h->err)
     }
 #endif
     Scope sc(h, kind == CS_WIDE ? F_CS_WIDE : F_CS_NARROW, st);
     launch_checksum_kind(h->d, list, cnt, n, kind, st ? st : h->s);
+    return 0;
 }
 
 // the hot slots' cells back into dent for rows [ol0, ol0 + n) (DS::hde: the slot is the cell of a hot member)
@@ -1010,10 +1028,7 @@ int checksum_dirty(swimsim *h, int mode, bool async = false) {
         hipLaunchKernelGGL(k_list, dim3(blocks_for_threads(h->NL)), dim3(256), 0, h->s, h->d, mode, h->tgt, h->failed,
                            h->list, h->cnt);
     }
-    if (mode != 0) {
-        hash_rows(h, h->list, h->cnt, h->NL, ~0u);
-        return 0;
-    }
+    if (mode != 0) return hash_rows(h, h->list, h->cnt, h->NL, ~0u);
     uint32_t *hn = h->hinfo + 8;
     HIPCHK(h, hipMemcpyAsync(hn, h->cnt, 4, hipMemcpyDeviceToHost, h->s));
     HIPCHK(h, hipStreamSynchronize(h->s));
@@ -1030,7 +1045,7 @@ int checksum_dirty(swimsim *h, int mode, bool async = false) {
         }
         HIPCHK(h, hipEventRecord(h->ev_snap, h->s));
         HIPCHK(h, hipStreamWaitEvent(h->side, h->ev_snap, 0));
-        hash_rows(h, h->side_ids, h->side_cnt, n2, n2, h->side);
+        if (int rc = hash_rows(h, h->side_ids, h->side_cnt, n2, n2, h->side)) return rc;
         hipLaunchKernelGGL(k_side_scatter, dim3(blocks_for_threads(n)), dim3(256), 0, h->side, h->d, h->side_map, n, n2);
         HIPCHK(h, hipEventRecord(h->ev_side, h->side));
         h->side_pending = true;
@@ -1039,16 +1054,22 @@ int checksum_dirty(swimsim *h, int mode, bool async = false) {
     const bool side_ok = async && h->cs_async;
     if (n < 2) {
         if (n == 1 && side_ok && h->snap_cap >= 1) return go_side(h->list, 1, h->list, nullptr);
-        hash_rows(h, h->list, h->cnt, n, n);
-        return 0;
+        return hash_rows(h, h->list, h->cnt, n, n);
     }
     {
         Scope sc(h, F_CSPREP);
-        hipLaunchKernelGGL(k_fp_keys, dim3(blocks_for_threads(n)), dim3(256), 0, h->s, h->d, h->list, n, h->keys, h->fpv);
+        // (k_list compacts with atomics: its order changes from run to run. Sorted by row first, the stable
+        // fingerprint sort leaves every group in row order, so the group heads, the rows hashed and the reference-row
+        // path's fallbacks are the same in every run of one command)
         size_t bytes = h->cub_bytes;
+        HIPCHK(h, hipcub::DeviceRadixSort::SortKeys(h->cub_tmp, bytes, h->list, h->fplist, (int)n, 0,
+                                                    32 - __builtin_clz(h->NL), h->s));
+        hipLaunchKernelGGL(k_fp_keys, dim3(blocks_for_threads(n)), dim3(256), 0, h->s, h->d, h->fplist, n, h->keys, h->fpv);
+        bytes = h->cub_bytes;
         HIPCHK(h, hipcub::DeviceRadixSort::SortPairs(h->cub_tmp, bytes, h->keys, h->keys_sorted, h->fpv, h->fpv_s, (int)n, 0,
                                                      64, h->s));
         hipLaunchKernelGGL(k_fp_heads, dim3(blocks_for_threads(n)), dim3(256), 0, h->s, h->keys_sorted, n, h->fph);
+        hipLaunchKernelGGL(k_ucols, dim3(1), dim3(1024), 0, h->s, h->d);   // (k_fp_verify compares by them)
         bytes = h->cub_bytes;
         HIPCHK(h, hipcub::DeviceScan::InclusiveScan(h->cub_tmp, bytes, h->fph, h->fph_s, hipcub::Max(), (int)n, h->s));
         HIPCHK(h, hipMemsetAsync(h->fpcnt, 0, 4, h->s));
@@ -1060,7 +1081,7 @@ int checksum_dirty(swimsim *h, int mode, bool async = false) {
     }
     HIPCHK(h, hipStreamSynchronize(h->s));                                         // picks the variant
     if (side_ok && hn[1] <= h->snap_cap) return go_side(h->fplist, hn[1], h->fpv_s, h->dup_of);
-    hash_rows(h, h->fplist, h->fpcnt, n, hn[1]);                                   // (sorted to row order there)
+    if (int rc = hash_rows(h, h->fplist, h->fpcnt, n, hn[1])) return rc;          // (sorted to row order there)
     Scope sc(h, F_CSPREP);
     hipLaunchKernelGGL(k_fp_copy, dim3(blocks_for_threads(n)), dim3(256), 0, h->s, h->d, h->fpv_s, n, h->dup_of);
     return 0;
@@ -1083,7 +1104,7 @@ int bound_lazy_snapshots(swimsim *h, int mode) {
     HIPCHK(h, hipStreamSynchronize(h->s));
     if (*hc <= h->d.dense_cap / 2) return 0;
     if (int rc = sync_side(h)) return rc;
-    hash_rows(h, h->list, h->cnt, h->NL, *hc);
+    if (int rc = hash_rows(h, h->list, h->cnt, h->NL, *hc)) return rc;
     h->lazy_fallbacks++;
     return 0;
 }
@@ -1103,6 +1124,7 @@ int resolve_deferred(swimsim *h, int phase, MsgDesc *rdesc, uint32_t maxn) {
     {
         Scope sc(h, F_CSPREP);
         HIPCHK(h, hipMemsetAsync(h->cnt, 0, 8, h->s));
+        hipLaunchKernelGGL(k_ucols, dim3(1), dim3(1024), 0, h->s, h->d);   // (k_defer_eq compares by them)
         hipLaunchKernelGGL(k_defer_eq, dim3(blocks_for_waves(maxn)), dim3(SWIM_WAVE_BLOCK), 0, h->s, h->d, h->defer, h->defer_cnt,
                            phase, h->defer_eq);
         hipLaunchKernelGGL(k_defer_ids, dim3(blocks_for_threads(maxn)), dim3(256), 0, h->s, h->d, h->defer,
@@ -1125,7 +1147,7 @@ int resolve_deferred(swimsim *h, int phase, MsgDesc *rdesc, uint32_t maxn) {
         // the list holds main-stream snapshot slots only (k_defer_ids), so their hash needs nothing from the side
         // stream and runs beside the previous phase C's side-stream launch (both are latency-bound launches of
         // few rows); k_recv_finish then compares with side-stream checksums, so it waits for the side stream
-        hash_rows(h, h->list, h->cnt, maxlist, *hc);
+        if (int rc = hash_rows(h, h->list, h->cnt, maxlist, *hc)) return rc;
         if (hc[1])
             if (int rc = sync_side(h)) return rc;
     }
@@ -1189,8 +1211,7 @@ bool host_reach(swimsim *h, uint32_t a, uint32_t b) { return h->live[a] && h->li
 
 int ensure_clean_checksum(swimsim *h, uint32_t ol) {
     hipLaunchKernelGGL(k_list_one, dim3(1), dim3(64), 0, h->s, h->list, h->cnt, ol, h->d);
-    hash_rows(h, h->list, h->cnt, 1, 1);
-    return 0;
+    return hash_rows(h, h->list, h->cnt, 1, 1);
 }
 
 inline bool own(const swimsim *h, uint32_t o) { return o >= h->lo && o < h->lo + h->NL; }
@@ -1205,7 +1226,7 @@ int push_item(swimsim *h, uint4 it) {
 int ping_with(swimsim *h, uint32_t o, uint32_t t, int slot) {
     const uint32_t root = owner_host(h, o), ot = owner_host(h, t);
     if (h->rank == root) {
-        ensure_clean_checksum(h, o - h->lo);
+        if (int rc = ensure_clean_checksum(h, o - h->lo)) return rc;
         hipLaunchKernelGGL(k_sender_info, dim3(1), dim3(64), 0, h->s, h->d, o - h->lo, h->hsics);
     }
     const MsgDesc *md = h->hdesc + slot;
@@ -1649,7 +1670,7 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
     if (tun && tun->cs_async >= 0) h->cs_async = tun->cs_async != 0;
     if (tun && tun->cs_narrow_rows >= 0) h->cs_narrow_rows = (uint32_t)tun->cs_narrow_rows;
     if (tun && tun->cs_ref >= 0) h->csr_mode = tun->cs_ref;
-    if (tun && tun->cs_ref_maxdiff >= 0) h->csr_maxdiff = (uint32_t)tun->cs_ref_maxdiff;
+    if (tun && tun->fault_inject > 0) h->fault_inject = tun->fault_inject;
 #ifdef SWIMSIM_DIAG                                 // diagnostics library only: the reference-row path
     if (const char *v = getenv("SWIMSIM_CS_DELTA")) h->csd_mode = atoi(v);
     if (const char *v = getenv("SWIMSIM_CS_DELTA_MAXDIFF")) h->csd_maxdiff = (uint32_t)strtoul(v, nullptr, 10);
@@ -1677,7 +1698,9 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
         (rc = dalloc(h, &d.ctr, (size_t)CTR_SHARDS * CTR_STRIDE, "counters")) || (rc = dalloc(h, &d.err, 4, "err")) ||
         (rc = dalloc(h, &d.clen, h->NL, "clen")) || (rc = dalloc(h, &d.clast, h->NL, "clast")) ||
         (rc = dalloc(h, &d.cpslot, h->NL, "cpslot")) || (rc = dalloc(h, &d.nhe, h->NL, "cold entry counts")) ||
-        (rc = dalloc(h, &d.colx, d.NBIT, "divergent columns")))
+        (rc = dalloc(h, &d.colx, d.NBIT, "divergent columns")) || (rc = dalloc(h, &d.ucl, h->N, "divergent column list")) ||
+        (rc = dalloc(h, &d.uhk, h->N, "divergent column hot slots")) || (rc = dalloc(h, &d.ucold, h->N, "cold divergent columns")) ||
+        (rc = dalloc(h, &d.ucnt, 2, "divergent column counts")))
         return bail(rc);
     hipMemset(d.nhe, 0, (size_t)h->NL * 4);
     hipMemset(d.colx, 0xFF, (size_t)d.NBIT * 4);
@@ -2207,7 +2230,7 @@ __global__ void k_iota(uint32_t *list, uint32_t *cnt, uint32_t n) {
 int swimsim_bench_checksum(swimsim_t *h, uint32_t nrows, int32_t mode, int32_t reps, double *ms) {
     if (!h || !ms || nrows == 0 || nrows > h->NL || reps < 1) return SWIMSIM_EINVAL;
 #ifndef SWIMSIM_DIAG
-    if (mode < 0 || mode > 5 || mode == 3)
+    if (mode < 0 || mode > 6 || mode == 3)
         return h->fail(SWIMSIM_EINVAL, "checksum mode %d: diagnostics build only", mode);
     const bool csd = false;
 #else
@@ -2217,7 +2240,8 @@ int swimsim_bench_checksum(swimsim_t *h, uint32_t nrows, int32_t mode, int32_t r
     const bool csd = mode == 3 || (mode >= 31 && mode <= 46);
     if (csd && (csd_alloc(h) || nrows > h->NL)) return h->fail(SWIMSIM_EINVAL, "reference-row path unavailable");
 #endif
-    if (mode == 5 && csr_alloc(h)) return h->fail(SWIMSIM_EINVAL, "reference-row path unavailable");
+    if ((mode == 5 || mode == 6) && csr_alloc(h)) return h->fail(SWIMSIM_EINVAL, "reference-row path unavailable");
+    int rc5 = 0;
     auto launch = [&]() {
         if (csd) {                                                 // the path itself, never declined here
 #ifdef SWIMSIM_DIAG
@@ -2229,7 +2253,8 @@ int swimsim_bench_checksum(swimsim_t *h, uint32_t nrows, int32_t mode, int32_t r
         }
         else if (mode <= 2) launch_checksum_kind(h->d, h->list, h->cnt, nrows, mode == 0 ? cs_kind(nrows, h->cs_narrow_rows) : (CsKind)mode, h->s);
         else if (mode == 4) launch_checksum_wide4(h->d, h->list, h->cnt, nrows, h->s);
-        else if (mode == 5) (void)csr_hash(h, h->list, h->cnt, nrows, true);   // the reference-row path, forced
+        else if (mode == 5) rc5 = csr_hash(h, h->list, h->cnt, nrows);   // the reference-row path, forced
+        else if (mode == 6) rc5 = csr_hash(h, h->list, h->cnt, nrows, 5);   // the same with round 4's chain kernel
 #ifdef SWIMSIM_DIAG
         else launch_checksum_mode(h->d, h->list, h->cnt, nrows, mode, h->s);
 #endif
@@ -2242,6 +2267,7 @@ int swimsim_bench_checksum(swimsim_t *h, uint32_t nrows, int32_t mode, int32_t r
     HIPCHK(h, hipEventRecord(a, h->s));
     for (int i = 0; i < reps; i++) launch();
     HIPCHK(h, hipEventRecord(b, h->s));
+    if (rc5 < 0) return rc5;
     HIPCHK(h, hipEventSynchronize(b));
     float t = 0;
     hipEventElapsedTime(&t, a, b);
@@ -2752,11 +2778,16 @@ int swimsim_checksum_path_stats(swimsim_t *h, uint64_t *delta_launches, uint64_t
         reasons[CSD_NFLAGS] = h->csd_declined;
     }
 #else                                       // the product's reference-row path (swimsim_checksum_csr.hip)
+    unsigned long long acc[8] = {0};
+    if (h->csr_ready) {                     // counted on the device (k_csr_fbsplit)
+        HIPCHK(h, hipMemcpyAsync(acc, h->csr_acc, sizeof acc, hipMemcpyDeviceToHost, h->s));
+        HIPCHK(h, hipStreamSynchronize(h->s));
+    }
     if (delta_launches) *delta_launches = h->csr_launches;
-    if (fallback_rows) *fallback_rows = h->csr_fallback_rows;
+    if (fallback_rows) *fallback_rows = acc[0];
     if (reasons) {
-        for (uint32_t b = 0; b < 7; b++) reasons[b] = h->csr_reasons[b];
-        reasons[7] = h->csr_declined;
+        for (uint32_t b = 0; b < 5; b++) reasons[b] = acc[1 + b];
+        for (uint32_t b = 5; b < 8; b++) reasons[b] = 0;   // (reserved)
     }
 #endif
     return SWIMSIM_OK;

@@ -1169,6 +1169,111 @@ __global__ void __launch_bounds__(256, RECV_MIN_WAVES) k_recv(DS d, RecvArgs a) 
     }
 }
 
+// the divergent-column lists (DS::ucl / uhk / ucold / ucnt) from the bitmap (one workgroup of 1024 threads: each thread
+// a run of bitmap words, a block prefix sum of their bit counts)
+__global__ void __launch_bounds__(1024) k_ucols(DS d) {
+    __shared__ uint32_t part[1024];
+    __shared__ uint32_t ncold;
+    const uint32_t t = threadIdx.x, per = (d.NBIT + 1023) / 1024, w0 = t * per;
+    if (t == 0) ncold = 0;
+    auto bitsof = [&](uint32_t w) -> uint32_t {                    // (bits of members >= N masked off)
+        const uint32_t x = d.colx[w], lo = w * 32;
+        return lo + 32 <= d.N ? x : lo >= d.N ? 0u : x & ((1u << (d.N - lo)) - 1u);
+    };
+    uint32_t c = 0;
+    for (uint32_t w = w0; w < min(w0 + per, d.NBIT); w++) c += (uint32_t)__popc(bitsof(w));
+    part[t] = c;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024; off <<= 1) {              // inclusive Hillis-Steele scan
+        const uint32_t v = t >= off ? part[t - off] : 0u;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint32_t at = part[t] - c;
+    for (uint32_t w = w0; w < min(w0 + per, d.NBIT); w++) {
+        uint32_t bits = bitsof(w);
+        while (bits) {
+            const uint32_t m = w * 32 + (uint32_t)__builtin_ctz(bits);
+            bits &= bits - 1;
+            const uint32_t k = hot_slot(d, m);
+            d.ucl[at] = m;
+            d.uhk[at] = k;
+            if (k == SRC_NONE) d.ucold[atomicAdd(&ncold, 1u)] = m;
+            at++;
+        }
+    }
+    __syncthreads();
+    if (t == 0) {
+        d.ucnt[0] = part[1023];
+        d.ucnt[1] = ncold;
+    }
+}
+
+// one wave: do two rows differ? Outside the divergent columns every row and every snapshot holds the same word
+// (DS::colx), so only those are compared while they are few (at most N/4), the rest being the hot slots' compact
+// copies (ha, hb: both rows' hmw, or null for a snapshot) and gathers for the others; every word otherwise.
+__device__ bool wave_rows_differ(const DS &d, const uint32_t *a, const uint32_t *b, const uint32_t *ha, const uint32_t *hb) {
+    const uint32_t lane = lane_id();
+    bool diff = false;
+    const uint32_t nu = d.ucnt[0];
+    if (nu <= d.N / 4) {
+        if (ha && hb) {                                            // live rows: hot slots, then the cold columns
+            const uint32_t nh = d.hot_cnt[0], nc = d.ucnt[1];
+            for (uint32_t k0 = 0; k0 < nh && !__any(diff); k0 += 64 * MB) {
+                uint32_t x[MB], y[MB];
+#pragma unroll
+                for (int u = 0; u < MB; u++) {
+                    const uint32_t k = k0 + u * 64 + lane;
+                    x[u] = k < nh ? ha[k] : 0u;
+                    y[u] = k < nh ? hb[k] : 0u;
+                }
+#pragma unroll
+                for (int u = 0; u < MB; u++) diff |= x[u] != y[u];
+            }
+            for (uint32_t c0 = 0; c0 < nc && !__any(diff); c0 += 64 * MB) {
+                uint32_t x[MB], y[MB];
+#pragma unroll
+                for (int u = 0; u < MB; u++) {
+                    const uint32_t c = c0 + u * 64 + lane;
+                    const uint32_t m = c < nc ? d.ucold[c] : 0u;
+                    x[u] = c < nc ? a[m] : 0u;
+                    y[u] = c < nc ? b[m] : 0u;
+                }
+#pragma unroll
+                for (int u = 0; u < MB; u++) diff |= x[u] != y[u];
+            }
+        } else {                                                   // a snapshot: every divergent column
+            for (uint32_t c0 = 0; c0 < nu && !__any(diff); c0 += 64 * MB) {
+                uint32_t x[MB], y[MB];
+#pragma unroll
+                for (int u = 0; u < MB; u++) {
+                    const uint32_t c = c0 + u * 64 + lane;
+                    const uint32_t m = c < nu ? d.ucl[c] : 0u;
+                    x[u] = c < nu ? a[m] : 0u;
+                    y[u] = c < nu ? b[m] : 0u;
+                }
+#pragma unroll
+                for (int u = 0; u < MB; u++) diff |= x[u] != y[u];
+            }
+        }
+    } else {
+        const uint4 *a4 = (const uint4 *)a, *b4 = (const uint4 *)b;
+        for (uint32_t base = 0; base < d.NP / 4 && !__any(diff); base += 64 * MB) {
+            uint4 x[MB], y[MB];
+#pragma unroll
+            for (int u = 0; u < MB; u++) {
+                const uint32_t k = base + u * 64 + lane;
+                x[u] = k < d.NP / 4 ? a4[k] : make_uint4(0, 0, 0, 0);
+                y[u] = k < d.NP / 4 ? b4[k] : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < MB; u++) diff |= x[u].x != y[u].x || x[u].y != y[u].y || x[u].z != y[u].z || x[u].w != y[u].w;
+        }
+    }
+    return __any(diff);
+}
+
 // resolve deferred full-sync decisions once the snapshot checksums exist (phase 2 = heal ping:
 // the job is queued at once; heal runs in phase E, before any phase-D job of the round)
 // Equal rows have equal checksums: a deferred decision whose receiver snapshot equals the sender's
@@ -1189,22 +1294,7 @@ __global__ void k_defer_eq(DS d, const uint4 *defer, const uint32_t *defer_cnt, 
         }
     }
     bool same = false;
-    if (srow) {
-        const uint4 *a = (const uint4 *)(d.dense + (size_t)e.y * d.NP), *b = (const uint4 *)srow;
-        bool diff = false;
-        for (uint32_t base = 0; base < d.NP / 4 && !__any(diff); base += 64 * MB) {
-            uint4 x[MB], y[MB];
-#pragma unroll
-            for (int u = 0; u < MB; u++) {
-                const uint32_t k = base + u * 64 + lane_id();
-                x[u] = k < d.NP / 4 ? a[k] : make_uint4(0, 0, 0, 0);
-                y[u] = k < d.NP / 4 ? b[k] : make_uint4(0, 0, 0, 0);
-            }
-#pragma unroll
-            for (int u = 0; u < MB; u++) diff |= x[u].x != y[u].x || x[u].y != y[u].y || x[u].z != y[u].z || x[u].w != y[u].w;
-        }
-        same = !__any(diff);
-    }
+    if (srow) same = !wave_rows_differ(d, d.dense + (size_t)e.y * d.NP, srow, nullptr, nullptr);
     if (lane_id() == 0) eq[i] = same ? 1 : 0;
 }
 
@@ -1371,21 +1461,9 @@ __global__ void k_fp_verify(DS d, const uint32_t *vals, const uint32_t *headpos,
     const uint32_t row = vals[i], hp = headpos[i];
     bool same = false;
     if (hp != i) {
-        const uint4 *a = (const uint4 *)(d.mw + (size_t)vals[hp] * d.NP);
-        const uint4 *b = (const uint4 *)(d.mw + (size_t)row * d.NP);
-        bool diff = false;
-        for (uint32_t base = 0; base < d.NP / 4 && !__any(diff); base += 64 * MB) {
-            uint4 x[MB], y[MB];
-#pragma unroll
-            for (int u = 0; u < MB; u++) {
-                const uint32_t k = base + u * 64 + lane_id();
-                x[u] = k < d.NP / 4 ? a[k] : make_uint4(0, 0, 0, 0);
-                y[u] = k < d.NP / 4 ? b[k] : make_uint4(0, 0, 0, 0);
-            }
-#pragma unroll
-            for (int u = 0; u < MB; u++) diff |= x[u].x != y[u].x || x[u].y != y[u].y || x[u].z != y[u].z || x[u].w != y[u].w;
-        }
-        same = !__any(diff);
+        const uint32_t head = vals[hp];
+        const uint32_t *ha = d.hidx ? d.hmw + (size_t)head * d.HP : nullptr, *hb = d.hidx ? d.hmw + (size_t)row * d.HP : nullptr;
+        same = !wave_rows_differ(d, d.mw + (size_t)head * d.NP, d.mw + (size_t)row * d.NP, ha, hb);
     }
     if (lane_id() == 0) {
         dup_of[row] = same ? vals[hp] : SRC_NONE;

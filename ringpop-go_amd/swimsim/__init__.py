@@ -57,7 +57,7 @@ class Tuning(C.Structure):
     """swimsim_tuning (include/swimsim.h): engine variants for tests and diagnostics, -1 = the production default."""
     _fields_ = [("hot_slots", C.c_int32), ("dense_slots", C.c_int32), ("cs_async", C.c_int32),
                 ("cs_async_rows", C.c_int32), ("cs_narrow_rows", C.c_int32), ("cs_ref", C.c_int32),
-                ("cs_ref_maxdiff", C.c_int32)]
+                ("fault_inject", C.c_int32)]
 
 
 def make_tuning(tuning):
@@ -561,10 +561,10 @@ class Cluster:
         return {"shards": g.value, "rank": r.value, "lo": lo.value, "hi": hi.value, "exchanged_bytes": xb.value,
                 "exchanges": xc.value, "exchange_host_syncs": xs.value}
 
-    # (rows the reference-row path left to the production kernels, by reason; "record_cap" is the diagnostics
-    # library's entry-batch reason, "jump_slots" and "window_miss" exist only there)
-    CSD_REASONS = ("short", "entry_cap", "window_plan", "record_cap", "exception_slots", "jump_slots", "window_miss",
-                   "declined_launches")
+    # (rows the reference-row path left to the production kernels, by reason; the diagnostics library's round-3 path
+    # reports its own reasons in the same slots: entry batch in "record_cap", jump slots and window misses in 5 and 6)
+    CSD_REASONS = ("short", "entry_cap", "window_plan", "record_cap", "exception_slots", "reserved5", "reserved6",
+                   "reserved7")
 
     def checksum_path_stats(self):
         dl, fb = C.c_uint64(), C.c_uint64()

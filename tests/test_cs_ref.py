@@ -20,7 +20,7 @@ pytestmark = pytest.mark.gpu
 
 
 def forced(n, **kw):
-    return swimsim.Cluster(n, tuning={"cs_ref": 2, "cs_async": 0, "cs_ref_maxdiff": kw.pop("maxdiff", 0)}, **kw)
+    return swimsim.Cluster(n, tuning={"cs_ref": 2, "cs_async": 0}, **kw)
 
 
 def run_vs_oracle(wl, rounds, init="converged", seed_members=()):
@@ -88,3 +88,30 @@ def test_mode5_on_real_cascade_rows(n, rounds):
         got = c.checksums()
         assert (got[:rows] == ref[:rows]).all(), f"{rows} rows: {(got[:rows] != ref[:rows]).sum()} differ"
     print(f"real rows n{n}", c.checksum_path_stats())
+
+
+def test_csr_alloc_failure_leaves_production_kernels_in_charge():
+    """swimsim_tuning.fault_inject = 1: the reference-row path's buffers fail to allocate. The failure frees what was
+    allocated and clears HIP's last error, so create and every step still succeed, on the production kernels."""
+    wl = W.config3(n=2048, rounds=30, kill_round=5)
+    eng = swimsim.Cluster(wl.n, tuning={"cs_ref": 2, "cs_async": 0, "fault_inject": 1})
+    ora = OracleSim(wl.n)
+    for r in range(30):
+        ev = wl.events_for(r)
+        eng.step(1, ev)
+        ora.step(ev)
+        assert (eng.checksums() == ora.checksums()).all(), f"round {r}"
+    assert eng.checksum_path_stats()["delta_launches"] == 0
+
+
+def test_csr_hash_hip_error_reaches_swimsim_step():
+    """swimsim_tuning.fault_inject = 2: the first reference-row launch fails with SWIMSIM_EHIP. The error comes back from
+    swimsim_step (HIP errors are mapped, never aborted on, and never swallowed), and the next handle
+    works."""
+    wl = W.config3(n=2048, rounds=30, kill_round=5)
+    eng = swimsim.Cluster(wl.n, tuning={"cs_ref": 2, "cs_async": 0, "fault_inject": 2})
+    with pytest.raises(swimsim.SwimsimError, match="EHIP"):
+        for r in range(30):
+            eng.step(1, wl.events_for(r))
+    eng.close()
+    run_vs_oracle(wl, 30)
