@@ -28,9 +28,13 @@
 constexpr int CSR_ROWS = 256;          // rows per workgroup (4 waves)
 constexpr int CSR_SB = 32;             // blocks per super step
 constexpr int CSR_WINMAX = 1024;       // window entries per buffer: phases in use x Wn
-constexpr int CSR_EXW = 384;           // exception entries per wave per buffer (128: a third of the rows of heavy cascade
+#ifndef CSR_EXW_DEF
+#define CSR_EXW_DEF 576
+#endif
+constexpr int CSR_EXW = CSR_EXW_DEF;   // exception entries per wave per buffer (128: a third of the rows of heavy cascade
                                        // rounds fell back, a differing column giving every row of a wave exceptions;
-                                       // 192: still an eighth in the heaviest)
+                                       // 192: still an eighth in the heaviest; 384: one row in the bench window. 576 once
+                                       // k_csr2 freed the code table's 36 KB of LDS)
 constexpr int CSR_ENT = CSR_WINMAX + 4 * CSR_EXW;   // entries per buffer
 constexpr int CSR_TW = 36;             // u32 words per row of the code table (32 codes + pad: ds_read_b128 conflict-free)
 constexpr uint32_t CSR_ESZ = 16;       // a code's unit: an entry's byte offset in each of the two entry arrays
@@ -231,329 +235,6 @@ __global__ void __launch_bounds__(256) k_csr_rec(DS d, const uint32_t *list, uin
     if (lane == 0) a.nrec[i] = nr;
 }
 
-template <int W>
-__global__ void __launch_bounds__(CSR_ROWS) k_csr(DS d, const uint32_t *list, const uint32_t *count, CsrArgs a) {
-    // per buffer: window entries, then each wave's exception entries, in two arrays of 16-B entries, EA {Mg, D, Mf, PF}
-    // and EB {Mh, KH, -, -}: a block is two ds_read_b128 at one byte address (the row's code, 16 e) plus each array's
-    // base as the immediate offset. ds_read_b128 runs at the LDS array's full rate with one wave per SIMD; 8-byte
-    // reads do not (three ds_read_b64 per block of 24-B entries: 10.3 ms per launch against 8.5 for one b64 + one b128).
-    // Two rows of a 16-lane group conflict when their entries are 16 apart; with Wn = 1 mod 32 the phases' windows
-    // start at different residues.
-    // (EB holds both buffers in each 16-B entry, buffer b in bytes 8b..8b+7: a ds_read_b128 of the whole entry and
-    // the compile-time buffer's half, with 16 KB more for exception slots)
-    __shared__ uint4 EA[2][CSR_ENT];
-    __shared__ uint4 EB[CSR_ENT];
-    // per row: the byte addresses of its 32 blocks' entries in the super step (one table, not one per buffer: a row's
-    // table is read and written only by its own lane, and rewritten only when its codes change)
-    __shared__ uint32_t T[CSR_ROWS * CSR_TW];
-    __shared__ uint32_t phs[20];
-    const uint32_t cnt = *count;
-    const uint32_t g0 = blockIdx.x * CSR_ROWS;
-    if (g0 >= cnt) return;
-    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
-    const uint32_t gi = g0 + tid;
-    const bool valid = gi < cnt;
-    const uint32_t id = list[valid ? gi : g0];
-    const bool is_row = id < d.NL;
-    const uint32_t *row = csd_row(d, id);
-    const CsdRow ri = a.rinfo[valid ? gi : g0];
-    const CsrPlan p = a.plan[blockIdx.x];
-    const uint32_t nrec = valid ? a.nrec[gi] : 0u;
-    const uint32_t len = csd_len(d, id);
-    const uint32_t iters = len > 24 ? (len - 1) / 20 : 0u;
-    uint32_t fl = !valid ? 0u : ri.flags ? ri.flags : !p.feasible || ri.ecnt > p.ecmax ? CSR_F_PLAN
-                : nrec == 0xFFFFFFFFu ? CSR_F_RCAP : 0u;
-    if (valid && !fl && iters == 0) fl = CSD_F_SHORT;
-    if (tid < 20 && ((p.phm >> tid) & 1u)) phs[__popc(p.phm & ((1u << tid) - 1u))] = tid;   // phase slot -> phase
-    __syncthreads();
-    const bool live = valid && fl == 0;
-    const uint32_t myit = live ? iters : 0u;
-    const uint32_t T_ = p.feasible ? (p.maxit + CSR_SB - 1) / CSR_SB : 0u;
-    const CsrRec *rec = a.rec + (size_t)(valid ? gi : g0) * a.rcap;
-    const uint4 *ent = a.ent + (size_t)(valid ? gi : g0) * a.ecap * 2;
-    const uint32_t nr = live ? nrec : 0u;
-    uint32_t *trow = T + (size_t)tid * CSR_TW;
-
-    // chain state (FarmHash-mk prologue, then X = state + the string's first words)
-    FH fh{0, 0, 0};
-    uint32_t it2 = 0;
-    const bool ok = cs_prologue<W>(d, id, is_row, row, fh, it2);
-    uint32_t Xg = fh.g + ri.b0, Xf = fh.f + ri.c0, Xh = fh.h + ri.a0;
-    int32_t s = 0;
-    uint32_t base = csr_base(p, 0);
-
-    // the next record and its first exception entries, loaded one record ahead
-    // (records partition the row's entries in order: record q + 1 begins where record q ends, so the entry loads never
-    // wait for the record itself; nothing here selects on a loaded value, which would wait for the load at once)
-    // (record and entries are held as whole vector registers, each loaded by one instruction into exactly the
-    // registers it lives in: loaded structs split into scalars came out as copies after the loads, each waiting for them)
-    uint32_t rcur = 0, ecur = 0;
-    bool rv = false;
-    u32x4 R0, R1, R2, R3, R4;                                    // CsrRec: {t, s_end, pos4, ne}, code[0..15]
-    u32x4 RE0a, RE1a, RE2a, RE3a;                                // entry values {Mg, D, Mf, PF}
-    u32x2 RE0b, RE1b, RE2b, RE3b;                                // {Mh, KH}
-    // (unconditional loads from clamped indices: conditionally assigned arrays would live in scratch)
-    auto load_rec = [&](uint32_t q, uint32_t e0) {
-        const u32x4 *rp = (const u32x4 *)(rec + min(q, a.rcap - 1u));
-        R0 = rp[0]; R1 = rp[1]; R2 = rp[2]; R3 = rp[3]; R4 = rp[4];
-        const u32x4 *ep = (const u32x4 *)(ent + 2 * min(e0, a.ecap - (uint32_t)CSR_EREG));
-        RE0a = ep[0]; RE0b = *(const u32x2 *)(ep + 1);
-        RE1a = ep[2]; RE1b = *(const u32x2 *)(ep + 3);
-        RE2a = ep[4]; RE2b = *(const u32x2 *)(ep + 5);
-        RE3a = ep[6]; RE3b = *(const u32x2 *)(ep + 7);
-        rv = q < nr;
-    };
-    load_rec(0, 0);
-#ifdef CSR_DIAG_STAMP
-    // (diagnostic build only: shader-clock stamps around the loop's sections, summed per wave into the diagnostic
-    // counters: 0 chain, 1 staging + preparation, 2 barrier, 3 whole loop; shares only, the stamps drain LDS waits)
-    uint64_t st_[4] = {0, 0, 0, 0};
-    auto stamp = [&]() -> uint64_t {
-        uint64_t tt;
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tt) :: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        return tt;
-    };
-#define CSR_STAMP(v) const uint64_t v = stamp()
-#define CSR_ACC(k, x) st_[k] += (x)
-#else
-#define CSR_STAMP(v)
-#define CSR_ACC(k, x)
-#endif
-
-    // window staging: entries u = tid + 256 v of the next super step's window, through registers
-    constexpr int WV = CSR_WINMAX / CSR_ROWS;
-    // two staging sets: super step u's window goes through set u & 1, loaded two super steps ahead (the window rows of
-    // P miss in L2 at their first touch: one HBM round trip, longer than a super step's chain)
-    // (vector types: a struct copy of a uint4 is a memcpy, and the compiler promoted the staging arrays to LDS)
-    u32x4 wA0[WV], wB0[WV];
-    u32x2 wA1[WV], wB1[WV];
-    const uint32_t nwin = p.nph * p.Wn;
-    // (each thread's window entries keep their phase and position from super step to super step: their source rows
-    // in P are fixed, the S_B block advances by CSR_SB)
-    const uint4 *wsrc[WV];
-    int32_t wk0[WV];
-#pragma unroll
-    for (int v = 0; v < WV; v++) {
-        const uint32_t u = tid + (uint32_t)CSR_ROWS * v;
-        const uint32_t ps = u < nwin ? u / p.Wn : 0u, w = u < nwin ? u - ps * p.Wn : 0u;
-        wsrc[v] = a.P + 2 * (size_t)phs[min(ps, 19u)] * a.KP;
-        wk0[v] = u < nwin ? (int32_t)w - p.cmax : 0x40000000;
-    }
-    auto wload = [&](u32x4 (&wst0)[WV], u32x2 (&wst1)[WV], uint32_t t) {
-#pragma unroll
-        for (int v = 0; v < WV; v++) {
-            // (positions outside S_B are read only by predicated blocks past a row's chain: any value does; a select on
-            // the loaded value would wait for this load here, one HBM round trip per super step)
-            const int32_t k = min(max(wk0[v] + (int32_t)(t * CSR_SB), 0), (int32_t)a.KP - 1);
-            const uint4 *src = wsrc[v] + 2 * (uint32_t)k;
-            wst0[v] = *(const u32x4 *)src;
-            wst1[v] = *(const u32x2 *)(src + 1);
-        }
-    };
-    auto put_entry = [&](uint32_t b, uint32_t e, uint2 x, uint2 y, uint2 z) {
-        EA[b][e] = make_uint4(x.x, x.y, y.x, y.y);
-        ((uint2 *)&EB[e])[b] = z;
-    };
-    auto wstore = [&](const u32x4 (&wst0)[WV], const u32x2 (&wst1)[WV], uint32_t b) {
-#pragma unroll
-        for (int v = 0; v < WV; v++) {
-            // (every thread stores all its entries, those past the window into unused window slots: a store on some
-            // paths only left its loads pending on the others, and the loop head waited for them)
-            const uint32_t u = tid + (uint32_t)CSR_ROWS * v;
-            put_entry(b, u, make_uint2(wst0[v].x, wst0[v].y), make_uint2(wst0[v].z, wst0[v].w),
-                      make_uint2(wst1[v].x, wst1[v].y));
-        }
-    };
-    // the chain's codes for the super step, per lane in registers: base(s) + i for a row without exception blocks
-    // (set in registers when the row's shift changes), a record's codes (through the row's LDS table row, where the
-    // exception codes are patched to the wave's slots) otherwise
-    uint32_t code[CSR_SB];
-    auto set_base = [&]() {
-        const uint32_t ba = base * CSR_ESZ;
-#pragma unroll
-        for (int i = 0; i < CSR_SB; i++) code[i] = ba + (uint32_t)i * CSR_ESZ;
-    };
-    // (a row that is not hashed reads entry 0)
-    if (live) set_base();
-    else {
-#pragma unroll
-        for (int i = 0; i < CSR_SB; i++) code[i] = 0u;
-    }
-    bool was = false;                                              // the row's codes are a record's
-    // a super step's row preparation in buffer b: a row with a record for t writes its codes and its exception
-    // entries (exception codes patched to the wave's slots); a row whose last super step had a record writes base + i
-    auto prep = [&](uint32_t t, uint32_t b) {
-        const bool has = live && rv && R0.x == t;
-        if (__ballot(has)) {
-            uint32_t ne = has ? R0.w : 0u, tot = 0;
-            const uint32_t sb = wscan_excl(ne, tot);              // this row's first slot in the wave's area
-            const uint32_t xb = (uint32_t)CSR_WINMAX + wave * CSR_EXW + sb;
-            if (has && sb + ne > (uint32_t)CSR_EXW) fl |= CSR_F_SLOTS;
-            if (has) {
-#pragma unroll
-                for (int q = 0; q < 4; q++) {                      // the record's 32 u16 codes
-                    const u32x4 Rq = q == 0 ? R1 : q == 1 ? R2 : q == 2 ? R3 : R4;
-                    *(u32x4 *)(trow + 8 * q) = u32x4{Rq.x & 0xFFFFu, Rq.x >> 16, Rq.y & 0xFFFFu, Rq.y >> 16};
-                    *(u32x4 *)(trow + 8 * q + 4) = u32x4{Rq.z & 0xFFFFu, Rq.z >> 16, Rq.w & 0xFFFFu, Rq.w >> 16};
-                }
-                const uint32_t xa = xb * CSR_ESZ;
-                if (ne <= (uint32_t)CSR_EREG) {                    // exception codes: positions from the record
-                    const uint32_t pos = R0.z;
-                    if (ne > 0) trow[pos & 31u] = xa;
-                    if (ne > 1) trow[(pos >> 8) & 31u] = xa + CSR_ESZ;
-                    if (ne > 2) trow[(pos >> 16) & 31u] = xa + 2u * CSR_ESZ;
-                    if (ne > 3) trow[(pos >> 24) & 31u] = xa + 3u * CSR_ESZ;
-                } else {                                           // (rare) from the codes' flags
-                    for (int q = 0; q < CSR_SB; q++) {
-                        const uint32_t c = trow[q];
-                        if (c & CSR_EXC) trow[q] = xa + (c & 0x7FFFu) * CSR_ESZ;
-                    }
-                }
-                if (!(fl & CSR_F_SLOTS)) {
-                    if (ne > 0) put_entry(b, xb + 0, make_uint2(RE0a.x, RE0a.y), make_uint2(RE0a.z, RE0a.w), make_uint2(RE0b.x, RE0b.y));
-                    if (ne > 1) put_entry(b, xb + 1, make_uint2(RE1a.x, RE1a.y), make_uint2(RE1a.z, RE1a.w), make_uint2(RE1b.x, RE1b.y));
-                    if (ne > 2) put_entry(b, xb + 2, make_uint2(RE2a.x, RE2a.y), make_uint2(RE2a.z, RE2a.w), make_uint2(RE2b.x, RE2b.y));
-                    if (ne > 3) put_entry(b, xb + 3, make_uint2(RE3a.x, RE3a.y), make_uint2(RE3a.z, RE3a.w), make_uint2(RE3b.x, RE3b.y));
-                    for (uint32_t k = CSR_EREG; k < ne; k++) {      // more than CSR_EREG: synchronous loads (rare)
-                        const uint4 x0 = ent[2 * (ecur + k)], x1 = ent[2 * (ecur + k) + 1];
-                        put_entry(b, xb + k, make_uint2(x0.x, x0.y), make_uint2(x0.z, x0.w), make_uint2(x1.x, x1.y));
-                    }
-                }
-                s = (int32_t)R0.y;
-#pragma unroll
-                for (int q = 0; q < 8; q++) {                      // the codes back (this lane's own writes)
-                    const u32x4 v = *(const u32x4 *)(trow + 4 * q);
-                    code[4 * q] = v.x; code[4 * q + 1] = v.y; code[4 * q + 2] = v.z; code[4 * q + 3] = v.w;
-                }
-            }
-        }
-        if (was && !has) set_base();
-        was = has;
-    };
-
-    // super step 0
-    wload(wA0, wA1, 0);
-    wstore(wA0, wA1, 0);
-    wload(wB0, wB1, 1);
-    prep(0, 0);
-    if (live && rv && R0.x == 0) { base = csr_base(p, s); rcur++; ecur += R0.w; load_rec(rcur, ecur); }
-    __syncthreads();
-    CSR_STAMP(tl0);
-    // (the loop runs two super steps per trip, one per buffer, so that every staging set and LDS buffer is named at
-    // compile time: a buffer chosen at run time made the compiler select between the two sets' addresses and keep
-    // both in scratch)
-    auto iter = [&](uint32_t t, auto BC) {
-        constexpr uint32_t b = decltype(BC)::value;
-        const uint32_t K0 = t * CSR_SB;
-        // set b is free: super step t is in LDS. (Issued even past the last super step, from clamped positions: with
-        // the loads on one path only, the wait before the stores of the other set had to cover the path without them,
-        // i.e. these very loads.)
-        if constexpr (b) wload(wB0, wB1, t + 2);
-        else wload(wA0, wA1, t + 2);
-        // ---- the chain over blocks K0 .. K0 + 31 ----
-        // The block loop is straight-line code per variant (FULL: every row's chain covers the whole super step, no
-        // predication), and each block's three LDS reads are issued CSR_PF blocks ahead of its arithmetic: a read
-        // followed at once by its use waits the whole LDS latency (about 120 cycles with four waves reading), twice
-        // the chain's own cost of a block.
-        CSR_STAMP(ts0);
-        const bool full = __all(myit == 0u || K0 + CSR_SB <= myit);
-        const char *EAb = (const char *)EA[b], *EBb = (const char *)EB;
-        auto run = [&](auto FULLC) {
-            constexpr bool FULL = decltype(FULLC)::value;
-            u32x4 va[CSR_PF + 1], vb[CSR_PF + 1];
-            auto fetch = [&](int i) {
-#ifdef CSR_DIAG_BCAST
-                // (diagnostic build only: every lane reads lane 0's entries: wrong checksums, no bank conflicts)
-                const uint32_t c = (uint32_t)__builtin_amdgcn_readfirstlane((int)code[i]);
-#else
-                const uint32_t c = code[i];
-#endif
-                va[i % (CSR_PF + 1)] = *(const u32x4 *)(EAb + c);
-                vb[i % (CSR_PF + 1)] = *(const u32x4 *)(EBb + c);
-            };
-#pragma unroll
-            for (int i = 0; i < CSR_PF; i++) fetch(i);
-#pragma unroll
-            for (int i = 0; i < CSR_SB; i++) {
-                if (i + CSR_PF < CSR_SB) fetch(i + CSR_PF);
-                const u32x4 A = va[i % (CSR_PF + 1)], B = vb[i % (CSR_PF + 1)];
-                if (FULL) {
-                    csd_block3(Xg, Xf, Xh, A.x, A.y, A.z, A.w, b ? B.z : B.x, b ? B.w : B.y);
-                } else {
-                    uint32_t ng = Xg, nf = Xf, nh = Xh;
-                    csd_block3(ng, nf, nh, A.x, A.y, A.z, A.w, b ? B.z : B.x, b ? B.w : B.y);
-                    const bool act = K0 + (uint32_t)i < myit;
-                    Xg = act ? ng : Xg;
-                    Xf = act ? nf : Xf;
-                    Xh = act ? nh : Xh;
-                }
-            }
-        };
-        if (full) run(std::integral_constant<bool, true>{});
-        else run(std::integral_constant<bool, false>{});
-        // ---- the next super step's window, rows and entries into the other buffer ----
-        // (kept after the chain: hoisted above it, the stores of a staging set would wait for its loads there)
-        asm volatile("" ::: "memory");
-        CSR_STAMP(ts1);
-        CSR_ACC(0, ts1 - ts0);
-        // (run after the last super step too, into a buffer nobody reads: skipped on one path, the staging set's loads
-        // stay pending on it, and the compiler waits for every load at the loop head before reusing their registers)
-        if constexpr (b) wstore(wA0, wA1, 0u);                      // super step t + 1 (even) -> buffer 0
-        else wstore(wB0, wB1, 1u);
-        prep(t + 1, b ^ 1u);
-        // (the record loads run for the whole wave whenever one of its rows moves on, the others reloading their
-        // current record: a load into only some lanes keeps the old values live in the rest, and the compiler
-        // copies the loaded registers over them, waiting for the loads right here)
-        const bool adv = live && rv && R0.x == t + 1;
-        if (adv) { base = csr_base(p, s); rcur++; ecur += R0.w; }
-        if (__ballot(adv)) load_rec(rcur, ecur);
-        CSR_STAMP(ts2);
-        __syncthreads();
-        CSR_STAMP(ts3);
-        CSR_ACC(1, ts2 - ts1);
-        CSR_ACC(2, ts3 - ts2);
-    };
-    // (both super steps of a trip always run, the odd last one after the loop: the loop head is then reached from
-    // one kind of trip only, and the loads in flight there are always the same)
-    uint32_t t = 0;
-    for (; t + 1 < T_; t += 2) {
-        iter(t, std::integral_constant<uint32_t, 0>{});
-        iter(t + 1, std::integral_constant<uint32_t, 1>{});
-    }
-    if (t < T_) iter(t, std::integral_constant<uint32_t, 0>{});
-    CSR_STAMP(tl1);
-    CSR_ACC(3, tl1 - tl0);
-#ifdef CSR_DIAG_STAMP
-    if (lane == 0)
-        for (int k = 0; k < 4; k++) ctr_add(d, C_NALL + k, (unsigned long long)st_[k]);
-#endif
-#undef CSR_STAMP
-#undef CSR_ACC
-    const bool mine = valid && fl == 0;
-    const uint32_t nmine = (uint32_t)__popcll(__ballot(mine));
-    if (lane == 0 && nmine) ctr_add(d, C_X_CS_ROWS, (unsigned long long)nmine);   // rows this launch hashed
-    if (!valid) return;
-    if (!mine) {                                                    // left to the production kernels
-        const uint32_t at = atomicAdd(a.fb_cnt, 1u);
-        a.fb_list[at] = id;
-        // by reason (swimsim_checksum_path_stats): short, entry/run capacity, window plan, record capacity, slots
-        const uint32_t r = (fl & CSD_F_SHORT) ? 0u : (fl & CSD_F_ECAP) ? 1u : (fl & CSR_F_PLAN) ? 2u : (fl & CSR_F_RCAP) ? 3u
-                         : (fl & CSR_F_SLOTS) ? 4u : 6u;
-        atomicAdd(a.fb_cnt + 1 + r, 1u);
-        return;
-    }
-    fh.h = Xh; fh.g = Xg; fh.f = Xf;
-    const uint32_t hv = ok ? fh.fin() : 0u;
-    if (is_row) {
-        d.cs[id] = hv;
-        d.dirty[id] = 0;
-    } else {
-        d.dense_cs[id - d.NL] = hv;
-    }
-}
-
 // ---------------------------------------------------------------------------------------------------------------
 // k_csr2: the chains with the h lane in a wave of its own (round 5). A block is 12 VALU instructions over three
 // lanes of one row, of which h is independent of the coupled g and f. With one lane per row, 65,536 rows fill the
@@ -694,6 +375,23 @@ __device__ __forceinline__ void csr2_role(const DS &d, const uint32_t *list, con
         was = has;
     };
 
+#ifdef CSR_DIAG_STAMP
+    // (diagnostic build only: shader-clock stamps of the g/f waves, summed into the diagnostic counters: 0 chain,
+    // 1 staging + preparation, 2 barrier, 3 whole loop)
+    uint64_t st_[4] = {0, 0, 0, 0};
+    auto stamp = [&]() -> uint64_t {
+        uint64_t tt;
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tt) :: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        return tt;
+    };
+#define CSR2_STAMP(v) const uint64_t v = stamp()
+#define CSR2_ACC(k, x) st_[k] += (x)
+#else
+#define CSR2_STAMP(v)
+#define CSR2_ACC(k, x)
+#endif
     // super step 0
     wload(wA, 0);
     wstore(wA, 0);
@@ -701,11 +399,13 @@ __device__ __forceinline__ void csr2_role(const DS &d, const uint32_t *list, con
     prep(0, 0);
     if (live && rv && R0.x == 0) { base = csr_base(p, s); rcur++; ecur += R0.w; load_rec(rcur, ecur); }
     lds_barrier();
+    CSR2_STAMP(tl0);
     auto iter = [&](uint32_t t, auto BC) {
         constexpr uint32_t b = decltype(BC)::value;
         const uint32_t K0 = t * CSR_SB;
         if constexpr (b) wload(wB, t + 2);
         else wload(wA, t + 2);
+        CSR2_STAMP(ts0);
         const bool full = __all(myit == 0u || K0 + CSR_SB <= myit);
         const char *Eb = GF ? (const char *)EA[b] : (const char *)EB[b];
         auto run = [&](auto FULLC) {
@@ -733,13 +433,19 @@ __device__ __forceinline__ void csr2_role(const DS &d, const uint32_t *list, con
         if (full) run(std::integral_constant<bool, true>{});
         else run(std::integral_constant<bool, false>{});
         asm volatile("" ::: "memory");
+        CSR2_STAMP(ts1);
+        CSR2_ACC(0, ts1 - ts0);
         if constexpr (b) wstore(wA, 0u);                           // super step t + 1 (even) -> buffer 0
         else wstore(wB, 1u);
         prep(t + 1, b ^ 1u);
         const bool adv = live && rv && R0.x == t + 1;
         if (adv) { base = csr_base(p, s); rcur++; ecur += R0.w; }
         if (__ballot(adv)) load_rec(rcur, ecur);
+        CSR2_STAMP(ts2);
         lds_barrier();
+        CSR2_STAMP(ts3);
+        CSR2_ACC(1, ts2 - ts1);
+        CSR2_ACC(2, ts3 - ts2);
     };
     uint32_t t = 0;
     for (; t + 1 < T_; t += 2) {
@@ -747,6 +453,14 @@ __device__ __forceinline__ void csr2_role(const DS &d, const uint32_t *list, con
         iter(t + 1, std::integral_constant<uint32_t, 1>{});
     }
     if (t < T_) iter(t, std::integral_constant<uint32_t, 0>{});
+    CSR2_STAMP(tl1);
+    CSR2_ACC(3, tl1 - tl0);
+#ifdef CSR_DIAG_STAMP
+    if (GF && (threadIdx.x & 63u) == 0)
+        for (int k = 0; k < 4; k++) ctr_add(d, C_NALL + k, (unsigned long long)st_[k]);
+#endif
+#undef CSR2_STAMP
+#undef CSR2_ACC
 
     if constexpr (!GF) XH[tid] = X0;
     lds_barrier();
@@ -790,6 +504,386 @@ __global__ void __launch_bounds__(2 * CSR_ROWS) k_csr2(DS d, const uint32_t *lis
     else csr2_role<W, 1>(d, list, cnt, a, p, EA, EB, XH, phs);
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// k_csr3: chain waves that only run chains (round 5). k_csr2's waves spent 39 % (light rounds) to 55 % (heavy) of
+// their loop outside the chain: staging the next super step's window, unpacking records, writing exception entries,
+// and waiting at the per-super-step barrier for the slowest of the eight (shader-clock stamps, tools/csr_stamps.py).
+// Here a third wave per SIMD, the stager (lane = row), does all of that one super step ahead, and no barrier is left
+// in the loop: buffer b of the window, exception areas and code table is handed over by two LDS counters,
+// ready[b] (stagers that finished filling it: 4 per super step) and done[b] (chain waves that finished reading it: 8
+// per super step). A chain wave waits only until the stagers have filled the super step it needs, reads its row's 32
+// codes (u16, written by the stager: base(s) + i, or a record's codes with its exceptions patched to the wave's slots)
+// and runs the chain. Roles: waves 0-3 g/f lanes, 4-7 h lanes, 8-11 stagers; waves w, w + 4 and w + 8 share a SIMD
+// and rows 64 w .. 64 w + 63.
+// ---------------------------------------------------------------------------------------------------------------
+constexpr int C3_EXW = 384;
+constexpr int C3_ENT = CSR_WINMAX + 4 * C3_EXW;
+
+struct Csr3Lds {
+    uint4 EA[2][C3_ENT];                   // {Mg, D, Mf, PF} per entry
+    uint2 EB[2][C3_ENT];                   // {Mh, KH}
+    uint4 TC[2][4][CSR_ROWS];              // codes: TC[b][q][row] = u16 codes 8q .. 8q + 7 of the row (lane-contiguous)
+    uint32_t XH[CSR_ROWS];                 // h lanes' final state
+    uint32_t FLX[CSR_ROWS];                // rows the stagers flagged (exception slots)
+    uint32_t ready[2], done[2];
+    uint32_t phs[20];
+};
+
+__device__ __forceinline__ void c3_wait(const uint32_t *ctr, uint32_t target) {
+    while (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target) __builtin_amdgcn_s_sleep(1);
+}
+__device__ __forceinline__ void c3_signal(uint32_t *ctr) {
+    if ((threadIdx.x & 63u) == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+struct C3Row {                                                      // what every role knows of its row
+    uint32_t gi, id, fl, iters, nrec;
+    bool valid, is_row, live;
+    CsdRow ri;
+};
+__device__ __forceinline__ C3Row c3_row(const DS &d, const uint32_t *list, uint32_t cnt, const CsrArgs &a,
+                                        const CsrPlan &p, uint32_t tid) {
+    C3Row r;
+    const uint32_t g0 = blockIdx.x * CSR_ROWS;
+    r.gi = g0 + tid;
+    r.valid = r.gi < cnt;
+    r.id = list[r.valid ? r.gi : g0];
+    r.is_row = r.id < d.NL;
+    r.ri = a.rinfo[r.valid ? r.gi : g0];
+    r.nrec = r.valid ? a.nrec[r.gi] : 0u;
+    const uint32_t len = csd_len(d, r.id);
+    r.iters = len > 24 ? (len - 1) / 20 : 0u;
+    r.fl = !r.valid ? 0u : r.ri.flags ? r.ri.flags : !p.feasible || r.ri.ecnt > p.ecmax ? CSR_F_PLAN
+         : r.nrec == 0xFFFFFFFFu ? CSR_F_RCAP : 0u;
+    if (r.valid && !r.fl && r.iters == 0) r.fl = CSD_F_SHORT;
+    r.live = r.valid && r.fl == 0;
+    return r;
+}
+
+// the stager of rows 64 w .. 64 w + 63 (lane = row) and of a quarter of every super step's window
+__device__ __forceinline__ void c3_stage(const DS &d, const uint32_t *list, uint32_t cnt, const CsrArgs &a, const CsrPlan &p,
+                                         Csr3Lds &L, uint32_t T_) {
+    const uint32_t tid = threadIdx.x & (CSR_ROWS - 1), rwave = tid >> 6;
+    C3Row r = c3_row(d, list, cnt, a, p, tid);
+    const CsrRec *rec = a.rec + (size_t)(r.valid ? r.gi : blockIdx.x * CSR_ROWS) * a.rcap;
+    const uint4 *ent = a.ent + (size_t)(r.valid ? r.gi : blockIdx.x * CSR_ROWS) * a.ecap * 2;
+    const uint32_t nr = r.live ? r.nrec : 0u;
+    uint32_t rcur = 0, ecur = 0;
+    bool rv = false;
+    u32x4 R0, R1, R2, R3, R4;
+    u32x4 EA0, EA1, EA2, EA3;
+    u32x2 EB0, EB1, EB2, EB3;
+    auto load_rec = [&](uint32_t q, uint32_t e0) {
+        const u32x4 *rp = (const u32x4 *)(rec + min(q, a.rcap - 1u));
+        R0 = rp[0]; R1 = rp[1]; R2 = rp[2]; R3 = rp[3]; R4 = rp[4];
+        const u32x4 *ep = (const u32x4 *)(ent + 2 * min(e0, a.ecap - (uint32_t)CSR_EREG));
+        EA0 = ep[0]; EB0 = *(const u32x2 *)(ep + 1);
+        EA1 = ep[2]; EB1 = *(const u32x2 *)(ep + 3);
+        EA2 = ep[4]; EB2 = *(const u32x2 *)(ep + 5);
+        EA3 = ep[6]; EB3 = *(const u32x2 *)(ep + 7);
+        rv = q < nr;
+    };
+    load_rec(0, 0);
+    // window: entries u = tid + 256 v (both halves), two register sets (super step u -> set u & 1), loaded two ahead
+    constexpr int WV = CSR_WINMAX / CSR_ROWS;
+    u32x4 wA0[WV], wB0[WV];
+    u32x2 wA1[WV], wB1[WV];
+    const uint32_t nwin = p.nph * p.Wn;
+    uint32_t wsrc[WV];                                               // (phase rows of P as entry offsets: 32-bit)
+    int32_t wk0[WV];
+#pragma unroll
+    for (int v = 0; v < WV; v++) {
+        const uint32_t u = tid + (uint32_t)CSR_ROWS * v;
+        const uint32_t ps = u < nwin ? u / p.Wn : 0u, w = u < nwin ? u - ps * p.Wn : 0u;
+        wsrc[v] = L.phs[min(ps, 19u)] * a.KP;
+        wk0[v] = u < nwin ? (int32_t)w - p.cmax : 0x40000000;
+    }
+    auto wload = [&](u32x4 (&w0)[WV], u32x2 (&w1)[WV], uint32_t t) {
+#pragma unroll
+        for (int v = 0; v < WV; v++) {
+            const int32_t k = min(max(wk0[v] + (int32_t)(t * CSR_SB), 0), (int32_t)a.KP - 1);
+            const uint4 *src = a.P + 2 * (size_t)(wsrc[v] + (uint32_t)k);
+            w0[v] = *(const u32x4 *)src;
+            w1[v] = *(const u32x2 *)(src + 1);
+        }
+    };
+    auto wstore = [&](const u32x4 (&w0)[WV], const u32x2 (&w1)[WV], uint32_t b) {
+#pragma unroll
+        for (int v = 0; v < WV; v++) {
+            const uint32_t u = tid + (uint32_t)CSR_ROWS * v;
+            *(u32x4 *)&L.EA[b][u] = w0[v];
+            *(u32x2 *)&L.EB[b][u] = w1[v];
+        }
+    };
+    int32_t s = 0;
+    uint32_t base = csr_base(p, 0);
+    uint32_t tag[2] = {0xFFFFFFFEu, 0xFFFFFFFEu};                  // what TC[b][.][row] holds: a base, or a record
+    // one super step's codes and exceptions of this row into buffer b
+    auto prep = [&](uint32_t t, uint32_t b) {
+        const bool has = r.live && rv && R0.x == t;
+        if (__ballot(has)) {
+            uint32_t ne = has ? R0.w : 0u, tot = 0;
+            const uint32_t sb = wscan_excl(ne, tot);
+            const uint32_t xb = (uint32_t)CSR_WINMAX + rwave * C3_EXW + sb;
+            if (has && sb + ne > (uint32_t)C3_EXW) r.fl |= CSR_F_SLOTS;
+            if (has) {
+                L.TC[b][0][tid] = make_uint4(R1.x, R1.y, R1.z, R1.w);
+                L.TC[b][1][tid] = make_uint4(R2.x, R2.y, R2.z, R2.w);
+                L.TC[b][2][tid] = make_uint4(R3.x, R3.y, R3.z, R3.w);
+                L.TC[b][3][tid] = make_uint4(R4.x, R4.y, R4.z, R4.w);
+                tag[b] = 0xFFFFFFFFu;
+                if (!(r.fl & CSR_F_SLOTS)) {
+                    const uint32_t xa = xb * CSR_ESZ;
+                    // exception codes -> the wave's slots (u16 stores into the row's codes): block i lives in
+                    // TC[b][i / 8][row], byte 2 (i % 8)
+                    auto patch = [&](uint32_t i, uint32_t ord) {
+                        uint16_t *c16 = (uint16_t *)&L.TC[b][i >> 3][tid] + (i & 7u);
+                        *c16 = (uint16_t)(xa + ord * CSR_ESZ);
+                    };
+                    if (ne <= (uint32_t)CSR_EREG) {
+                        const uint32_t pos = R0.z;
+                        if (ne > 0) patch(pos & 31u, 0);
+                        if (ne > 1) patch((pos >> 8) & 31u, 1);
+                        if (ne > 2) patch((pos >> 16) & 31u, 2);
+                        if (ne > 3) patch((pos >> 24) & 31u, 3);
+                    } else {                                       // (rare) from the codes' flags, in LDS
+                        const uint16_t *cw = (const uint16_t *)&L.TC[b][0][tid];
+                        for (uint32_t i = 0; i < (uint32_t)CSR_SB; i++) {
+                            const uint32_t c = ((const uint16_t *)&L.TC[b][i >> 3][tid])[i & 7u];
+                            if (c & CSR_EXC) patch(i, c & 0x7FFFu);
+                        }
+                        (void)cw;
+                    }
+                    auto putx = [&](uint32_t e, const u32x4 &x, const u32x2 &y) {
+                        *(u32x4 *)&L.EA[b][e] = x;
+                        *(u32x2 *)&L.EB[b][e] = y;
+                    };
+                    if (ne > 0) putx(xb + 0, EA0, EB0);
+                    if (ne > 1) putx(xb + 1, EA1, EB1);
+                    if (ne > 2) putx(xb + 2, EA2, EB2);
+                    if (ne > 3) putx(xb + 3, EA3, EB3);
+                    for (uint32_t k = CSR_EREG; k < ne; k++) {      // more than CSR_EREG: synchronous loads (rare)
+                        const uint4 *ep = ent + 2 * (ecur + k);
+                        putx(xb + k, *(const u32x4 *)ep, *(const u32x2 *)(ep + 1));
+                    }
+                }
+                s = (int32_t)R0.y;
+            }
+        }
+        if (!has) {
+            const uint32_t want = r.live ? base : 0xFFFFFFFDu;      // (rows not hashed read entry 0)
+            if (tag[b] != want) {
+                const uint32_t c0 = r.live ? base * CSR_ESZ : 0u, st2 = r.live ? 2u * CSR_ESZ : 0u, st1 = r.live ? CSR_ESZ : 0u;
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const uint32_t c = c0 + (uint32_t)(4 * q) * st2;
+                    L.TC[b][q][tid] = make_uint4(c | ((c + st1) << 16), (c + st2) | ((c + st2 + st1) << 16),
+                                                 (c + 2 * st2) | ((c + 2 * st2 + st1) << 16),
+                                                 (c + 3 * st2) | ((c + 3 * st2 + st1) << 16));
+                }
+                tag[b] = want;
+            }
+        }
+        const bool adv = has;
+        if (adv) { base = csr_base(p, s); rcur++; ecur += R0.w; }
+        if (__ballot(adv)) load_rec(rcur, ecur);
+    };
+#ifdef CSR_DIAG_STAMP
+    // (diagnostic build only: the stagers' shader-clock stamps into diagnostic counters 4-7: waiting for the chains,
+    // the window, the rows' codes and exceptions, the hand-over)
+    uint64_t st_[4] = {0, 0, 0, 0};
+    auto stamp = [&]() -> uint64_t {
+        uint64_t tt;
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tt) :: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        return tt;
+    };
+#define C3S_STAMP(v) const uint64_t v = stamp()
+#define C3S_ACC(k, x) st_[k] += (x)
+#else
+#define C3S_STAMP(v)
+#define C3S_ACC(k, x)
+#endif
+    wload(wA0, wA1, 0);
+    wload(wB0, wB1, 1);
+    auto step = [&](uint32_t u, auto BC) {
+        constexpr uint32_t b = decltype(BC)::value;
+        C3S_STAMP(s0);
+        if (u >= 2) c3_wait(&L.done[b], 8u * (u >> 1));           // the chains are done with super step u - 2
+        C3S_STAMP(s1);
+        // (window loads before the records' loads: issued after them (loads complete in order, and the compiler
+        // waits for every load of the wave that may precede a set's), the stores of a set waited for the last step's
+        // records and the heavy rounds took 4 % longer)
+        if constexpr (b) { wstore(wB0, wB1, 1u); wload(wB0, wB1, u + 2); }
+        else { wstore(wA0, wA1, 0u); wload(wA0, wA1, u + 2); }
+        C3S_STAMP(s2);
+        prep(u, b);
+        C3S_STAMP(s3);
+        c3_signal(&L.ready[b]);
+        C3S_STAMP(s4);
+        C3S_ACC(0, s1 - s0);
+        C3S_ACC(1, s2 - s1);
+        C3S_ACC(2, s3 - s2);
+        C3S_ACC(3, s4 - s3);
+    };
+    uint32_t u = 0;
+    for (; u + 1 < T_; u += 2) {
+        step(u, std::integral_constant<uint32_t, 0>{});
+        step(u + 1, std::integral_constant<uint32_t, 1>{});
+    }
+    if (u < T_) step(u, std::integral_constant<uint32_t, 0>{});
+#ifdef CSR_DIAG_STAMP
+    if ((threadIdx.x & 63u) == 0)
+        for (int k = 0; k < 4; k++) ctr_add(d, C_NALL + 4 + k, (unsigned long long)st_[k]);
+#endif
+#undef C3S_STAMP
+#undef C3S_ACC
+    L.FLX[tid] = r.fl;
+}
+
+template <int W, int ROLE>                                          // ROLE 0: g/f lanes, 1: h lanes
+__device__ __forceinline__ void c3_chain(const DS &d, const uint32_t *list, uint32_t cnt, const CsrArgs &a, const CsrPlan &p,
+                                         Csr3Lds &L, uint32_t T_) {
+    constexpr bool GF = ROLE == 0;
+    typedef typename std::conditional<GF, u32x4, u32x2>::type EV;
+    const uint32_t tid = threadIdx.x & (CSR_ROWS - 1);
+    const C3Row r = c3_row(d, list, cnt, a, p, tid);
+    const uint32_t myit = r.live ? r.iters : 0u;
+    const uint32_t *row = csd_row(d, r.id);
+    FH fh{0, 0, 0};
+    uint32_t it2 = 0;
+    const bool ok = cs_prologue<W>(d, r.id, r.is_row, row, fh, it2);
+    uint32_t X0 = GF ? fh.g + r.ri.b0 : fh.h + r.ri.a0;             // Xg, or Xh
+    uint32_t X1 = GF ? fh.f + r.ri.c0 : 0u;                         // Xf
+#ifdef CSR_DIAG_STAMP
+    // (diagnostic build only: shader-clock stamps of the g/f waves, summed into the diagnostic counters: 0 chain,
+    // 1 waiting for the stagers, 2 codes, 3 whole loop)
+    uint64_t st_[4] = {0, 0, 0, 0};
+    auto stamp = [&]() -> uint64_t {
+        uint64_t tt;
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tt) :: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        return tt;
+    };
+#define C3_STAMP(v) const uint64_t v = stamp()
+#define C3_ACC(k, x) st_[k] += (x)
+#else
+#define C3_STAMP(v)
+#define C3_ACC(k, x)
+#endif
+    C3_STAMP(tl0);
+    uint32_t code[CSR_SB];
+    auto step = [&](uint32_t t, auto BC) {
+        constexpr uint32_t b = decltype(BC)::value;
+        const uint32_t K0 = t * CSR_SB;
+        C3_STAMP(ta);
+        c3_wait(&L.ready[b], 4u * ((t >> 1) + 1u));               // the stagers have filled super step t
+        C3_STAMP(tb);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint4 v = L.TC[b][q][tid];
+            const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                if constexpr (GF) { code[8 * q + 2 * j] = w4[j] & 0xFFFFu; code[8 * q + 2 * j + 1] = w4[j] >> 16; }
+                else { code[8 * q + 2 * j] = __builtin_amdgcn_ubfe(w4[j], 1, 15); code[8 * q + 2 * j + 1] = w4[j] >> 17; }
+            }
+        }
+        C3_STAMP(tc);
+        const bool full = __all(myit == 0u || K0 + CSR_SB <= myit);
+        const char *Eb = GF ? (const char *)L.EA[b] : (const char *)L.EB[b];
+        auto run = [&](auto FULLC) {
+            constexpr bool FULL = decltype(FULLC)::value;
+            EV va[CSR_PF + 1];
+            auto fetch = [&](int i) { va[i % (CSR_PF + 1)] = *(const EV *)(Eb + code[i]); };
+#pragma unroll
+            for (int i = 0; i < CSR_PF; i++) fetch(i);
+#pragma unroll
+            for (int i = 0; i < CSR_SB; i++) {
+                if (i + CSR_PF < CSR_SB) fetch(i + CSR_PF);
+                const EV A = va[i % (CSR_PF + 1)];
+                uint32_t n0 = X0, n1 = X1;
+                if constexpr (GF) csd_gf_step(n0, n1, A.x, A.y, A.z, A.w);
+                else csd_h_step(n0, A.x, A.y);
+                if (FULL) {
+                    X0 = n0; X1 = n1;
+                } else {
+                    const bool act = K0 + (uint32_t)i < myit;
+                    X0 = act ? n0 : X0;
+                    X1 = act ? n1 : X1;
+                }
+            }
+        };
+        if (full) run(std::integral_constant<bool, true>{});
+        else run(std::integral_constant<bool, false>{});
+        c3_signal(&L.done[b]);
+        C3_STAMP(td);
+        C3_ACC(0, td - tc);
+        C3_ACC(1, tb - ta);
+        C3_ACC(2, tc - tb);
+    };
+    uint32_t t = 0;
+    for (; t + 1 < T_; t += 2) {
+        step(t, std::integral_constant<uint32_t, 0>{});
+        step(t + 1, std::integral_constant<uint32_t, 1>{});
+    }
+    if (t < T_) step(t, std::integral_constant<uint32_t, 0>{});
+    C3_STAMP(tl1);
+    C3_ACC(3, tl1 - tl0);
+#ifdef CSR_DIAG_STAMP
+    if (GF && (threadIdx.x & 63u) == 0)
+        for (int k = 0; k < 4; k++) ctr_add(d, C_NALL + k, (unsigned long long)st_[k]);
+#endif
+#undef C3_STAMP
+#undef C3_ACC
+    if constexpr (!GF) L.XH[tid] = X0;
+    __syncthreads();                                                // (every wave: XH and the stagers' FLX)
+    if constexpr (GF) {
+        const uint32_t fl = r.fl | L.FLX[tid];
+        const bool mine = r.valid && fl == 0;
+        const uint32_t nmine = (uint32_t)__popcll(__ballot(mine));
+        if ((threadIdx.x & 63u) == 0 && nmine) ctr_add(d, C_X_CS_ROWS, (unsigned long long)nmine);
+        if (!r.valid) return;
+        if (!mine) {                                                // left to the production kernels
+            const uint32_t at = atomicAdd(a.fb_cnt, 1u);
+            a.fb_list[at] = r.id;
+            const uint32_t rr = (fl & CSD_F_SHORT) ? 0u : (fl & CSD_F_ECAP) ? 1u : (fl & CSR_F_PLAN) ? 2u
+                              : (fl & CSR_F_RCAP) ? 3u : 4u;
+            atomicAdd(a.fb_cnt + 1 + rr, 1u);
+            return;
+        }
+        fh.h = L.XH[tid]; fh.g = X0; fh.f = X1;
+        const uint32_t hv = ok ? fh.fin() : 0u;
+        if (r.is_row) {
+            d.cs[r.id] = hv;
+            d.dirty[r.id] = 0;
+        } else {
+            d.dense_cs[r.id - d.NL] = hv;
+        }
+    }
+}
+
+template <int W>
+__global__ void __launch_bounds__(3 * CSR_ROWS) k_csr3(DS d, const uint32_t *list, const uint32_t *count, CsrArgs a) {
+    __shared__ Csr3Lds L;
+    const uint32_t cnt = *count;
+    if (blockIdx.x * CSR_ROWS >= cnt) return;
+    const CsrPlan p = a.plan[blockIdx.x];
+    if (threadIdx.x < 20 && ((p.phm >> threadIdx.x) & 1u)) L.phs[__popc(p.phm & ((1u << threadIdx.x) - 1u))] = threadIdx.x;
+    if (threadIdx.x < 2) { L.ready[threadIdx.x] = 0; L.done[threadIdx.x] = 0; }
+    __syncthreads();
+    const uint32_t T_ = p.feasible ? (p.maxit + CSR_SB - 1) / CSR_SB : 0u;
+    const uint32_t role = threadIdx.x / CSR_ROWS;
+    if (role == 0) c3_chain<W, 0>(d, list, cnt, a, p, L, T_);
+    else if (role == 1) c3_chain<W, 1>(d, list, cnt, a, p, L, T_);
+    else {
+        c3_stage(d, list, cnt, a, p, L, T_);
+        __syncthreads();                                            // (the chain waves' final barrier)
+    }
+}
+
 // launches of the path (part): 0 S_B string, 1 P table, 2 scan, 3 plan + records, 4 the chains
 template <int W>
 void launch_csr_w(const DS &d, const uint32_t *list, uint32_t n, const uint32_t *count, const CsdArgs &ca, const CsrArgs &a,
@@ -805,9 +899,9 @@ void launch_csr_w(const DS &d, const uint32_t *list, uint32_t n, const uint32_t 
         hipLaunchKernelGGL(k_csr_plan, dim3((n + CSR_ROWS - 1) / CSR_ROWS), dim3(CSR_ROWS), 0, s, d, list, n, a);
         hipLaunchKernelGGL(k_csr_rec, dim3((n + 3) / 4), dim3(256), 0, s, d, list, n, a);
     } else if (part == 4) {
+        hipLaunchKernelGGL((k_csr3<W>), dim3((n + CSR_ROWS - 1) / CSR_ROWS), dim3(3 * CSR_ROWS), 0, s, d, list, count, a);
+    } else {                                                        // (k_csr2, for comparison)
         hipLaunchKernelGGL((k_csr2<W>), dim3((n + CSR_ROWS - 1) / CSR_ROWS), dim3(2 * CSR_ROWS), 0, s, d, list, count, a);
-    } else {                                                        // (round 4's one-wave chains, for comparison)
-        hipLaunchKernelGGL((k_csr<W>), dim3((n + CSR_ROWS - 1) / CSR_ROWS), dim3(CSR_ROWS), 0, s, d, list, count, a);
     }
 }
 

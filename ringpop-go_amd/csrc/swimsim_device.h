@@ -43,7 +43,7 @@ enum Counter {
 };
 
 constexpr int CTR_SHARDS = 64, CTR_STRIDE = 40;   // d.ctr is [CTR_SHARDS][CTR_STRIDE] u64
-static_assert(C_NALL + 4 <= CTR_STRIDE, "counter block too small (4 diagnostic slots follow C_NALL)");
+static_assert(C_NALL + 8 <= CTR_STRIDE, "counter block too small (8 diagnostic slots follow C_NALL)");
 constexpr uint32_t POOL_SHARDS = 64, POOL_CUR_STRIDE = 16;   // d.pool_cur is [POOL_SHARDS][POOL_CUR_STRIDE] u64
 
 enum ErrBits : uint32_t {

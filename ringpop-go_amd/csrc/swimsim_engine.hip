@@ -2608,10 +2608,10 @@ int swimsim_kernel_units(swimsim_t *h, const char **names, double *values, size_
     static const char *kn[] = {"cs_rows_wide", "cs_rows_narrow", "cs_dup_rows", "recv_merged", "recv_applied",
                                "recv_issued", "recv_calls", "resp_merged", "resp_applied", "resp_bumped", "issued",
                                "bitmap_words_per_row", "diag_stamp0", "diag_stamp1", "diag_stamp2", "diag_stamp3",
-                               "hot_slots"};
+                               "hot_slots", "diag_stamp4", "diag_stamp5", "diag_stamp6", "diag_stamp7"};
     const int ki[] = {C_X_CS_ROWS, C_X_CS_ROWS_N, C_X_CS_DUP, C_X_MERGED, C_X_APPLIED, C_X_RISSUED, C_X_RCALLS,
                       C_X_MERGED_R, C_X_APPLIED_R, C_X_BUMPED, C_X_ISSUED, -1, C_NALL, C_NALL + 1, C_NALL + 2, C_NALL + 3,
-                      -2};
+                      -2, C_NALL + 4, C_NALL + 5, C_NALL + 6, C_NALL + 7};
     uint32_t hot = 0;                                              // hot slots in use now (not a delta)
     if (h->d.hot_cnt) {
         HIPCHK(h, hipMemcpyAsync(&hot, h->d.hot_cnt, 4, hipMemcpyDeviceToHost, h->s));

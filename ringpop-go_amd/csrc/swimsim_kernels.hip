@@ -167,18 +167,26 @@ __device__ __forceinline__ void merge_change(const DS &d, uint32_t ol, uint32_t 
 __device__ __forceinline__ void fold_row(const DS &d, uint32_t ol, int dping, int ddc, int napp, int nref, int evict,
                                          int dlen, int maxlast, int inval, unsigned long long dfp, bool next_update = true,
                                          int dnh = 0) {
-    if (napp && next_update && d.useq) d.useq[ol] += 1ull;          // the next Update of this row takes the next tag
-    if (dnh) d.nhe[ol] += dnh;
-    if (dfp) d.fp[ol] += dfp;
-    if (dping) d.ping[ol] += dping;
-    if (ddc) d.dcnt[ol] += ddc;
+    if (!(dnh | dping | ddc | napp | evict | dlen | inval) && !dfp && maxlast <= -1 && !nref) return;
+    // every read first, then the writes: one memory round trip per Update instead of one per field (each
+    // read-modify-write of a row field below would otherwise wait for its own load)
+    const int nhe0 = d.nhe[ol], ping0 = d.ping[ol], dcnt0 = d.dcnt[ol], clast0 = d.clast[ol];
+    const unsigned long long fp0 = d.fp[ol];
+    const uint32_t clen0 = d.clen[ol];
+    const unsigned long long useq0 = d.useq ? d.useq[ol] : 0ull;
+    if (napp && next_update && d.useq) d.useq[ol] = useq0 + 1ull;  // the next Update of this row takes the next tag
+    if (dnh) d.nhe[ol] = nhe0 + dnh;
+    if (dfp) d.fp[ol] = fp0 + dfp;
+    const int ping1 = ping0 + dping;
+    if (dping) d.ping[ol] = ping1;
+    if (ddc) d.dcnt[ol] = dcnt0 + ddc;
     if (napp) {
-        d.maxp[ol] = (int32_t)d.pfactor * digits10(d.ping[ol]);    // AdjustMaxPropagations
+        d.maxp[ol] = (int32_t)d.pfactor * digits10(ping1);          // AdjustMaxPropagations
         ctr_add(d, C_APPLIED, (unsigned long long)napp);
     }
     if (napp || evict) d.dirty[ol] = 1;                            // ComputeChecksum pending
-    if (dlen) d.clen[ol] += dlen;
-    if (maxlast > d.clast[ol]) d.clast[ol] = maxlast;
+    if (dlen) d.clen[ol] = clen0 + (uint32_t)dlen;
+    if (maxlast > clast0) d.clast[ol] = maxlast;
     else if (inval) d.clast[ol] = -2;                              // rescanned by the checksum kernel
     if (nref) ctr_add(d, C_REFUTES, (unsigned long long)nref);
 }
@@ -361,21 +369,23 @@ __device__ __forceinline__ uint32_t wscan_excl(uint32_t v, uint32_t &total) {
 // a message does not matter (its changes are distinct members).
 template <bool RECV>
 __device__ uint32_t wave_issue_t(const DS &d, uint32_t ol, uint32_t sender, uint32_t sinc, MsgDesc &out) {
+    // (the row's reads in one round trip, before the pool allocation's returning atomic)
     const uint32_t cnt = (uint32_t)d.dcnt[ol];
+    const int maxp = RECV ? d.maxp[ol] : 0;
+    const bool hotwalk = d.hidx && d.nhe[ol] == 0;
+    const uint32_t nslots = d.hidx ? d.hot_cnt[0] : 0u;
     out.kind = 0; out.len = 0; out.off_lo = out.off_hi = 0;
     if (cnt == 0) return 0;
     const unsigned long long off = pool_alloc(d, cnt);
     if (off == ~0ull) return 0;
-    const int maxp = RECV ? d.maxp[ol] : 0;
     const size_t rb = (size_t)ol * d.NP, hb = (size_t)ol * d.HP;
     uint32_t *bits = d.dbit + (size_t)ol * d.NBIT;
     uint32_t pos = 0;
     int del = 0, delnh = 0;
-    if (d.hidx && d.nhe[ol] == 0) {
+    if (hotwalk) {
         // every buffered member of this row has a hot slot: walk the row's slots in use (a few KB,
         // contiguous) instead of the presence bitmap (N/8 bytes) and the gathers it leads to. Records come out in
         // slot order; the order of a message does not matter (its changes are distinct members).
-        const uint32_t nslots = d.hot_cnt[0];
         for (uint32_t base = 0; base < nslots; base += 64 * MB) {
             uint2 ce[MB];
             uint32_t wv[MB], m[MB];

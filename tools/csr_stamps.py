@@ -19,7 +19,10 @@ c.bench_checksum(rows, 5, reps=1)
 c.enable_timing(True)
 ms = c.bench_checksum(rows, 5, reps=1)
 ku = c.kernel_units()
-st = [ku.get(f"diag_stamp{i}", 0) for i in range(4)]
+st = [ku.get(f"diag_stamp{i}", 0) for i in range(8)]
 tot = st[3] or 1
-print(json.dumps({"rows": rows, "ms": ms, "cycles": st, "share": {k: round(st[i] / tot, 3) for i, k in
-                                                                  enumerate(["chain", "prep", "barrier", "loop"])}}))
+# k_csr3: 0-3 the g/f chain waves (chain, waiting for the stagers, codes, whole loop), 4-7 the stagers (waiting for the
+# chains, window, rows' codes and exceptions, hand-over), each as a share of the chain waves' loop
+names = ["chain", "wait", "codes", "loop", "s_wait", "s_window", "s_prep", "s_signal"]
+print(json.dumps({"round": R, "rows": rows, "ms": ms, "cycles": st, "share": {k: round(st[i] / tot, 3) for i, k in
+                                                                              enumerate(names)}}))
