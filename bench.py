@@ -224,13 +224,15 @@ def live_member_rounds(wl, first, last):
     return total
 
 
-def cpu_baseline(gpu_window, members, seconds_budget=40.0):
+def cpu_baseline(gpu_window, members, seconds_budget=50.0):
     """The CPU oracle on a bounded sample of the same protocol at the GPU line's own N (tools/cpu_baseline.py does the
     timing in a child process so that OpenMP threads do not share this process with the HIP runtime): the reference
-    cost model and the optimized port, each on the box's cores, over the first rounds of the GPU window that fit the
-    budget (at 65,536 members a cascade round of the reference cost model takes tens of seconds)."""
+    cost model and the optimized port, each on the box's cores and on one thread, over the first rounds
+    of the GPU window that fit the budget (at 65,536 members a cascade round of the reference cost model takes tens of
+    seconds); the line's window_note says which rounds each covers."""
     out = subprocess.run([sys.executable, os.path.join(REPO, "tools", "cpu_baseline.py"), "--budget",
-                          str(seconds_budget), "--window", gpu_window, "--members", str(members), "--variants", "ref,opt"],
+                          str(seconds_budget), "--window", gpu_window, "--members", str(members), "--variants",
+                          "ref,opt,ref1,opt1"],
                          capture_output=True, text=True, timeout=1200)
     if out.returncode != 0:
         return {"error": out.stderr[-400:]}

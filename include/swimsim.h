@@ -78,9 +78,11 @@ typedef struct swimsim_tuning {
                                  kernel only; default 8,192 */
     int32_t cs_ref;           /* the reference-row checksum path: 0 off, 1 wide launches (default), 2
                                  every launch of at least 1,024 rows */
-    int32_t fault_inject;     /* tests only: 1 = the reference-row path's buffers fail to allocate (the production kernels
-                                 stay in charge, create and step succeed); 2 = the next reference-row launch fails with
-                                 SWIMSIM_EHIP (the step returns it; the handle stays usable); default 0 */
+    int32_t fault_inject;     /* tests only, bits: 1 = the reference-row path's buffers fail to allocate (the production
+                                 kernels stay in charge, create and step succeed); 2 = the next reference-row launch fails
+                                 with SWIMSIM_EHIP (the step returns it); 4 = 8 exception slots per stager wave (the
+                                 overflow slots and the fallback rows run); 8 = dedup keys narrowed to 3 bits (fingerprint
+                                 groups of unequal rows); default 0. Results are identical with 4 and 8. */
 } swimsim_tuning;
 
 /* Events applied in phase E of a round (docs/ROUND_SEMANTICS.md §4). */

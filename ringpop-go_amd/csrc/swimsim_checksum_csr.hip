@@ -16,27 +16,15 @@
 //   k_csr_rec     per row: one record per super step (CSR_SB blocks) that holds exception blocks: the super step's
 //                 32 codes (u16: a clean block's window entry as an LDS byte address, CSR_EXC | ordinal for an
 //                 exception block), the shift after it and where its first exceptions are
-//   k_csr         the chains. 256 rows per workgroup (4 waves, lane = row, one wave per SIMD at one workgroup per CU).
-//                 Per super step the waves stage the next super step's window (every phase in use, Wn positions)
-//                 from P and the rows' exception entries into the other LDS buffer while the chain of this one
-//                 runs. Each row reads its 32 blocks' entries at the byte addresses in its own LDS table, which its
-//                 lane rewrites only when the codes change: from a record (exception codes patched to the wave's
-//                 slots), and back to base(s) + i in the super step after one.
-// Rows the path cannot take (scan flags, an infeasible window, a super step with more exception entries than a
-// wave's slots) are listed and hashed by the production kernels (k_checksum3 / k_checksum_q16): bit-exact either way.
+//   k_csr3        the chains (below): 256 rows per workgroup, three waves per SIMD (the rows' g/f lanes, their h lanes,
+//                 and a stager that fills the next super step's window, codes and exception entries), handed over
+//                 through LDS counters
+// Rows the path cannot take (scan flags, an infeasible window, a super step with more exception entries than the
+// slots) are listed and hashed by the production kernels (k_checksum3 / k_checksum_q16): bit-exact either way.
 
-constexpr int CSR_ROWS = 256;          // rows per workgroup (4 waves)
+constexpr int CSR_ROWS = 256;          // rows per workgroup (4 row groups of 64)
 constexpr int CSR_SB = 32;             // blocks per super step
 constexpr int CSR_WINMAX = 1024;       // window entries per buffer: phases in use x Wn
-#ifndef CSR_EXW_DEF
-#define CSR_EXW_DEF 576
-#endif
-constexpr int CSR_EXW = CSR_EXW_DEF;   // exception entries per wave per buffer (128: a third of the rows of heavy cascade
-                                       // rounds fell back, a differing column giving every row of a wave exceptions;
-                                       // 192: still an eighth in the heaviest; 384: one row in the bench window. 576 once
-                                       // k_csr2 freed the code table's 36 KB of LDS)
-constexpr int CSR_ENT = CSR_WINMAX + 4 * CSR_EXW;   // entries per buffer
-constexpr int CSR_TW = 36;             // u32 words per row of the code table (32 codes + pad: ds_read_b128 conflict-free)
 constexpr uint32_t CSR_ESZ = 16;       // a code's unit: an entry's byte offset in each of the two entry arrays
 constexpr int CSR_EREG = 4;            // exception entries of a record prefetched with it
 #ifndef CSR_PF_DEF
@@ -78,6 +66,8 @@ struct CsrArgs {
     uint32_t *nrec;        // [rows]
     uint32_t rcap;
     uint32_t *fb_list, *fb_cnt;   // rows left to the production kernels
+    uint32_t exw;                 // k_csr3: exception slots a stager wave uses before the overflow slots (C3_EXW; tests
+                                  // lower it, swimsim_tuning.fault_inject bit 4)
 };
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -236,275 +226,6 @@ __global__ void __launch_bounds__(256) k_csr_rec(DS d, const uint32_t *list, uin
 }
 
 // ---------------------------------------------------------------------------------------------------------------
-// k_csr2: the chains with the h lane in a wave of its own (round 5). A block is 12 VALU instructions over three
-// lanes of one row, of which h is independent of the coupled g and f. With one lane per row, 65,536 rows fill the
-// chip's 1,024 SIMDs at one wave each, and a lone wave issues at best one instruction every ~5 cycles and waits
-// ~10 for a dependent one: k_csr ran its 12-instruction block at ~93 cycles from LDS. Here each 64-row group has
-// a g/f wave (8 instructions a block, a 5-deep dependent chain) and an h wave (4, 4 deep) on the same SIMD (waves w
-// and w + 4 of the workgroup), so the SIMD interleaves two chains at the same instruction count. Each role stages its
-// own half of the window (EA for g/f, EB for h), decodes the same records into its own codes (no code table in LDS:
-// a record's 32 u16 codes are unpacked in registers, exception codes patched to the wave's slots), and writes its
-// own half of the exception entries. The h wave hands its final state to the g/f wave through LDS at the end.
-// ---------------------------------------------------------------------------------------------------------------
-template <int W, int ROLE>                                           // ROLE 0: g/f lanes, 1: h lanes
-__device__ __forceinline__ void csr2_role(const DS &d, const uint32_t *list, const uint32_t cnt, const CsrArgs &a,
-                                          const CsrPlan &p, uint4 (*EA)[CSR_ENT], uint2 (*EB)[CSR_ENT], uint32_t *XH,
-                                          const uint32_t *phs) {
-    constexpr bool GF = ROLE == 0;
-    constexpr uint32_t CSH = GF ? 0u : 1u;                           // EA entries are 16 B, EB entries 8 B
-    const uint32_t tid = threadIdx.x & (CSR_ROWS - 1), rwave = tid >> 6;
-    const uint32_t g0 = blockIdx.x * CSR_ROWS;
-    const uint32_t gi = g0 + tid;
-    const bool valid = gi < cnt;
-    const uint32_t id = list[valid ? gi : g0];
-    const bool is_row = id < d.NL;
-    const uint32_t *row = csd_row(d, id);
-    const CsdRow ri = a.rinfo[valid ? gi : g0];
-    const uint32_t nrec = valid ? a.nrec[gi] : 0u;
-    const uint32_t len = csd_len(d, id);
-    const uint32_t iters = len > 24 ? (len - 1) / 20 : 0u;
-    uint32_t fl = !valid ? 0u : ri.flags ? ri.flags : !p.feasible || ri.ecnt > p.ecmax ? CSR_F_PLAN
-                : nrec == 0xFFFFFFFFu ? CSR_F_RCAP : 0u;
-    if (valid && !fl && iters == 0) fl = CSD_F_SHORT;
-    const bool live = valid && fl == 0;
-    const uint32_t myit = live ? iters : 0u;
-    const uint32_t T_ = p.feasible ? (p.maxit + CSR_SB - 1) / CSR_SB : 0u;
-    const CsrRec *rec = a.rec + (size_t)(valid ? gi : g0) * a.rcap;
-    const uint4 *ent = a.ent + (size_t)(valid ? gi : g0) * a.ecap * 2;
-    const uint32_t nr = live ? nrec : 0u;
-
-    FH fh{0, 0, 0};
-    uint32_t it2 = 0;
-    const bool ok = cs_prologue<W>(d, id, is_row, row, fh, it2);
-    uint32_t X0 = GF ? fh.g + ri.b0 : fh.h + ri.a0;                  // Xg, or Xh
-    uint32_t X1 = GF ? fh.f + ri.c0 : 0u;                            // Xf
-    int32_t s = 0;
-    uint32_t base = csr_base(p, 0);
-
-    // records, one ahead (as k_csr: whole vector registers, unconditional loads from clamped indices)
-    uint32_t rcur = 0, ecur = 0;
-    bool rv = false;
-    u32x4 R0, R1, R2, R3, R4;
-    typedef typename std::conditional<GF, u32x4, u32x2>::type EV;   // this role's half of an exception entry
-    EV RE0, RE1, RE2, RE3;
-    auto ent_half = [&](uint32_t e) -> EV {
-        if constexpr (GF) return *(const u32x4 *)(ent + 2 * e);
-        else return *(const u32x2 *)(ent + 2 * e + 1);
-    };
-    auto load_rec = [&](uint32_t q, uint32_t e0) {
-        const u32x4 *rp = (const u32x4 *)(rec + min(q, a.rcap - 1u));
-        R0 = rp[0]; R1 = rp[1]; R2 = rp[2]; R3 = rp[3]; R4 = rp[4];
-        const uint32_t eb = min(e0, a.ecap - (uint32_t)CSR_EREG);
-        RE0 = ent_half(eb); RE1 = ent_half(eb + 1); RE2 = ent_half(eb + 2); RE3 = ent_half(eb + 3);
-        rv = q < nr;
-    };
-    load_rec(0, 0);
-
-    // window staging: entries u = tid + 256 v, this role's half, two register sets (super step u -> set u & 1)
-    constexpr int WV = CSR_WINMAX / CSR_ROWS;
-    EV wA[WV], wB[WV];
-    const uint32_t nwin = p.nph * p.Wn;
-    const uint4 *wsrc[WV];
-    int32_t wk0[WV];
-#pragma unroll
-    for (int v = 0; v < WV; v++) {
-        const uint32_t u = tid + (uint32_t)CSR_ROWS * v;
-        const uint32_t ps = u < nwin ? u / p.Wn : 0u, w = u < nwin ? u - ps * p.Wn : 0u;
-        wsrc[v] = a.P + 2 * (size_t)phs[min(ps, 19u)] * a.KP + (GF ? 0 : 1);
-        wk0[v] = u < nwin ? (int32_t)w - p.cmax : 0x40000000;
-    }
-    auto wload = [&](EV (&wst)[WV], uint32_t t) {
-#pragma unroll
-        for (int v = 0; v < WV; v++) {
-            const int32_t k = min(max(wk0[v] + (int32_t)(t * CSR_SB), 0), (int32_t)a.KP - 1);
-            wst[v] = *(const EV *)(wsrc[v] + 2 * (uint32_t)k);
-        }
-    };
-    auto put = [&](uint32_t b, uint32_t e, const EV &x) {
-        if constexpr (GF) *(u32x4 *)&EA[b][e] = x;
-        else *(u32x2 *)&EB[b][e] = x;
-    };
-    auto wstore = [&](const EV (&wst)[WV], uint32_t b) {
-#pragma unroll
-        for (int v = 0; v < WV; v++) put(b, tid + (uint32_t)CSR_ROWS * v, wst[v]);
-    };
-
-    uint32_t code[CSR_SB];
-    auto set_base = [&]() {
-        const uint32_t ba = (base * CSR_ESZ) >> CSH;
-#pragma unroll
-        for (int i = 0; i < CSR_SB; i++) code[i] = ba + (((uint32_t)i * CSR_ESZ) >> CSH);
-    };
-    if (live) set_base();
-    else {
-#pragma unroll
-        for (int i = 0; i < CSR_SB; i++) code[i] = 0u;
-    }
-    bool was = false;
-    auto prep = [&](uint32_t t, uint32_t b) {
-        const bool has = live && rv && R0.x == t;
-        if (__ballot(has)) {
-            uint32_t ne = has ? R0.w : 0u, tot = 0;
-            const uint32_t sb = wscan_excl(ne, tot);              // this row's first slot in the wave's area
-            const uint32_t xb = (uint32_t)CSR_WINMAX + rwave * CSR_EXW + sb;
-            if (has && sb + ne > (uint32_t)CSR_EXW) fl |= CSR_F_SLOTS;
-            if (has) {
-                const uint32_t xa = xb * CSR_ESZ;
-                auto dec = [&](uint32_t c) -> uint32_t {          // a record code -> this role's LDS offset
-                    return ((c & CSR_EXC) ? xa + (c & 0x7FFFu) * CSR_ESZ : c) >> CSH;
-                };
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    const u32x4 Rq = q == 0 ? R1 : q == 1 ? R2 : q == 2 ? R3 : R4;
-                    code[8 * q + 0] = dec(Rq.x & 0xFFFFu); code[8 * q + 1] = dec(Rq.x >> 16);
-                    code[8 * q + 2] = dec(Rq.y & 0xFFFFu); code[8 * q + 3] = dec(Rq.y >> 16);
-                    code[8 * q + 4] = dec(Rq.z & 0xFFFFu); code[8 * q + 5] = dec(Rq.z >> 16);
-                    code[8 * q + 6] = dec(Rq.w & 0xFFFFu); code[8 * q + 7] = dec(Rq.w >> 16);
-                }
-                if (!(fl & CSR_F_SLOTS)) {
-                    if (ne > 0) put(b, xb + 0, RE0);
-                    if (ne > 1) put(b, xb + 1, RE1);
-                    if (ne > 2) put(b, xb + 2, RE2);
-                    if (ne > 3) put(b, xb + 3, RE3);
-                    for (uint32_t k = CSR_EREG; k < ne; k++) put(b, xb + k, ent_half(ecur + k));   // (rare)
-                }
-                s = (int32_t)R0.y;
-            }
-        }
-        if (was && !has) set_base();
-        was = has;
-    };
-
-#ifdef CSR_DIAG_STAMP
-    // (diagnostic build only: shader-clock stamps of the g/f waves, summed into the diagnostic counters: 0 chain,
-    // 1 staging + preparation, 2 barrier, 3 whole loop)
-    uint64_t st_[4] = {0, 0, 0, 0};
-    auto stamp = [&]() -> uint64_t {
-        uint64_t tt;
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tt) :: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        return tt;
-    };
-#define CSR2_STAMP(v) const uint64_t v = stamp()
-#define CSR2_ACC(k, x) st_[k] += (x)
-#else
-#define CSR2_STAMP(v)
-#define CSR2_ACC(k, x)
-#endif
-    // super step 0
-    wload(wA, 0);
-    wstore(wA, 0);
-    wload(wB, 1);
-    prep(0, 0);
-    if (live && rv && R0.x == 0) { base = csr_base(p, s); rcur++; ecur += R0.w; load_rec(rcur, ecur); }
-    lds_barrier();
-    CSR2_STAMP(tl0);
-    auto iter = [&](uint32_t t, auto BC) {
-        constexpr uint32_t b = decltype(BC)::value;
-        const uint32_t K0 = t * CSR_SB;
-        if constexpr (b) wload(wB, t + 2);
-        else wload(wA, t + 2);
-        CSR2_STAMP(ts0);
-        const bool full = __all(myit == 0u || K0 + CSR_SB <= myit);
-        const char *Eb = GF ? (const char *)EA[b] : (const char *)EB[b];
-        auto run = [&](auto FULLC) {
-            constexpr bool FULL = decltype(FULLC)::value;
-            EV va[CSR_PF + 1];
-            auto fetch = [&](int i) { va[i % (CSR_PF + 1)] = *(const EV *)(Eb + code[i]); };
-#pragma unroll
-            for (int i = 0; i < CSR_PF; i++) fetch(i);
-#pragma unroll
-            for (int i = 0; i < CSR_SB; i++) {
-                if (i + CSR_PF < CSR_SB) fetch(i + CSR_PF);
-                const EV A = va[i % (CSR_PF + 1)];
-                uint32_t n0 = X0, n1 = X1;
-                if constexpr (GF) csd_gf_step(n0, n1, A.x, A.y, A.z, A.w);
-                else csd_h_step(n0, A.x, A.y);
-                if (FULL) {
-                    X0 = n0; X1 = n1;
-                } else {
-                    const bool act = K0 + (uint32_t)i < myit;
-                    X0 = act ? n0 : X0;
-                    X1 = act ? n1 : X1;
-                }
-            }
-        };
-        if (full) run(std::integral_constant<bool, true>{});
-        else run(std::integral_constant<bool, false>{});
-        asm volatile("" ::: "memory");
-        CSR2_STAMP(ts1);
-        CSR2_ACC(0, ts1 - ts0);
-        if constexpr (b) wstore(wA, 0u);                           // super step t + 1 (even) -> buffer 0
-        else wstore(wB, 1u);
-        prep(t + 1, b ^ 1u);
-        const bool adv = live && rv && R0.x == t + 1;
-        if (adv) { base = csr_base(p, s); rcur++; ecur += R0.w; }
-        if (__ballot(adv)) load_rec(rcur, ecur);
-        CSR2_STAMP(ts2);
-        lds_barrier();
-        CSR2_STAMP(ts3);
-        CSR2_ACC(1, ts2 - ts1);
-        CSR2_ACC(2, ts3 - ts2);
-    };
-    uint32_t t = 0;
-    for (; t + 1 < T_; t += 2) {
-        iter(t, std::integral_constant<uint32_t, 0>{});
-        iter(t + 1, std::integral_constant<uint32_t, 1>{});
-    }
-    if (t < T_) iter(t, std::integral_constant<uint32_t, 0>{});
-    CSR2_STAMP(tl1);
-    CSR2_ACC(3, tl1 - tl0);
-#ifdef CSR_DIAG_STAMP
-    if (GF && (threadIdx.x & 63u) == 0)
-        for (int k = 0; k < 4; k++) ctr_add(d, C_NALL + k, (unsigned long long)st_[k]);
-#endif
-#undef CSR2_STAMP
-#undef CSR2_ACC
-
-    if constexpr (!GF) XH[tid] = X0;
-    lds_barrier();
-    if constexpr (GF) {
-        const bool mine = valid && fl == 0;
-        const uint32_t nmine = (uint32_t)__popcll(__ballot(mine));
-        if ((threadIdx.x & 63u) == 0 && nmine) ctr_add(d, C_X_CS_ROWS, (unsigned long long)nmine);
-        if (!valid) return;
-        if (!mine) {                                                // left to the production kernels
-            const uint32_t at = atomicAdd(a.fb_cnt, 1u);
-            a.fb_list[at] = id;
-            const uint32_t r = (fl & CSD_F_SHORT) ? 0u : (fl & CSD_F_ECAP) ? 1u : (fl & CSR_F_PLAN) ? 2u : (fl & CSR_F_RCAP) ? 3u
-                             : 4u;
-            atomicAdd(a.fb_cnt + 1 + r, 1u);
-            return;
-        }
-        fh.h = XH[tid]; fh.g = X0; fh.f = X1;
-        const uint32_t hv = ok ? fh.fin() : 0u;
-        if (is_row) {
-            d.cs[id] = hv;
-            d.dirty[id] = 0;
-        } else {
-            d.dense_cs[id - d.NL] = hv;
-        }
-    }
-}
-
-template <int W>
-__global__ void __launch_bounds__(2 * CSR_ROWS) k_csr2(DS d, const uint32_t *list, const uint32_t *count, CsrArgs a) {
-    __shared__ uint4 EA[2][CSR_ENT];
-    __shared__ uint2 EB[2][CSR_ENT];
-    __shared__ uint32_t XH[CSR_ROWS];
-    __shared__ uint32_t phs[20];
-    const uint32_t cnt = *count;
-    if (blockIdx.x * CSR_ROWS >= cnt) return;
-    const CsrPlan p = a.plan[blockIdx.x];
-    if (threadIdx.x < 20 && ((p.phm >> threadIdx.x) & 1u)) phs[__popc(p.phm & ((1u << threadIdx.x) - 1u))] = threadIdx.x;
-    __syncthreads();
-    // waves 0-3: g/f lanes of rows 64 w .. 64 w + 63; waves 4-7: their h lanes (wave w + 4 shares wave w's SIMD)
-    if (threadIdx.x < CSR_ROWS) csr2_role<W, 0>(d, list, cnt, a, p, EA, EB, XH, phs);
-    else csr2_role<W, 1>(d, list, cnt, a, p, EA, EB, XH, phs);
-}
-
-// ---------------------------------------------------------------------------------------------------------------
 // k_csr3: chain waves that only run chains (round 5). k_csr2's waves spent 39 % (light rounds) to 55 % (heavy) of
 // their loop outside the chain: staging the next super step's window, unpacking records, writing exception entries,
 // and waiting at the per-super-step barrier for the slowest of the eight (shader-clock stamps, tools/csr_stamps.py).
@@ -526,6 +247,7 @@ struct Csr3Lds {
     uint32_t XH[CSR_ROWS];                 // h lanes' final state
     uint32_t FLX[CSR_ROWS];                // rows the stagers flagged (exception slots)
     uint32_t ready[2], done[2];
+    uint32_t ovf[2];                       // buffer b's overflow slots in the window's unused tail: (super step << 16) | used
     uint32_t phs[20];
 };
 
@@ -611,8 +333,10 @@ __device__ __forceinline__ void c3_stage(const DS &d, const uint32_t *list, uint
 #pragma unroll
         for (int v = 0; v < WV; v++) {
             const uint32_t u = tid + (uint32_t)CSR_ROWS * v;
-            *(u32x4 *)&L.EA[b][u] = w0[v];
-            *(u32x2 *)&L.EB[b][u] = w1[v];
+            if (u < nwin) {                                        // (the tail holds overflow exception entries)
+                *(u32x4 *)&L.EA[b][u] = w0[v];
+                *(u32x2 *)&L.EB[b][u] = w1[v];
+            }
         }
     };
     int32_t s = 0;
@@ -624,8 +348,37 @@ __device__ __forceinline__ void c3_stage(const DS &d, const uint32_t *list, uint
         if (__ballot(has)) {
             uint32_t ne = has ? R0.w : 0u, tot = 0;
             const uint32_t sb = wscan_excl(ne, tot);
-            const uint32_t xb = (uint32_t)CSR_WINMAX + rwave * C3_EXW + sb;
-            if (has && sb + ne > (uint32_t)C3_EXW) r.fl |= CSR_F_SLOTS;
+            uint32_t xb = (uint32_t)CSR_WINMAX + rwave * C3_EXW + sb;
+            if (tot > a.exw) {
+                // more exceptions than the wave's area: the rows past it take slots in the window's unused tail
+                // [nwin, CSR_WINMAX) of this buffer (shared by the stagers of this super step, tagged with it), else they
+                // are left to the production kernels
+                const bool over = has && sb + ne > a.exw;
+                uint32_t f = over ? sb : 0xFFFFFFFFu;              // the first row past the area
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) f = min(f, (uint32_t)__shfl_xor((int)f, o, 64));
+                const uint32_t need = tot - f;
+                uint32_t got = 0xFFFFFFFFu;
+                if ((threadIdx.x & 63u) == 0) {
+                    const uint32_t room = (uint32_t)CSR_WINMAX - nwin;
+                    uint32_t old = __hip_atomic_load(&L.ovf[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    while (true) {
+                        const uint32_t used = (old >> 16) == (t & 0xFFFFu) ? (old & 0xFFFFu) : 0u;
+                        if (used + need > room) break;
+                        const uint32_t nw = ((t & 0xFFFFu) << 16) | (used + need);
+                        if (__hip_atomic_compare_exchange_strong(&L.ovf[b], &old, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                                 __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                            got = nwin + used;
+                            break;
+                        }
+                    }
+                }
+                got = (uint32_t)__shfl((int)got, 0, 64);
+                if (over) {
+                    if (got != 0xFFFFFFFFu) xb = got + (sb - f);
+                    else r.fl |= CSR_F_SLOTS;
+                }
+            }
             if (has) {
                 L.TC[b][0][tid] = make_uint4(R1.x, R1.y, R1.z, R1.w);
                 L.TC[b][1][tid] = make_uint4(R2.x, R2.y, R2.z, R2.w);
@@ -872,7 +625,7 @@ __global__ void __launch_bounds__(3 * CSR_ROWS) k_csr3(DS d, const uint32_t *lis
     if (blockIdx.x * CSR_ROWS >= cnt) return;
     const CsrPlan p = a.plan[blockIdx.x];
     if (threadIdx.x < 20 && ((p.phm >> threadIdx.x) & 1u)) L.phs[__popc(p.phm & ((1u << threadIdx.x) - 1u))] = threadIdx.x;
-    if (threadIdx.x < 2) { L.ready[threadIdx.x] = 0; L.done[threadIdx.x] = 0; }
+    if (threadIdx.x < 2) { L.ready[threadIdx.x] = 0; L.done[threadIdx.x] = 0; L.ovf[threadIdx.x] = 0xFFFF0000u; }
     __syncthreads();
     const uint32_t T_ = p.feasible ? (p.maxit + CSR_SB - 1) / CSR_SB : 0u;
     const uint32_t role = threadIdx.x / CSR_ROWS;
@@ -900,8 +653,6 @@ void launch_csr_w(const DS &d, const uint32_t *list, uint32_t n, const uint32_t 
         hipLaunchKernelGGL(k_csr_rec, dim3((n + 3) / 4), dim3(256), 0, s, d, list, n, a);
     } else if (part == 4) {
         hipLaunchKernelGGL((k_csr3<W>), dim3((n + CSR_ROWS - 1) / CSR_ROWS), dim3(3 * CSR_ROWS), 0, s, d, list, count, a);
-    } else {                                                        // (k_csr2, for comparison)
-        hipLaunchKernelGGL((k_csr2<W>), dim3((n + CSR_ROWS - 1) / CSR_ROWS), dim3(2 * CSR_ROWS), 0, s, d, list, count, a);
     }
 }
 

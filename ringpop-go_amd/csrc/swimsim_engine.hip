@@ -357,6 +357,7 @@ struct swimsim {
     unsigned long long *csr_acc = nullptr;        // [8] fallback rows so far, then per reason (read by path stats)
     uint64_t csr_launches = 0;
     int fault_inject = 0;                         // swimsim_tuning.fault_inject (tests)
+    bool colx_stale = false;                      // raw row writes marked every column: rebuilt at the next step
 #ifdef SWIMSIM_DIAG
     // reference-row checksum path (swimsim_checksum_delta.hip), allocated at its first launch
     int csd_mode = 0;                             // SWIMSIM_CS_DELTA: 0 off, 1 wide launches, 2 every launch >= 1024 rows
@@ -629,13 +630,17 @@ int xchg(swimsim *h) {
     // the host waits once per exchange, for its own sizes and the peers' together; the others exchange host arrays
     // after the pack (two host synchronisations).
     const bool dev_sizes = h->xp->stream_ordered();
-    std::vector<uint64_t> sz(2 * G), sendsz(2 * G), recvsz(2 * G);
+    std::vector<uint64_t> sz(2 * G), sendsz(2 * G), recvsz(2 * G), devsend(2 * G);
     uint32_t nitems = 0;
+    hipLaunchKernelGGL(k_x_sendsz, dim3(1), dim3(64), 0, h->s, h->xsz, G, h->xsz + 2 * G);
     if (dev_sizes) {
-        hipLaunchKernelGGL(k_x_sendsz, dim3(1), dim3(64), 0, h->s, h->xsz, G, h->xsz + 2 * G);
         if (int rc = h->xp->sizes_dev((const uint64_t *)(h->xsz + 2 * G), (uint64_t *)(h->xsz + 4 * G), 2, h->s))
             return h->fail(rc, "shard size exchange failed (%s)", h->xp->name());
         HIPCHK(h, hipMemcpyAsync(recvsz.data(), h->xsz + 4 * G, 2 * G * 8, hipMemcpyDeviceToHost, h->s));
+    } else {
+        // (the host transports exchange the host's sizes; the device's, which the RCCL transport sends, are checked
+        // against them on every exchange, so the formula k_x_sendsz repeats is covered without RCCL)
+        HIPCHK(h, hipMemcpyAsync(devsend.data(), h->xsz + 2 * G, 2 * G * 8, hipMemcpyDeviceToHost, h->s));
     }
     HIPCHK(h, hipMemcpyAsync(sz.data(), h->xsz, 2 * G * 8, hipMemcpyDeviceToHost, h->s));
     HIPCHK(h, hipMemcpyAsync(&nitems, h->xcnt, 4, hipMemcpyDeviceToHost, h->s));
@@ -656,6 +661,8 @@ int xchg(swimsim *h) {
         sendsz[2 * p] = sbytes[p];   // (k_x_sendsz computes the same on the device)
         sendsz[2 * p + 1] = sz[2 * p + 1];
     }
+    if (!dev_sizes && devsend != sendsz)
+        return h->fail(SWIMSIM_EHIP, "exchange: device send sizes (k_x_sendsz) differ from the host's");
     if (total > h->sbuf_cap) {
         if (h->sbuf) hipFree(h->sbuf);
         h->sbuf_cap = std::max<uint64_t>(total + total / 2, 1 << 20);
@@ -916,6 +923,7 @@ int csr_hash(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t n, 
     a.rcap = h->csr_rcap;
     a.fb_list = h->csr_fb;
     a.fb_cnt = h->csr_fbcnt;
+    a.exw = (h->fault_inject & 4) ? 8u : (uint32_t)C3_EXW;
     {
         Scope sc(h, F_CSD_SCAN);
         hipLaunchKernelGGL(k_csd_ref, dim3((h->N + 256) / 256), dim3(256), 0, h->s, h->d, list, n, h->csr_B, h->csr_Lb);
@@ -1064,7 +1072,8 @@ int checksum_dirty(swimsim *h, int mode, bool async = false) {
         size_t bytes = h->cub_bytes;
         HIPCHK(h, hipcub::DeviceRadixSort::SortKeys(h->cub_tmp, bytes, h->list, h->fplist, (int)n, 0,
                                                     32 - __builtin_clz(h->NL), h->s));
-        hipLaunchKernelGGL(k_fp_keys, dim3(blocks_for_threads(n)), dim3(256), 0, h->s, h->d, h->fplist, n, h->keys, h->fpv);
+        hipLaunchKernelGGL(k_fp_keys, dim3(blocks_for_threads(n)), dim3(256), 0, h->s, h->d, h->fplist, n, h->keys, h->fpv,
+                           (h->fault_inject & 8) ? 7ull : ~0ull);
         bytes = h->cub_bytes;
         HIPCHK(h, hipcub::DeviceRadixSort::SortPairs(h->cub_tmp, bytes, h->keys, h->keys_sorted, h->fpv, h->fpv_s, (int)n, 0,
                                                      64, h->s));
@@ -1882,6 +1891,7 @@ static int init_rows(swimsim_t *h, int mode) {
     hipLaunchKernelGGL(k_init_rows, dim3(blocks_for_waves(h->NL)), dim3(SWIM_WAVE_BLOCK), 0, h->s, h->d, mode, 0u);
     // converged rows are all equal: no column differs; self-only rows differ everywhere
     HIPCHK(h, hipMemsetAsync(h->d.colx, mode == 0 ? 0 : 0xFF, (size_t)h->d.NBIT * 4, h->s));
+    h->colx_stale = mode != 0;
     if (int rc = checksum_dirty(h, 0)) return rc;
     return check_err(h);
 }
@@ -1900,6 +1910,7 @@ int swimsim_set_member(swimsim_t *h, uint32_t o, uint32_t m, int32_t status, int
     }
     const uint32_t w = (e << 3) | (uint32_t)status;
     HIPCHK(h, hipMemsetAsync(h->d.colx, 0xFF, (size_t)h->d.NBIT * 4, h->s));   // raw write: every column may differ
+    h->colx_stale = true;
     hot_reset(h, true);
     HIPCHK(h, hipMemcpyAsync(h->d.mw + (size_t)(o - h->lo) * h->NP + m, &w, 4, hipMemcpyHostToDevice, h->s));
     hipLaunchKernelGGL(k_recount, dim3(1), dim3(64), 0, h->s, h->d, o - h->lo);
@@ -1922,6 +1933,7 @@ int swimsim_set_row(swimsim_t *h, uint32_t o, const uint8_t *status, const int64
     }
     if (int rc = ensure_ecap(h, emax)) return rc;                  // the checksum tables cover every incarnation
     HIPCHK(h, hipMemsetAsync(h->d.colx, 0xFF, (size_t)h->d.NBIT * 4, h->s));   // raw write: every column may differ
+    h->colx_stale = true;
     hot_reset(h, true);
     HIPCHK(h, hipMemcpyAsync(h->d.mw + (size_t)(o - h->lo) * h->NP, row.data(), (size_t)h->N * 4,
                              hipMemcpyHostToDevice, h->s));
@@ -2008,6 +2020,10 @@ int swimsim_set_round(swimsim_t *h, uint32_t r) {
 int swimsim_step(swimsim_t *h, uint32_t nrounds, const swimsim_event *events, size_t nevents) {
     if (!h) return SWIMSIM_EINVAL;
     if (h->G == 1 && h->NL != h->N) return h->fail(SWIMSIM_EINVAL, "a partial observer range needs a shard transport");
+    if (h->colx_stale && nrounds) {                                // (no snapshot is alive between step calls)
+        hipLaunchKernelGGL(k_colx_rebuild, dim3(blocks_for_threads(h->NP)), dim3(256), 0, h->s, h->d);
+        h->colx_stale = false;
+    }
     for (uint32_t i = 0; i < nrounds; i++) {
         if (int rc = ensure_ecap(h, h->round + 1)) return rc;
         if (int rc = step_one(h, events, nevents)) return rc;
@@ -2230,7 +2246,7 @@ __global__ void k_iota(uint32_t *list, uint32_t *cnt, uint32_t n) {
 int swimsim_bench_checksum(swimsim_t *h, uint32_t nrows, int32_t mode, int32_t reps, double *ms) {
     if (!h || !ms || nrows == 0 || nrows > h->NL || reps < 1) return SWIMSIM_EINVAL;
 #ifndef SWIMSIM_DIAG
-    if (mode < 0 || mode > 6 || mode == 3)
+    if (mode < 0 || mode > 5 || mode == 3)
         return h->fail(SWIMSIM_EINVAL, "checksum mode %d: diagnostics build only", mode);
     const bool csd = false;
 #else
@@ -2240,7 +2256,7 @@ int swimsim_bench_checksum(swimsim_t *h, uint32_t nrows, int32_t mode, int32_t r
     const bool csd = mode == 3 || (mode >= 31 && mode <= 46);
     if (csd && (csd_alloc(h) || nrows > h->NL)) return h->fail(SWIMSIM_EINVAL, "reference-row path unavailable");
 #endif
-    if ((mode == 5 || mode == 6) && csr_alloc(h)) return h->fail(SWIMSIM_EINVAL, "reference-row path unavailable");
+    if (mode == 5 && csr_alloc(h)) return h->fail(SWIMSIM_EINVAL, "reference-row path unavailable");
     int rc5 = 0;
     auto launch = [&]() {
         if (csd) {                                                 // the path itself, never declined here
@@ -2254,7 +2270,6 @@ int swimsim_bench_checksum(swimsim_t *h, uint32_t nrows, int32_t mode, int32_t r
         else if (mode <= 2) launch_checksum_kind(h->d, h->list, h->cnt, nrows, mode == 0 ? cs_kind(nrows, h->cs_narrow_rows) : (CsKind)mode, h->s);
         else if (mode == 4) launch_checksum_wide4(h->d, h->list, h->cnt, nrows, h->s);
         else if (mode == 5) rc5 = csr_hash(h, h->list, h->cnt, nrows);   // the reference-row path, forced
-        else if (mode == 6) rc5 = csr_hash(h, h->list, h->cnt, nrows, 5);   // the same with round 4's chain kernel
 #ifdef SWIMSIM_DIAG
         else launch_checksum_mode(h->d, h->list, h->cnt, nrows, mode, h->s);
 #endif

@@ -1179,6 +1179,24 @@ __global__ void __launch_bounds__(256, RECV_MIN_WAVES) k_recv(DS d, RecvArgs a) 
     }
 }
 
+// DS::colx from the rows themselves (one lane per column, a wave's 64 columns in two bitmap words): after raw row
+// writes every column was marked, and the divergent-column scans fell back to whole rows for the rest of the handle's
+// life. Run at the next step's start, when no snapshot is alive (every step call ends with the side stream drained).
+__global__ void k_colx_rebuild(DS d) {
+    const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+    bool diff = false;
+    if (m < d.N) {
+        const uint32_t w0 = d.mw[m];
+        for (uint32_t ol = 1; ol < d.NL && !diff; ol++) diff = d.mw[(size_t)ol * d.NP + m] != w0;
+    }
+    const unsigned long long bits = __ballot(diff);
+    const uint32_t w = (m & ~63u) >> 5;
+    if (lane_id() == 0) {
+        if (w < d.NBIT) d.colx[w] = (uint32_t)bits;
+        if (w + 1 < d.NBIT) d.colx[w + 1] = (uint32_t)(bits >> 32);
+    }
+}
+
 // the divergent-column lists (DS::ucl / uhk / ucold / ucnt) from the bitmap (one workgroup of 1024 threads: each thread
 // a run of bitmap words, a block prefix sum of their bit counts)
 __global__ void __launch_bounds__(1024) k_ucols(DS d) {
@@ -1449,10 +1467,11 @@ __global__ void k_jobs_reset(DS d, uint8_t *need) {
 // only group heads and rows that differ from their head are hashed; the others copy the head's
 // checksum. Exact: the fingerprint only proposes the pairs that the comparison checks.
 // ---------------------------------------------------------------------------------------------
-__global__ void k_fp_keys(DS d, const uint32_t *list, uint32_t n, unsigned long long *keys, uint32_t *vals) {
+__global__ void k_fp_keys(DS d, const uint32_t *list, uint32_t n, unsigned long long *keys, uint32_t *vals,
+                          unsigned long long keymask) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    keys[i] = d.fp[list[i]];
+    keys[i] = d.fp[list[i]] & keymask;                             // (tests narrow the keys: collision groups)
     vals[i] = list[i];
 }
 

@@ -115,3 +115,35 @@ def test_csr_hash_hip_error_reaches_swimsim_step():
             eng.step(1, wl.events_for(r))
     eng.close()
     run_vs_oracle(wl, 30)
+
+
+def test_exception_overflow_slots_every_round():
+    """swimsim_tuning.fault_inject = 4: 8 exception slots per stager wave, so waves spill into the window's unused tail
+    (k_csr3's overflow slots) and, when that is full too, rows go to the production kernels. Bit-exact either way."""
+    wl = W.config3(n=2048, rounds=40, kill_round=5)
+    eng = swimsim.Cluster(wl.n, tuning={"cs_ref": 2, "cs_async": 0, "fault_inject": 4})
+    ora = OracleSim(wl.n)
+    for r in range(40):
+        ev = wl.events_for(r)
+        eng.step(1, ev)
+        ora.step(ev)
+        bad = np.nonzero(eng.checksums() != ora.checksums())[0]
+        assert len(bad) == 0, f"round {r}: {len(bad)} checksums differ, first rows {bad[:5]}"
+    st = eng.checksum_path_stats()
+    print("overflow slots", st)
+    assert st["delta_launches"] >= 4, st
+
+
+def test_dedup_fingerprint_collision_groups():
+    """swimsim_tuning.fault_inject = 8: dedup keys narrowed to 3 bits, so every fingerprint group holds unequal rows.
+    k_fp_verify must hash every row that differs from its group head (memberlist.go:106-128: equal strings, equal
+    checksums; only equality, never the fingerprint, decides a copy)."""
+    for wl, rounds in ((W.config3(n=1024, rounds=30, kill_round=5), 30), (W.config2(n=1024, rounds=12), 12)):
+        eng = swimsim.Cluster(wl.n, tuning={"fault_inject": 8})
+        ora = OracleSim(wl.n)
+        for r in range(rounds):
+            ev = wl.events_for(r)
+            eng.step(1, ev)
+            ora.step(ev)
+            bad = np.nonzero(eng.checksums() != ora.checksums())[0]
+            assert len(bad) == 0, f"{wl.name} round {r}: {len(bad)} checksums differ"

@@ -148,6 +148,11 @@ def main():
         "optimized_port": {**opt, "note": "static-order string, checksum once per round per dirty row"},
         "reference_cost_1thread": ref1,
         "optimized_port_1thread": opt1,
+        "window_note": f"the GPU line times rounds {warmup}-{warmup + steps - 1}; each CPU run times the first rounds of "
+                       f"that window that fit its share of the {b:.0f}-s budget (reference cost model, {nthr} threads: "
+                       f"rounds {rr[0]}-{rr[1]}). The rounds left out are the cascade's heaviest (every dirty row's string "
+                       f"rebuilt and hashed at each applying Update), so each CPU value is its rate over the lighter "
+                       f"rounds: it overstates the CPU over the whole window",
     }))
 
 
