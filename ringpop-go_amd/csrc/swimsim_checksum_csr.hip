@@ -354,9 +354,7 @@ __device__ __forceinline__ void c3_stage(const DS &d, const uint32_t *list, uint
                 // [nwin, CSR_WINMAX) of this buffer (shared by the stagers of this super step, tagged with it), else they
                 // are left to the production kernels
                 const bool over = has && sb + ne > a.exw;
-                uint32_t f = over ? sb : 0xFFFFFFFFu;              // the first row past the area
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) f = min(f, (uint32_t)__shfl_xor((int)f, o, 64));
+                const uint32_t f = wmin(over ? sb : 0xFFFFFFFFu);  // the first row past the area
                 const uint32_t need = tot - f;
                 uint32_t got = 0xFFFFFFFFu;
                 if ((threadIdx.x & 63u) == 0) {
@@ -373,7 +371,7 @@ __device__ __forceinline__ void c3_stage(const DS &d, const uint32_t *list, uint
                         }
                     }
                 }
-                got = (uint32_t)__shfl((int)got, 0, 64);
+                got = (uint32_t)__builtin_amdgcn_readlane((int)got, 0);
                 if (over) {
                     if (got != 0xFFFFFFFFu) xb = got + (sb - f);
                     else r.fl |= CSR_F_SLOTS;

@@ -273,12 +273,7 @@ __global__ void __launch_bounds__(256) k_csd_scan(DS d, const uint32_t *list, ui
         nruns++;
     };
     auto wred = [&](int32_t v, int op) -> int32_t {                 // wave min (0), max (1) or or (2)
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) {
-            const int32_t y = __shfl_xor(v, off, 64);
-            v = op == 0 ? min(v, y) : op == 1 ? max(v, y) : (v | y);
-        }
-        return v;
+        return (int32_t)lane63(op == 0 ? (uint32_t)dpp_scan_imin(v) : op == 1 ? (uint32_t)dpp_scan_imax(v) : dpp_scan_or((uint32_t)v));
     };
     // one chunk: m = its differing lanes; this lane's member mm, row word wm, B word bm, O_B[mm], O_B[mm - 1]
     auto chunk = [&](uint64_t m, uint32_t mm, uint32_t wm, uint32_t bm, uint32_t obm, uint32_t ob1) {
@@ -293,13 +288,8 @@ __global__ void __launch_bounds__(256) k_csd_scan(DS d, const uint32_t *list, ui
         if (khi > (int32_t)kl) khi = (int32_t)kl;
         const bool vd = dl && klo <= (int32_t)kl && khi >= klo;
         // the last block of every run before this member: the open run's, or the previous valid member's (a prefix max)
-        int32_t px = vd ? khi : (-0x7FFFFFFF - 1);
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const int32_t yv = __shfl_up(px, off, 64);
-            if (lane >= (uint32_t)off) px = max(px, yv);
-        }
-        const int32_t pxe = __shfl_up(px, 1, 64);                   // (exclusive: the lanes below this one)
+        const int32_t px = dpp_scan_imax(vd ? khi : (-0x7FFFFFFF - 1));
+        const int32_t pxe = (int32_t)dpp_shr1((uint32_t)px, 0x80000000u);   // (exclusive: the lanes below this one)
         const int32_t pk = lane ? max(pxe, (int32_t)rhi) : (int32_t)rhi;
         const bool st = vd && klo > pk + 1;                         // this member begins a new run
         const uint64_t sm = __ballot(st);
@@ -341,9 +331,9 @@ __global__ void __launch_bounds__(256) k_csd_scan(DS d, const uint32_t *list, ui
         nruns += K;
         // the last start's run stays open
         const uint32_t ll = 63u - (uint32_t)__builtin_clzll(sm);
-        rlo = (uint32_t)__shfl(klo, (int)ll, 64);
-        rm0 = (uint32_t)__shfl((int)m0, (int)ll, 64);
-        ro0 = (uint32_t)__shfl((int)o0, (int)ll, 64);
+        rlo = (uint32_t)__builtin_amdgcn_readlane(klo, (int)ll);   // (ll is wave-uniform)
+        rm0 = (uint32_t)__builtin_amdgcn_readlane((int)m0, (int)ll);
+        ro0 = (uint32_t)__builtin_amdgcn_readlane((int)o0, (int)ll);
         rhi = (uint32_t)wred(vd && lane >= ll ? khi : (-0x7FFFFFFF - 1), 1);
         s += (int32_t)tot;
     };

@@ -9,23 +9,51 @@
 
 namespace swimdev {
 
-__device__ __forceinline__ int wsum(int v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
+// ---- wave scans and reductions on DPP (GFX9 data-parallel moves: shifts within a row of 16 lanes, then the rows'
+// last lanes broadcast to the rows after them) instead of ds_bpermute, whose every step is an LDS crossbar round trip:
+// six VALU steps for a 64-lane inclusive scan. Callers run them with every lane of the wave active. ----
+#define SWIM_DPP(old, src, ctrl, rm) ((uint32_t)__builtin_amdgcn_update_dpp((int)(old), (int)(src), (ctrl), (rm), 0xf, false))
+template <typename Op>
+__device__ __forceinline__ uint32_t dpp_scan(uint32_t x, uint32_t id, Op op) {
+    x = op(x, SWIM_DPP(id, x, 0x111, 0xf));                     // row_shr:1
+    x = op(x, SWIM_DPP(id, x, 0x112, 0xf));                     // row_shr:2
+    x = op(x, SWIM_DPP(id, x, 0x114, 0xf));                     // row_shr:4
+    x = op(x, SWIM_DPP(id, x, 0x118, 0xf));                     // row_shr:8
+    x = op(x, SWIM_DPP(id, x, 0x142, 0xa));                     // row_bcast:15 into rows 1 and 3
+    x = op(x, SWIM_DPP(id, x, 0x143, 0xc));                     // row_bcast:31 into rows 2 and 3
+    return x;
 }
-__device__ __forceinline__ uint32_t wmin(uint32_t v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, off, 64));
-    return v;
+__device__ __forceinline__ uint32_t dpp_scan_add(uint32_t x) { return dpp_scan(x, 0u, [](uint32_t a, uint32_t b) { return a + b; }); }
+__device__ __forceinline__ uint32_t dpp_scan_umin(uint32_t x) {
+    return dpp_scan(x, 0xFFFFFFFFu, [](uint32_t a, uint32_t b) { return min(a, b); });
 }
+__device__ __forceinline__ int32_t dpp_scan_imax(int32_t x) {
+    return (int32_t)dpp_scan((uint32_t)x, 0x80000000u, [](uint32_t a, uint32_t b) { return (uint32_t)max((int32_t)a, (int32_t)b); });
+}
+__device__ __forceinline__ int32_t dpp_scan_imin(int32_t x) {
+    return (int32_t)dpp_scan((uint32_t)x, 0x7FFFFFFFu, [](uint32_t a, uint32_t b) { return (uint32_t)min((int32_t)a, (int32_t)b); });
+}
+__device__ __forceinline__ uint32_t dpp_scan_or(uint32_t x) { return dpp_scan(x, 0u, [](uint32_t a, uint32_t b) { return a | b; }); }
+__device__ __forceinline__ uint32_t lane63(uint32_t x) { return (uint32_t)__builtin_amdgcn_readlane((int)x, 63); }
+// lane i gets lane i - 1's value (lane 0: id)
+__device__ __forceinline__ uint32_t dpp_shr1(uint32_t x, uint32_t id) { return SWIM_DPP(id, x, 0x138, 0xf); }   // wave_shr:1
+
+__device__ __forceinline__ int wsum(int v) { return (int)lane63(dpp_scan_add((uint32_t)v)); }
+__device__ __forceinline__ uint32_t wmin(uint32_t v) { return lane63(dpp_scan_umin(v)); }
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ uint32_t wave_gid() { return (blockIdx.x * blockDim.x + threadIdx.x) >> 6; }
 __device__ __forceinline__ uint64_t lanemask_lt() { return (1ull << lane_id()) - 1ull; }
 
 __device__ __forceinline__ unsigned long long bcast64(unsigned long long v) {
-    uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, 0, 64), hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), 0, 64);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 0);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 0);
     return ((unsigned long long)hi << 32) | lo;
+}
+// the wave's sum of a 64-bit value, as three 32-bit DPP sums (the low word in 16-bit halves: no carry is lost)
+__device__ __forceinline__ unsigned long long wsum64(unsigned long long v) {
+    const uint32_t a = lane63(dpp_scan_add((uint32_t)v & 0xFFFFu)), b = lane63(dpp_scan_add((uint32_t)v >> 16));
+    const uint32_t c = lane63(dpp_scan_add((uint32_t)(v >> 32)));
+    return ((unsigned long long)c << 32) + ((unsigned long long)b << 16) + (unsigned long long)a;
 }
 
 // protocol counters: CTR_SHARDS copies on separate lines, picked by workgroup, summed at read-back
@@ -191,19 +219,13 @@ __device__ __forceinline__ void fold_row(const DS &d, uint32_t ol, int dping, in
     if (nref) ctr_add(d, C_REFUTES, (unsigned long long)nref);
 }
 
-__device__ __forceinline__ int wmax(int v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off, 64));
-    return v;
-}
+__device__ __forceinline__ int wmax(int v) { return (int)lane63((uint32_t)dpp_scan_imax(v)); }
 
 __device__ __forceinline__ void wave_finalize(const DS &d, uint32_t ol, const MAcc &acc, int cset = 0, bool next_update = true) {
     const int dping = wsum(acc.dping), ddc = wsum(acc.ddc), napp = wsum(acc.napp), nref = wsum(acc.nref);
     const int ev = wsum(acc.evict), np = wsum(acc.nproc), dl = wsum(acc.dlen), ml = wmax(acc.maxlast);
     const int inv = wmax(acc.inval), dnh = wsum(acc.dnh);
-    unsigned long long dfp = acc.dfp;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) dfp += __shfl_xor(dfp, off, 64);
+    const unsigned long long dfp = wsum64(acc.dfp);
     if (lane_id() == 0) {
         fold_row(d, ol, dping, ddc, napp, nref, ev, dl, ml, inv, dfp, next_update, dnh);
         if (np && cset < 2) ctr_add(d, cset ? C_X_MERGED_R : C_X_MERGED, (unsigned long long)np);
@@ -350,13 +372,8 @@ __device__ __forceinline__ unsigned long long pool_alloc(const DS &d, uint32_t n
 }
 
 __device__ __forceinline__ uint32_t wscan_excl(uint32_t v, uint32_t &total) {
-    uint32_t x = v;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)x, off, 64);
-        if (lane_id() >= (uint32_t)off) x += y;
-    }
-    total = (uint32_t)__shfl((int)x, 63, 64);
+    const uint32_t x = dpp_scan_add(v);
+    total = lane63(x);
     return x - v;
 }
 
@@ -540,7 +557,7 @@ __device__ uint32_t wave_issue_recv(const DS &d, uint32_t ol, uint32_t sender, u
 __device__ bool wave_snapshot(const DS &d, uint32_t ol, uint32_t o, MsgDesc &out) {
     uint32_t slot = 0;
     if (lane_id() == 0) slot = atomicAdd(d.dense_cur, 1u);
-    slot = (uint32_t)__shfl((int)slot, 0, 64);
+    slot = (uint32_t)__builtin_amdgcn_readlane((int)slot, 0);
     out.kind = 2; out.len = 0; out.off_lo = out.off_hi = 0;
     if (slot >= d.dense_cap) {
         if (lane_id() == 0) atomicOr(d.err, E_DENSE);
