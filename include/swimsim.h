@@ -238,6 +238,8 @@ int swimsim_memory(swimsim_t *h, swimsim_memory_t *out);
 /* average device time (ms) of each kernel family since the last reset, for roofline reporting */
 int swimsim_kernel_times(swimsim_t *h, const char **names, double *avg_ms, uint64_t *launches,
                          double *alg_bytes, size_t cap, size_t *n);
+/* enable: 0 off, 1 every kernel family, 2 only the families the bench line's roofline reports (checksum chains, merges,
+ * issue; each timed family costs an event pair per launch in the timed stream) */
 int swimsim_enable_timing(swimsim_t *h, int32_t enable);
 /* the unit counts behind those byte figures since swimsim_enable_timing (rows hashed by each checksum kernel,
  * changes processed / applied by each merge kernel, records issued, ...): names[i], values[i]; "hot_slots" is
