@@ -75,14 +75,20 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ int32_t csr_ceil20(int32_t x) { return x >= 0 ? (x + 19) / 20 : -((-x) / 20); }
 
-// window code of a clean block at position i of a super step for a row at shift s (plan of its workgroup)
-// (clamped into the window: a shift with no clean block after it, i.e. past the row's last exception run, is only
-// ever read by predicated blocks beyond the row's chain)
+// The window of a super step holds, for every phase in use (slot ps of nph) and window position w (0 .. Wn-1), the
+// premixed entry of S_B block 32 t - cmax + w at that phase, phase-interleaved: entry w nph + ps. A row at shift s
+// reads position cmax - ceil(s / 20) + i for block i, so its entry is const + nph i - s / 2 (for even shifts; nph = 10
+// with every even phase in use): rows at nearby shifts read nearby entries, in distinct LDS banks. (Round 4's
+// phase-major layout, entry ps Wn + w, put rows 18 bytes apart on one bank: 1.05e9 bank-conflict cycles per heavy
+// launch, half of the LDS's active cycles.)
+// The entry of block 0 of a super step for a row at shift s (clamped into the window: a shift with no clean block
+// after it, i.e. past the row's last exception run, is only ever read by predicated blocks beyond the row's chain);
+// block i's entry is that + i nph.
 __device__ __forceinline__ uint32_t csr_base(const CsrPlan &p, int32_t s) {
     const uint32_t phi = csd_phase(s);
     const uint32_t ps = (uint32_t)__popc(p.phm & ((1u << phi) - 1u));
-    const int32_t c = ps * (int32_t)p.Wn + (p.cmax - csr_ceil20(s));
-    return (uint32_t)min(max(c, 0), CSR_WINMAX - CSR_SB);
+    const int32_t w = min(max(p.cmax - csr_ceil20(s), 0), (int32_t)p.Wn - CSR_SB);
+    return (uint32_t)w * p.nph + ps;
 }
 
 __global__ void k_csr_ptable(const uint32_t *__restrict__ SBw, uint32_t sbw_words, uint32_t KP, uint4 *__restrict__ P) {
@@ -133,7 +139,7 @@ __global__ void __launch_bounds__(CSR_ROWS) k_csr_plan(DS d, const uint32_t *lis
             uint32_t phm = ph[k];
             if (phm == 0) { phm = 1; smin = 0; smax = 0; }
             p.cmax = csr_ceil20(smax);
-            p.Wn = ((uint32_t)(CSR_SB + (p.cmax - csr_ceil20(smin)) + 1) + 30u) / 32u * 32u + 1u;   // = 1 mod 32 (k_csr)
+            p.Wn = (uint32_t)(CSR_SB + (p.cmax - csr_ceil20(smin)) + 1);
             p.phm = phm;
             p.nph = (uint32_t)__popc(phm);
             p.maxit = mi[k];
@@ -198,7 +204,7 @@ __global__ void __launch_bounds__(256) k_csr_rec(DS d, const uint32_t *list, uin
                             q++;
                             kn = q < gend ? hd[wv][q].x : 0xFFFFFFFFu;
                         } else {
-                            c = j < iters ? (csr_base(p, s) + b) * CSR_ESZ : 0u;
+                            c = j < iters ? (csr_base(p, s) + b * p.nph) * CSR_ESZ : 0u;
                         }
                         if (b & 1u) r.code[b >> 1] |= c << 16;
                         else r.code[b >> 1] = c;
@@ -316,7 +322,7 @@ __device__ __forceinline__ void c3_stage(const DS &d, const uint32_t *list, uint
 #pragma unroll
     for (int v = 0; v < WV; v++) {
         const uint32_t u = tid + (uint32_t)CSR_ROWS * v;
-        const uint32_t ps = u < nwin ? u / p.Wn : 0u, w = u < nwin ? u - ps * p.Wn : 0u;
+        const uint32_t w = u < nwin ? u / p.nph : 0u, ps = u < nwin ? u - w * p.nph : 0u;   // (phase-interleaved)
         wsrc[v] = L.phs[min(ps, 19u)] * a.KP;
         wk0[v] = u < nwin ? (int32_t)w - p.cmax : 0x40000000;
     }
@@ -424,7 +430,7 @@ __device__ __forceinline__ void c3_stage(const DS &d, const uint32_t *list, uint
         if (!has) {
             const uint32_t want = r.live ? base : 0xFFFFFFFDu;      // (rows not hashed read entry 0)
             if (tag[b] != want) {
-                const uint32_t c0 = r.live ? base * CSR_ESZ : 0u, st2 = r.live ? 2u * CSR_ESZ : 0u, st1 = r.live ? CSR_ESZ : 0u;
+                const uint32_t c0 = r.live ? base * CSR_ESZ : 0u, st1 = r.live ? p.nph * CSR_ESZ : 0u, st2 = 2u * st1;
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
                     const uint32_t c = c0 + (uint32_t)(4 * q) * st2;
