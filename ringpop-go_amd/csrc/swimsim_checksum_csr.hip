@@ -235,13 +235,17 @@ __global__ void __launch_bounds__(256) k_csr_rec(DS d, const uint32_t *list, uin
 // k_csr3: chain waves that only run chains (round 5). k_csr2's waves spent 39 % (light rounds) to 55 % (heavy) of
 // their loop outside the chain: staging the next super step's window, unpacking records, writing exception entries,
 // and waiting at the per-super-step barrier for the slowest of the eight (shader-clock stamps, tools/csr_stamps.py).
-// Here a third wave per SIMD, the stager (lane = row), does all of that one super step ahead, and no barrier is left
-// in the loop: buffer b of the window, exception areas and code table is handed over by two LDS counters,
-// ready[b] (stagers that finished filling it: 4 per super step) and done[b] (chain waves that finished reading it: 8
-// per super step). A chain wave waits only until the stagers have filled the super step it needs, reads its row's 32
-// codes (u16, written by the stager: base(s) + i, or a record's codes with its exceptions patched to the wave's slots)
-// and runs the chain. Roles: waves 0-3 g/f lanes, 4-7 h lanes, 8-11 stagers; waves w, w + 4 and w + 8 share a SIMD
-// and rows 64 w .. 64 w + 63.
+// Here two more waves per SIMD do all of that one super step ahead, the record stager (lane = row: codes, exception
+// entries) and the window stager (a quarter of the window, two super steps ahead), and no barrier is left in the
+// loop: buffer b of the window, exception areas and code table is handed over by LDS counters: readyw[b] (window
+// stagers that finished filling it: 4 per super step), readyr[g][b] (row group g's record stager: 1 per super step),
+// done[b] (chain waves that finished reading it: 8 per super step, which the window stagers wait for) and doner[g][b]
+// (group g's two chain waves, which its record stager waits for: a group's codes and exception area are its own, so a
+// slow record stager holds up only its own group's chains).
+// A chain wave waits only until the stagers have filled the super step it needs, reads its row's 32 codes (u16,
+// written by the record stager: base(s) + i, or a record's codes with its exceptions patched to the wave's slots) and
+// runs the chain. Roles: waves 0-3 g/f lanes, 4-7 h lanes, 8-11 record stagers, 12-15 window stagers; waves w, w + 4,
+// w + 8 and w + 12 share a SIMD and rows 64 w .. 64 w + 63.
 // ---------------------------------------------------------------------------------------------------------------
 constexpr int C3_EXW = 384;
 constexpr int C3_ENT = CSR_WINMAX + 4 * C3_EXW;
@@ -252,7 +256,8 @@ struct Csr3Lds {
     uint4 TC[2][4][CSR_ROWS];              // codes: TC[b][q][row] = u16 codes 8q .. 8q + 7 of the row (lane-contiguous)
     uint32_t XH[CSR_ROWS];                 // h lanes' final state
     uint32_t FLX[CSR_ROWS];                // rows the stagers flagged (exception slots)
-    uint32_t ready[2], done[2];
+    uint32_t readyw[2], done[2];           // window stagers that filled buffer b (4 a super step); chains done with it (8)
+    uint32_t readyr[4][2], doner[4][2];    // per row group: its record stager (1 a super step), its two chain waves (2)
     uint32_t ovf[2];                       // buffer b's overflow slots in the window's unused tail: (super step << 16) | used
     uint32_t phs[20];
 };
@@ -288,10 +293,13 @@ __device__ __forceinline__ C3Row c3_row(const DS &d, const uint32_t *list, uint3
     return r;
 }
 
-// the stager of rows 64 w .. 64 w + 63 (lane = row) and of a quarter of every super step's window
+// the record stager of rows 64 w .. 64 w + 63 (lane = row): their codes and exception entries one super step ahead
 __device__ __forceinline__ void c3_stage(const DS &d, const uint32_t *list, uint32_t cnt, const CsrArgs &a, const CsrPlan &p,
                                          Csr3Lds &L, uint32_t T_) {
     const uint32_t tid = threadIdx.x & (CSR_ROWS - 1), rwave = tid >> 6;
+#if defined(C3_SPRIO) && C3_SPRIO > 0
+    __builtin_amdgcn_s_setprio(C3_SPRIO);
+#endif
     C3Row r = c3_row(d, list, cnt, a, p, tid);
     const CsrRec *rec = a.rec + (size_t)(r.valid ? r.gi : blockIdx.x * CSR_ROWS) * a.rcap;
     const uint4 *ent = a.ent + (size_t)(r.valid ? r.gi : blockIdx.x * CSR_ROWS) * a.ecap * 2;
@@ -312,50 +320,36 @@ __device__ __forceinline__ void c3_stage(const DS &d, const uint32_t *list, uint
         rv = q < nr;
     };
     load_rec(0, 0);
-    // window: entries u = tid + 256 v (both halves), two register sets (super step u -> set u & 1), loaded two ahead
-    constexpr int WV = CSR_WINMAX / CSR_ROWS;
-    u32x4 wA0[WV], wB0[WV];
-    u32x2 wA1[WV], wB1[WV];
     const uint32_t nwin = p.nph * p.Wn;
-    uint32_t wsrc[WV];                                               // (phase rows of P as entry offsets: 32-bit)
-    int32_t wk0[WV];
-#pragma unroll
-    for (int v = 0; v < WV; v++) {
-        const uint32_t u = tid + (uint32_t)CSR_ROWS * v;
-        const uint32_t w = u < nwin ? u / p.nph : 0u, ps = u < nwin ? u - w * p.nph : 0u;   // (phase-interleaved)
-        wsrc[v] = L.phs[min(ps, 19u)] * a.KP;
-        wk0[v] = u < nwin ? (int32_t)w - p.cmax : 0x40000000;
-    }
-    auto wload = [&](u32x4 (&w0)[WV], u32x2 (&w1)[WV], uint32_t t) {
-#pragma unroll
-        for (int v = 0; v < WV; v++) {
-            const int32_t k = min(max(wk0[v] + (int32_t)(t * CSR_SB), 0), (int32_t)a.KP - 1);
-            const uint4 *src = a.P + 2 * (size_t)(wsrc[v] + (uint32_t)k);
-            w0[v] = *(const u32x4 *)src;
-            w1[v] = *(const u32x2 *)(src + 1);
-        }
-    };
-    auto wstore = [&](const u32x4 (&w0)[WV], const u32x2 (&w1)[WV], uint32_t b) {
-#pragma unroll
-        for (int v = 0; v < WV; v++) {
-            const uint32_t u = tid + (uint32_t)CSR_ROWS * v;
-            if (u < nwin) {                                        // (the tail holds overflow exception entries)
-                *(u32x4 *)&L.EA[b][u] = w0[v];
-                *(u32x2 *)&L.EB[b][u] = w1[v];
-            }
-        }
-    };
     int32_t s = 0;
     uint32_t base = csr_base(p, 0);
     uint32_t tag[2] = {0xFFFFFFFEu, 0xFFFFFFFEu};                  // what TC[b][.][row] holds: a base, or a record
     // one super step's codes and exceptions of this row into buffer b
+#ifdef CSR_DIAG_NE
+    uint64_t dg_[4] = {0, 0, 0, 0};
+#endif
     auto prep = [&](uint32_t t, uint32_t b) {
+#ifdef C3_T_NOREC
+        const bool has = false;
+#else
         const bool has = r.live && rv && R0.x == t;
+#endif
         if (__ballot(has)) {
             uint32_t ne = has ? R0.w : 0u, tot = 0;
+#ifdef CSR_DIAG_NE
+            {                                                       // (diagnostics: record super steps, long ones)
+                const uint64_t bh = __ballot(has), bl = __ballot(ne > (uint32_t)CSR_EREG);
+                dg_[0]++;
+                dg_[1] += (uint64_t)__popcll(bh);
+                dg_[2] += bl ? 1u : 0u;
+                dg_[3] += (uint64_t)__popcll(bl);
+            }
+#endif
             const uint32_t sb = wscan_excl(ne, tot);
             uint32_t xb = (uint32_t)CSR_WINMAX + rwave * C3_EXW + sb;
             if (tot > a.exw) {
+                // (the tail is shared by the groups: every chain must be done with super step t - 2 first)
+                if (t >= 2) c3_wait(&L.done[b], 8u * (t >> 1));
                 // more exceptions than the wave's area: the rows past it take slots in the window's unused tail
                 // [nwin, CSR_WINMAX) of this buffer (shared by the stagers of this super step, tagged with it), else they
                 // are left to the production kernels
@@ -462,27 +456,27 @@ __device__ __forceinline__ void c3_stage(const DS &d, const uint32_t *list, uint
 #define C3S_STAMP(v)
 #define C3S_ACC(k, x)
 #endif
-    wload(wA0, wA1, 0);
-    wload(wB0, wB1, 1);
     auto step = [&](uint32_t u, auto BC) {
         constexpr uint32_t b = decltype(BC)::value;
         C3S_STAMP(s0);
-        if (u >= 2) c3_wait(&L.done[b], 8u * (u >> 1));           // the chains are done with super step u - 2
+        if (u >= 2) c3_wait(&L.doner[rwave][b], 2u * (u >> 1));   // this group's chains are done with super step u - 2
         C3S_STAMP(s1);
-        // (window loads before the records' loads: issued after them (loads complete in order, and the compiler
-        // waits for every load of the wave that may precede a set's), the stores of a set waited for the last step's
-        // records and the heavy rounds took 4 % longer)
-        if constexpr (b) { wstore(wB0, wB1, 1u); wload(wB0, wB1, u + 2); }
-        else { wstore(wA0, wA1, 0u); wload(wA0, wA1, u + 2); }
+#ifdef CSR_DIAG_STAMP
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");            // (diagnostics: slot 1 = the record loads' wait)
+#endif
         C3S_STAMP(s2);
         prep(u, b);
         C3S_STAMP(s3);
-        c3_signal(&L.ready[b]);
+        c3_signal(&L.readyr[rwave][b]);
         C3S_STAMP(s4);
         C3S_ACC(0, s1 - s0);
+#ifndef CSR_DIAG_WINDOW
         C3S_ACC(1, s2 - s1);
+#endif
         C3S_ACC(2, s3 - s2);
+#ifndef CSR_DIAG_WINDOW
         C3S_ACC(3, s4 - s3);
+#endif
     };
     uint32_t u = 0;
     for (; u + 1 < T_; u += 2) {
@@ -496,7 +490,73 @@ __device__ __forceinline__ void c3_stage(const DS &d, const uint32_t *list, uint
 #endif
 #undef C3S_STAMP
 #undef C3S_ACC
+#ifdef CSR_DIAG_NE
+    if ((threadIdx.x & 63u) == 0)
+        for (int k = 0; k < 4; k++) ctr_add(d, C_NALL + 4 + k, (unsigned long long)dg_[k]);
+#endif
     L.FLX[tid] = r.fl;
+}
+
+// the window stager (role 3): a quarter of every super step's window, entries u = tid + 256 v (both halves), from
+// two register sets (super step u -> set u & 1) loaded two super steps ahead. A wave of its own since round 5's
+// stamps: in the record stager's loop the window took 34-43 % of the chain waves' loop, and the chains waited for it.
+__device__ __forceinline__ void c3_wstage(const CsrArgs &a, const CsrPlan &p, Csr3Lds &L, uint32_t T_) {
+    const uint32_t tid = threadIdx.x & (CSR_ROWS - 1);
+#if defined(C3_WPRIO) && C3_WPRIO > 0
+    __builtin_amdgcn_s_setprio(C3_WPRIO);
+#endif
+    // window: entries u = tid + 256 v (both halves), two register sets (super step u -> set u & 1), loaded two ahead
+    constexpr int WV = CSR_WINMAX / CSR_ROWS;
+    u32x4 wA0[WV], wB0[WV];
+    u32x2 wA1[WV], wB1[WV];
+    const uint32_t nwin = p.nph * p.Wn;
+    uint32_t wsrc[WV];                                               // (phase rows of P as entry offsets: 32-bit)
+    int32_t wk0[WV];
+#pragma unroll
+    for (int v = 0; v < WV; v++) {
+        const uint32_t u = tid + (uint32_t)CSR_ROWS * v;
+        const uint32_t w = u < nwin ? u / p.nph : 0u, ps = u < nwin ? u - w * p.nph : 0u;   // (phase-interleaved)
+        wsrc[v] = L.phs[min(ps, 19u)] * a.KP;
+        wk0[v] = u < nwin ? (int32_t)w - p.cmax : 0x40000000;
+    }
+    auto wload = [&](u32x4 (&w0)[WV], u32x2 (&w1)[WV], uint32_t t) {
+#pragma unroll
+        for (int v = 0; v < WV; v++) {
+            const int32_t k = min(max(wk0[v] + (int32_t)(t * CSR_SB), 0), (int32_t)a.KP - 1);
+            const uint4 *src = a.P + 2 * (size_t)(wsrc[v] + (uint32_t)k);
+#ifdef C3_T_NOWIN
+            w0[v] = u32x4{(uint32_t)k, 1u, 2u, 3u}; w1[v] = u32x2{(uint32_t)k, 5u}; (void)src;
+#else
+            w0[v] = *(const u32x4 *)src;
+            w1[v] = *(const u32x2 *)(src + 1);
+#endif
+        }
+    };
+    auto wstore = [&](const u32x4 (&w0)[WV], const u32x2 (&w1)[WV], uint32_t b) {
+#pragma unroll
+        for (int v = 0; v < WV; v++) {
+            const uint32_t u = tid + (uint32_t)CSR_ROWS * v;
+            if (u < nwin) {                                        // (the tail holds overflow exception entries)
+                *(u32x4 *)&L.EA[b][u] = w0[v];
+                *(u32x2 *)&L.EB[b][u] = w1[v];
+            }
+        }
+    };
+    wload(wA0, wA1, 0);
+    wload(wB0, wB1, 1);
+    auto step = [&](uint32_t u, auto BC) {
+        constexpr uint32_t b = decltype(BC)::value;
+        if (u >= 2) c3_wait(&L.done[b], 8u * (u >> 1));           // every chain is done with super step u - 2
+        if constexpr (b) { wstore(wB0, wB1, 1u); wload(wB0, wB1, u + 2); }
+        else { wstore(wA0, wA1, 0u); wload(wA0, wA1, u + 2); }
+        c3_signal(&L.readyw[b]);
+    };
+    uint32_t u = 0;
+    for (; u + 1 < T_; u += 2) {
+        step(u, std::integral_constant<uint32_t, 0>{});
+        step(u + 1, std::integral_constant<uint32_t, 1>{});
+    }
+    if (u < T_) step(u, std::integral_constant<uint32_t, 0>{});
 }
 
 template <int W, int ROLE>                                          // ROLE 0: g/f lanes, 1: h lanes
@@ -504,7 +564,7 @@ __device__ __forceinline__ void c3_chain(const DS &d, const uint32_t *list, uint
                                          Csr3Lds &L, uint32_t T_) {
     constexpr bool GF = ROLE == 0;
     typedef typename std::conditional<GF, u32x4, u32x2>::type EV;
-    const uint32_t tid = threadIdx.x & (CSR_ROWS - 1);
+    const uint32_t tid = threadIdx.x & (CSR_ROWS - 1), grp = tid >> 6;
     const C3Row r = c3_row(d, list, cnt, a, p, tid);
     const uint32_t myit = r.live ? r.iters : 0u;
     const uint32_t *row = csd_row(d, r.id);
@@ -536,7 +596,8 @@ __device__ __forceinline__ void c3_chain(const DS &d, const uint32_t *list, uint
         constexpr uint32_t b = decltype(BC)::value;
         const uint32_t K0 = t * CSR_SB;
         C3_STAMP(ta);
-        c3_wait(&L.ready[b], 4u * ((t >> 1) + 1u));               // the stagers have filled super step t
+        c3_wait(&L.readyr[grp][b], (t >> 1) + 1u);                // this group's record stager has filled super step t
+        c3_wait(&L.readyw[b], 4u * ((t >> 1) + 1u));              // and the window stagers
         C3_STAMP(tb);
 #pragma unroll
         for (int q = 0; q < 4; q++) {
@@ -576,10 +637,13 @@ __device__ __forceinline__ void c3_chain(const DS &d, const uint32_t *list, uint
         if (full) run(std::integral_constant<bool, true>{});
         else run(std::integral_constant<bool, false>{});
         c3_signal(&L.done[b]);
+        c3_signal(&L.doner[grp][b]);
         C3_STAMP(td);
         C3_ACC(0, td - tc);
         C3_ACC(1, tb - ta);
+#ifndef CSR_DIAG_WINDOW
         C3_ACC(2, tc - tb);
+#endif
     };
     uint32_t t = 0;
     for (; t + 1 < T_; t += 2) {
@@ -623,21 +687,32 @@ __device__ __forceinline__ void c3_chain(const DS &d, const uint32_t *list, uint
 }
 
 template <int W>
-__global__ void __launch_bounds__(3 * CSR_ROWS) k_csr3(DS d, const uint32_t *list, const uint32_t *count, CsrArgs a) {
+__global__ void __launch_bounds__(4 * CSR_ROWS) k_csr3(DS d, const uint32_t *list, const uint32_t *count, CsrArgs a) {
     __shared__ Csr3Lds L;
     const uint32_t cnt = *count;
     if (blockIdx.x * CSR_ROWS >= cnt) return;
     const CsrPlan p = a.plan[blockIdx.x];
     if (threadIdx.x < 20 && ((p.phm >> threadIdx.x) & 1u)) L.phs[__popc(p.phm & ((1u << threadIdx.x) - 1u))] = threadIdx.x;
-    if (threadIdx.x < 2) { L.ready[threadIdx.x] = 0; L.done[threadIdx.x] = 0; L.ovf[threadIdx.x] = 0xFFFF0000u; }
+    if (threadIdx.x < 2) { L.readyw[threadIdx.x] = 0; L.done[threadIdx.x] = 0; L.ovf[threadIdx.x] = 0xFFFF0000u; }
+    if (threadIdx.x < 8) { (&L.readyr[0][0])[threadIdx.x] = 0; (&L.doner[0][0])[threadIdx.x] = 0; }
     __syncthreads();
     const uint32_t T_ = p.feasible ? (p.maxit + CSR_SB - 1) / CSR_SB : 0u;
     const uint32_t role = threadIdx.x / CSR_ROWS;
     if (role == 0) c3_chain<W, 0>(d, list, cnt, a, p, L, T_);
     else if (role == 1) c3_chain<W, 1>(d, list, cnt, a, p, L, T_);
-    else {
+    else if (role == 2) {
         c3_stage(d, list, cnt, a, p, L, T_);
         __syncthreads();                                            // (the chain waves' final barrier)
+    } else {
+        c3_wstage(a, p, L, T_);
+#if defined(CSR_DIAG_STAMP) && defined(CSR_DIAG_WINDOW)
+        if (threadIdx.x == 3 * CSR_ROWS) {                          // (diagnostics: window geometry per super step)
+            ctr_add(d, C_NALL + 2, (unsigned long long)T_);
+            ctr_add(d, C_NALL + 5, (unsigned long long)T_ * p.nph * p.Wn);
+            ctr_add(d, C_NALL + 7, (unsigned long long)T_ * p.nph);
+        }
+#endif
+        __syncthreads();
     }
 }
 
@@ -656,7 +731,7 @@ void launch_csr_w(const DS &d, const uint32_t *list, uint32_t n, const uint32_t 
         hipLaunchKernelGGL(k_csr_plan, dim3((n + CSR_ROWS - 1) / CSR_ROWS), dim3(CSR_ROWS), 0, s, d, list, n, a);
         hipLaunchKernelGGL(k_csr_rec, dim3((n + 3) / 4), dim3(256), 0, s, d, list, n, a);
     } else if (part == 4) {
-        hipLaunchKernelGGL((k_csr3<W>), dim3((n + CSR_ROWS - 1) / CSR_ROWS), dim3(3 * CSR_ROWS), 0, s, d, list, count, a);
+        hipLaunchKernelGGL((k_csr3<W>), dim3((n + CSR_ROWS - 1) / CSR_ROWS), dim3(4 * CSR_ROWS), 0, s, d, list, count, a);
     }
 }
 

@@ -22,7 +22,7 @@ ku = c.kernel_units()
 st = [ku.get(f"diag_stamp{i}", 0) for i in range(8)]
 tot = st[3] or 1
 # k_csr3: 0-3 the g/f chain waves (chain, waiting for the stagers, codes, whole loop), 4-7 the stagers (waiting for the
-# chains, window, rows' codes and exceptions, hand-over), each as a share of the chain waves' loop
-names = ["chain", "wait", "codes", "loop", "s_wait", "s_window", "s_prep", "s_signal"]
+# chains, the record loads (vmcnt), rows' codes and exceptions, hand-over), each as a share of the chain waves' loop
+names = ["chain", "wait", "codes", "loop", "s_wait", "s_recload", "s_prep", "s_signal"]
 print(json.dumps({"round": R, "rows": rows, "ms": ms, "cycles": st, "share": {k: round(st[i] / tot, 3) for i, k in
                                                                               enumerate(names)}}))
