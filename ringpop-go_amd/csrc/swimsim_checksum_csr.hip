@@ -66,8 +66,8 @@ struct CsrArgs {
     uint32_t *nrec;        // [rows]
     uint32_t rcap;
     uint32_t *fb_list, *fb_cnt;   // rows left to the production kernels
-    uint32_t exw;                 // k_csr3: exception slots a stager wave uses before the overflow slots (C3_EXW; tests
-                                  // lower it, swimsim_tuning.fault_inject bit 4)
+    uint32_t exw;                 // k_csr3: entries of a row group's exception ring, a power of two (C3_RING; tests
+                                  // lower it to 8, swimsim_tuning.fault_inject bit 4)
 };
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -235,30 +235,38 @@ __global__ void __launch_bounds__(256) k_csr_rec(DS d, const uint32_t *list, uin
 // k_csr3: chain waves that only run chains (round 5). k_csr2's waves spent 39 % (light rounds) to 55 % (heavy) of
 // their loop outside the chain: staging the next super step's window, unpacking records, writing exception entries,
 // and waiting at the per-super-step barrier for the slowest of the eight (shader-clock stamps, tools/csr_stamps.py).
-// Here two more waves per SIMD do all of that one super step ahead, the record stager (lane = row: codes, exception
+// Here two more waves per SIMD do all of that ahead of the chains, the record stager (lane = row: codes, exception
 // entries) and the window stager (a quarter of the window, two super steps ahead), and no barrier is left in the
-// loop: buffer b of the window, exception areas and code table is handed over by LDS counters: readyw[b] (window
-// stagers that finished filling it: 4 per super step), readyr[g][b] (row group g's record stager: 1 per super step),
-// done[b] (chain waves that finished reading it: 8 per super step, which the window stagers wait for) and doner[g][b]
-// (group g's two chain waves, which its record stager waits for: a group's codes and exception area are its own, so a
-// slow record stager holds up only its own group's chains).
-// A chain wave waits only until the stagers have filled the super step it needs, reads its row's 32 codes (u16,
-// written by the record stager: base(s) + i, or a record's codes with its exceptions patched to the wave's slots) and
-// runs the chain. Roles: waves 0-3 g/f lanes, 4-7 h lanes, 8-11 record stagers, 12-15 window stagers; waves w, w + 4,
-// w + 8 and w + 12 share a SIMD and rows 64 w .. 64 w + 63.
+// loop. The window is double-buffered (window buffer t & 1); the codes are triple-buffered (TC[t % 3]) and the
+// exception entries live in a ring per row group, so a record stager runs up to two super steps ahead of its chains
+// (the stamps of the double-buffered version: its chains waited 30 % of a heavy round for it while it waited 45 % of
+// the time for them, one super step of slack against records that come in bursts). LDS counters hand the buffers
+// over: readyw[b] (window stagers that filled window buffer b: 4 per super step), done[b] (chain waves done with it:
+// 8 per super step, which the window stagers wait for), readyr[g] (super steps group g's record stager has staged)
+// and doner[g] (super steps group g's two chain waves have finished, 2 per super step: a group's codes and ring are
+// its own, so its record stager waits only for them). Codes are u16 byte offsets into the entry arrays (window
+// buffer 0, window buffer 1, then the four rings) from the super step's window buffer, so base codes do not depend on
+// which window buffer a code buffer meets.
+// A chain wave waits only until the stagers have filled the super step it needs, reads its row's 32 codes (base(s) + i
+// in its window buffer, or a record's codes with its exceptions patched to ring slots) and runs the chain. Roles:
+// waves 0-3 g/f lanes, 4-7 h lanes, 8-11 record stagers, 12-15 window stagers; waves w, w + 4, w + 8 and w + 12 share
+// a SIMD and rows 64 w .. 64 w + 63.
 // ---------------------------------------------------------------------------------------------------------------
-constexpr int C3_EXW = 384;
-constexpr int C3_ENT = CSR_WINMAX + 4 * C3_EXW;
+constexpr int C3_RING = 512;                       // exception ring entries per row group (a power of two)
+constexpr int C3_ENT = 2 * CSR_WINMAX + 4 * C3_RING;   // 4,096 entries: byte offsets fit the u16 codes
+constexpr int C3_TCB = 3;                          // code table buffers
+static_assert(C3_ENT * CSR_ESZ <= 65536, "codes are u16 byte offsets");
 
 struct Csr3Lds {
-    uint4 EA[2][C3_ENT];                   // {Mg, D, Mf, PF} per entry
-    uint2 EB[2][C3_ENT];                   // {Mh, KH}
-    uint4 TC[2][4][CSR_ROWS];              // codes: TC[b][q][row] = u16 codes 8q .. 8q + 7 of the row (lane-contiguous)
+    // (EB first: both arrays then start below 64 KB, so an entry's base folds into the LDS reads' immediate offset;
+    // with EB at 64 KB every h-lane read took a v_or of its base)
+    uint2 EB[C3_ENT];                      // {Mh, KH} per entry: window buffers 0 and 1, then the rings
+    uint4 EA[C3_ENT];                      // {Mg, D, Mf, PF}
+    uint4 TC[C3_TCB][4][CSR_ROWS];         // codes: TC[k][q][row] = u16 codes 8q .. 8q + 7 of the row (lane-contiguous)
     uint32_t XH[CSR_ROWS];                 // h lanes' final state
     uint32_t FLX[CSR_ROWS];                // rows the stagers flagged (exception slots)
     uint32_t readyw[2], done[2];           // window stagers that filled buffer b (4 a super step); chains done with it (8)
-    uint32_t readyr[4][2], doner[4][2];    // per row group: its record stager (1 a super step), its two chain waves (2)
-    uint32_t ovf[2];                       // buffer b's overflow slots in the window's unused tail: (super step << 16) | used
+    uint32_t readyr[4], doner[4];          // per row group: super steps staged by its record stager; its chains' steps
     uint32_t phs[20];
 };
 
@@ -293,7 +301,8 @@ __device__ __forceinline__ C3Row c3_row(const DS &d, const uint32_t *list, uint3
     return r;
 }
 
-// the record stager of rows 64 w .. 64 w + 63 (lane = row): their codes and exception entries one super step ahead
+// the record stager of rows 64 w .. 64 w + 63 (lane = row): their codes and exception entries, up to two super steps
+// ahead of the group's chains
 __device__ __forceinline__ void c3_stage(const DS &d, const uint32_t *list, uint32_t cnt, const CsrArgs &a, const CsrPlan &p,
                                          Csr3Lds &L, uint32_t T_) {
     const uint32_t tid = threadIdx.x & (CSR_ROWS - 1), rwave = tid >> 6;
@@ -320,22 +329,35 @@ __device__ __forceinline__ void c3_stage(const DS &d, const uint32_t *list, uint
         rv = q < nr;
     };
     load_rec(0, 0);
-    const uint32_t nwin = p.nph * p.Wn;
     int32_t s = 0;
     uint32_t base = csr_base(p, 0);
-    uint32_t tag[2] = {0xFFFFFFFEu, 0xFFFFFFFEu};                  // what TC[b][.][row] holds: a base, or a record
-    // one super step's codes and exceptions of this row into buffer b
+    // what TC[k][.][row] holds: base codes (base), or a record (~0)
+    uint32_t tg0 = 0xFFFFFFFEu, tg1 = 0xFFFFFFFEu, tg2 = 0xFFFFFFFEu;
+    // the group's ring (a.exw entries, a power of two): alloc counts the entries handed out (monotone), e1 .. e3 what it
+    // was after super steps u - 1 .. u - 3
+    const uint32_t R = a.exw, ring0 = 2u * CSR_WINMAX + rwave * (uint32_t)C3_RING;
+    uint32_t alloc = 0, e1 = 0, e2 = 0, e3 = 0;
+    // (k is a compile-time constant: the loop is unrolled by 6 = window buffers x code buffers, so the tags stay in
+    // registers)
+    auto tag_ref = [&](auto KC) -> uint32_t & {
+        constexpr uint32_t k = decltype(KC)::value;
+        if constexpr (k == 0) return tg0;
+        else if constexpr (k == 1) return tg1;
+        else return tg2;
+    };
+    // one super step's codes and exceptions of this row into code buffer k (window buffer b)
 #ifdef CSR_DIAG_NE
     uint64_t dg_[4] = {0, 0, 0, 0};
 #endif
-    auto prep = [&](uint32_t t, uint32_t b) {
+    auto prep = [&](uint32_t t, uint32_t b, auto KC) {
+        constexpr uint32_t k = decltype(KC)::value;
 #ifdef C3_T_NOREC
         const bool has = false;
 #else
         const bool has = r.live && rv && R0.x == t;
 #endif
         if (__ballot(has)) {
-            uint32_t ne = has ? R0.w : 0u, tot = 0;
+            uint32_t ne = has && !(r.fl & CSR_F_SLOTS) ? R0.w : 0u, tot = 0;
 #ifdef CSR_DIAG_NE
             {                                                       // (diagnostics: record super steps, long ones)
                 const uint64_t bh = __ballot(has), bl = __ballot(ne > (uint32_t)CSR_EREG);
@@ -346,76 +368,55 @@ __device__ __forceinline__ void c3_stage(const DS &d, const uint32_t *list, uint
             }
 #endif
             const uint32_t sb = wscan_excl(ne, tot);
-            uint32_t xb = (uint32_t)CSR_WINMAX + rwave * C3_EXW + sb;
-            if (tot > a.exw) {
-                // (the tail is shared by the groups: every chain must be done with super step t - 2 first)
-                if (t >= 2) c3_wait(&L.done[b], 8u * (t >> 1));
-                // more exceptions than the wave's area: the rows past it take slots in the window's unused tail
-                // [nwin, CSR_WINMAX) of this buffer (shared by the stagers of this super step, tagged with it), else they
-                // are left to the production kernels
-                const bool over = has && sb + ne > a.exw;
-                const uint32_t f = wmin(over ? sb : 0xFFFFFFFFu);  // the first row past the area
-                const uint32_t need = tot - f;
-                uint32_t got = 0xFFFFFFFFu;
-                if ((threadIdx.x & 63u) == 0) {
-                    const uint32_t room = (uint32_t)CSR_WINMAX - nwin;
-                    uint32_t old = __hip_atomic_load(&L.ovf[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    while (true) {
-                        const uint32_t used = (old >> 16) == (t & 0xFFFFu) ? (old & 0xFFFFu) : 0u;
-                        if (used + need > room) break;
-                        const uint32_t nw = ((t & 0xFFFFu) << 16) | (used + need);
-                        if (__hip_atomic_compare_exchange_strong(&L.ovf[b], &old, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                                 __HIP_MEMORY_SCOPE_WORKGROUP)) {
-                            got = nwin + used;
-                            break;
-                        }
-                    }
-                }
-                got = (uint32_t)__builtin_amdgcn_readlane((int)got, 0);
-                if (over) {
-                    if (got != 0xFFFFFFFFu) xb = got + (sb - f);
-                    else r.fl |= CSR_F_SLOTS;
-                }
+            // ring slots for the wave's exceptions; rows past the ring's size are left to the production kernels
+            const bool over = has && ne > 0 && sb + ne > R;
+            const uint32_t need = tot > R ? wmin(over ? sb : 0xFFFFFFFFu) : tot;
+            if (over) r.fl |= CSR_F_SLOTS;
+            const uint32_t pos = alloc & (R - 1u), skip = pos + need > R ? R - pos : 0u;
+            // the slots of super steps t - 2 and t - 1 may still be read (those of t - 3 are free: the step's wait)
+            if (alloc + skip + need - e3 > R) {
+                if (t >= 2) c3_wait(&L.doner[rwave], 2u * (t - 1u));
+                if (alloc + skip + need - e2 > R && t >= 1) c3_wait(&L.doner[rwave], 2u * t);
             }
+            const uint32_t xb = ring0 + ((alloc + skip) & (R - 1u)) + sb;
+            alloc += skip + need;
             if (has) {
-                L.TC[b][0][tid] = make_uint4(R1.x, R1.y, R1.z, R1.w);
-                L.TC[b][1][tid] = make_uint4(R2.x, R2.y, R2.z, R2.w);
-                L.TC[b][2][tid] = make_uint4(R3.x, R3.y, R3.z, R3.w);
-                L.TC[b][3][tid] = make_uint4(R4.x, R4.y, R4.z, R4.w);
-                tag[b] = 0xFFFFFFFFu;
+                L.TC[k][0][tid] = make_uint4(R1.x, R1.y, R1.z, R1.w);
+                L.TC[k][1][tid] = make_uint4(R2.x, R2.y, R2.z, R2.w);
+                L.TC[k][2][tid] = make_uint4(R3.x, R3.y, R3.z, R3.w);
+                L.TC[k][3][tid] = make_uint4(R4.x, R4.y, R4.z, R4.w);
+                tag_ref(KC) = 0xFFFFFFFFu;
                 if (!(r.fl & CSR_F_SLOTS)) {
-                    const uint32_t xa = xb * CSR_ESZ;
-                    // exception codes -> the wave's slots (u16 stores into the row's codes): block i lives in
-                    // TC[b][i / 8][row], byte 2 (i % 8)
+                    const uint32_t xa = (xb - b * (uint32_t)CSR_WINMAX) * CSR_ESZ;   // (relative to window buffer b)
+                    // exception codes -> the ring's slots (u16 stores into the row's codes): block i lives in
+                    // TC[k][i / 8][row], halfword i % 8
                     auto patch = [&](uint32_t i, uint32_t ord) {
-                        uint16_t *c16 = (uint16_t *)&L.TC[b][i >> 3][tid] + (i & 7u);
+                        uint16_t *c16 = (uint16_t *)&L.TC[k][i >> 3][tid] + (i & 7u);
                         *c16 = (uint16_t)(xa + ord * CSR_ESZ);
                     };
                     if (ne <= (uint32_t)CSR_EREG) {
-                        const uint32_t pos = R0.z;
-                        if (ne > 0) patch(pos & 31u, 0);
-                        if (ne > 1) patch((pos >> 8) & 31u, 1);
-                        if (ne > 2) patch((pos >> 16) & 31u, 2);
-                        if (ne > 3) patch((pos >> 24) & 31u, 3);
+                        const uint32_t at = R0.z;                   // the first 4 exceptions' blocks
+                        if (ne > 0) patch(at & 31u, 0);
+                        if (ne > 1) patch((at >> 8) & 31u, 1);
+                        if (ne > 2) patch((at >> 16) & 31u, 2);
+                        if (ne > 3) patch((at >> 24) & 31u, 3);
                     } else {                                       // (rare) from the codes' flags, in LDS
-                        const uint16_t *cw = (const uint16_t *)&L.TC[b][0][tid];
                         for (uint32_t i = 0; i < (uint32_t)CSR_SB; i++) {
-                            const uint32_t c = ((const uint16_t *)&L.TC[b][i >> 3][tid])[i & 7u];
+                            const uint32_t c = ((const uint16_t *)&L.TC[k][i >> 3][tid])[i & 7u];
                             if (c & CSR_EXC) patch(i, c & 0x7FFFu);
                         }
-                        (void)cw;
                     }
                     auto putx = [&](uint32_t e, const u32x4 &x, const u32x2 &y) {
-                        *(u32x4 *)&L.EA[b][e] = x;
-                        *(u32x2 *)&L.EB[b][e] = y;
+                        *(u32x4 *)&L.EA[e] = x;
+                        *(u32x2 *)&L.EB[e] = y;
                     };
                     if (ne > 0) putx(xb + 0, EA0, EB0);
                     if (ne > 1) putx(xb + 1, EA1, EB1);
                     if (ne > 2) putx(xb + 2, EA2, EB2);
                     if (ne > 3) putx(xb + 3, EA3, EB3);
-                    for (uint32_t k = CSR_EREG; k < ne; k++) {      // more than CSR_EREG: synchronous loads (rare)
-                        const uint4 *ep = ent + 2 * (ecur + k);
-                        putx(xb + k, *(const u32x4 *)ep, *(const u32x2 *)(ep + 1));
+                    for (uint32_t j = CSR_EREG; j < ne; j++) {      // more than CSR_EREG: synchronous loads (rare)
+                        const uint4 *ep = ent + 2 * (ecur + j);
+                        putx(xb + j, *(const u32x4 *)ep, *(const u32x2 *)(ep + 1));
                     }
                 }
                 s = (int32_t)R0.y;
@@ -423,16 +424,17 @@ __device__ __forceinline__ void c3_stage(const DS &d, const uint32_t *list, uint
         }
         if (!has) {
             const uint32_t want = r.live ? base : 0xFFFFFFFDu;      // (rows not hashed read entry 0)
-            if (tag[b] != want) {
-                const uint32_t c0 = r.live ? base * CSR_ESZ : 0u, st1 = r.live ? p.nph * CSR_ESZ : 0u, st2 = 2u * st1;
+            if (tag_ref(KC) != want) {
+                const uint32_t c0 = r.live ? base * CSR_ESZ : 0u;
+                const uint32_t st1 = r.live ? p.nph * CSR_ESZ : 0u, st2 = 2u * st1;
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
                     const uint32_t c = c0 + (uint32_t)(4 * q) * st2;
-                    L.TC[b][q][tid] = make_uint4(c | ((c + st1) << 16), (c + st2) | ((c + st2 + st1) << 16),
+                    L.TC[k][q][tid] = make_uint4(c | ((c + st1) << 16), (c + st2) | ((c + st2 + st1) << 16),
                                                  (c + 2 * st2) | ((c + 2 * st2 + st1) << 16),
                                                  (c + 3 * st2) | ((c + 3 * st2 + st1) << 16));
                 }
-                tag[b] = want;
+                tag_ref(KC) = want;
             }
         }
         const bool adv = has;
@@ -456,18 +458,19 @@ __device__ __forceinline__ void c3_stage(const DS &d, const uint32_t *list, uint
 #define C3S_STAMP(v)
 #define C3S_ACC(k, x)
 #endif
-    auto step = [&](uint32_t u, auto BC) {
+    auto step = [&](uint32_t u, auto BC, auto KC) {
         constexpr uint32_t b = decltype(BC)::value;
         C3S_STAMP(s0);
-        if (u >= 2) c3_wait(&L.doner[rwave][b], 2u * (u >> 1));   // this group's chains are done with super step u - 2
+        if (u >= 3) c3_wait(&L.doner[rwave], 2u * (u - 2u));      // this group's chains are done with super step u - 3
         C3S_STAMP(s1);
 #ifdef CSR_DIAG_STAMP
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");            // (diagnostics: slot 1 = the record loads' wait)
 #endif
         C3S_STAMP(s2);
-        prep(u, b);
+        prep(u, b, KC);
+        e3 = e2; e2 = e1; e1 = alloc;
         C3S_STAMP(s3);
-        c3_signal(&L.readyr[rwave][b]);
+        c3_signal(&L.readyr[rwave]);
         C3S_STAMP(s4);
         C3S_ACC(0, s1 - s0);
 #ifndef CSR_DIAG_WINDOW
@@ -478,12 +481,22 @@ __device__ __forceinline__ void c3_stage(const DS &d, const uint32_t *list, uint
         C3S_ACC(3, s4 - s3);
 #endif
     };
-    uint32_t u = 0;
-    for (; u + 1 < T_; u += 2) {
-        step(u, std::integral_constant<uint32_t, 0>{});
-        step(u + 1, std::integral_constant<uint32_t, 1>{});
+    using I0 = std::integral_constant<uint32_t, 0>;
+    using I1 = std::integral_constant<uint32_t, 1>;
+    using I2 = std::integral_constant<uint32_t, 2>;
+    for (uint32_t u = 0; u < T_; u += 6) {                          // (super step u + j: window buffer j & 1, codes j % 3)
+        step(u, I0{}, I0{});
+        if (u + 1 >= T_) break;
+        step(u + 1, I1{}, I1{});
+        if (u + 2 >= T_) break;
+        step(u + 2, I0{}, I2{});
+        if (u + 3 >= T_) break;
+        step(u + 3, I1{}, I0{});
+        if (u + 4 >= T_) break;
+        step(u + 4, I0{}, I1{});
+        if (u + 5 >= T_) break;
+        step(u + 5, I1{}, I2{});
     }
-    if (u < T_) step(u, std::integral_constant<uint32_t, 0>{});
 #ifdef CSR_DIAG_STAMP
     if ((threadIdx.x & 63u) == 0)
         for (int k = 0; k < 4; k++) ctr_add(d, C_NALL + 4 + k, (unsigned long long)st_[k]);
@@ -536,9 +549,9 @@ __device__ __forceinline__ void c3_wstage(const CsrArgs &a, const CsrPlan &p, Cs
 #pragma unroll
         for (int v = 0; v < WV; v++) {
             const uint32_t u = tid + (uint32_t)CSR_ROWS * v;
-            if (u < nwin) {                                        // (the tail holds overflow exception entries)
-                *(u32x4 *)&L.EA[b][u] = w0[v];
-                *(u32x2 *)&L.EB[b][u] = w1[v];
+            if (u < nwin) {
+                *(u32x4 *)&L.EA[b * CSR_WINMAX + u] = w0[v];
+                *(u32x2 *)&L.EB[b * CSR_WINMAX + u] = w1[v];
             }
         }
     };
@@ -592,16 +605,22 @@ __device__ __forceinline__ void c3_chain(const DS &d, const uint32_t *list, uint
 #endif
     C3_STAMP(tl0);
     uint32_t code[CSR_SB];
+    uint32_t k3 = 0;                                                 // code buffer of super step t: t % 3
+    uint32_t pr = 0, pw = 0;                                         // the hand-over counters, as last read
     auto step = [&](uint32_t t, auto BC) {
         constexpr uint32_t b = decltype(BC)::value;
         const uint32_t K0 = t * CSR_SB;
         C3_STAMP(ta);
-        c3_wait(&L.readyr[grp][b], (t >> 1) + 1u);                // this group's record stager has filled super step t
-        c3_wait(&L.readyw[b], 4u * ((t >> 1) + 1u));              // and the window stagers
+        // this group's record stager has staged super step t, and the window stagers its window: the counters were
+        // read during the last super step's chain (an LDS round trip per read, 10 % of a light round's loop when
+        // read here); only when they were short is there a wait, then an acquire fence for what they hand over
+        if (pr < t + 1u) c3_wait(&L.readyr[grp], t + 1u);
+        if (pw < 4u * ((t >> 1) + 1u)) c3_wait(&L.readyw[b], 4u * ((t >> 1) + 1u));
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         C3_STAMP(tb);
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            const uint4 v = L.TC[b][q][tid];
+            const uint4 v = L.TC[k3][q][tid];
             const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
             for (int j = 0; j < 4; j++) {
@@ -610,8 +629,10 @@ __device__ __forceinline__ void c3_chain(const DS &d, const uint32_t *list, uint
             }
         }
         C3_STAMP(tc);
+        pr = __hip_atomic_load(&L.readyr[grp], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        pw = __hip_atomic_load(&L.readyw[b ^ 1u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         const bool full = __all(myit == 0u || K0 + CSR_SB <= myit);
-        const char *Eb = GF ? (const char *)L.EA[b] : (const char *)L.EB[b];
+        const char *Eb = GF ? (const char *)(L.EA + b * CSR_WINMAX) : (const char *)(L.EB + b * CSR_WINMAX);
         auto run = [&](auto FULLC) {
             constexpr bool FULL = decltype(FULLC)::value;
             EV va[CSR_PF + 1];
@@ -637,7 +658,8 @@ __device__ __forceinline__ void c3_chain(const DS &d, const uint32_t *list, uint
         if (full) run(std::integral_constant<bool, true>{});
         else run(std::integral_constant<bool, false>{});
         c3_signal(&L.done[b]);
-        c3_signal(&L.doner[grp][b]);
+        c3_signal(&L.doner[grp]);
+        k3 = k3 == 2u ? 0u : k3 + 1u;
         C3_STAMP(td);
         C3_ACC(0, td - tc);
         C3_ACC(1, tb - ta);
@@ -693,8 +715,8 @@ __global__ void __launch_bounds__(4 * CSR_ROWS) k_csr3(DS d, const uint32_t *lis
     if (blockIdx.x * CSR_ROWS >= cnt) return;
     const CsrPlan p = a.plan[blockIdx.x];
     if (threadIdx.x < 20 && ((p.phm >> threadIdx.x) & 1u)) L.phs[__popc(p.phm & ((1u << threadIdx.x) - 1u))] = threadIdx.x;
-    if (threadIdx.x < 2) { L.readyw[threadIdx.x] = 0; L.done[threadIdx.x] = 0; L.ovf[threadIdx.x] = 0xFFFF0000u; }
-    if (threadIdx.x < 8) { (&L.readyr[0][0])[threadIdx.x] = 0; (&L.doner[0][0])[threadIdx.x] = 0; }
+    if (threadIdx.x < 2) { L.readyw[threadIdx.x] = 0; L.done[threadIdx.x] = 0; }
+    if (threadIdx.x < 4) { L.readyr[threadIdx.x] = 0; L.doner[threadIdx.x] = 0; }
     __syncthreads();
     const uint32_t T_ = p.feasible ? (p.maxit + CSR_SB - 1) / CSR_SB : 0u;
     const uint32_t role = threadIdx.x / CSR_ROWS;
