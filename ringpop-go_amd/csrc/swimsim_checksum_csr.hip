@@ -66,8 +66,8 @@ struct CsrArgs {
     uint32_t *nrec;        // [rows]
     uint32_t rcap;
     uint32_t *fb_list, *fb_cnt;   // rows left to the production kernels
-    uint32_t exw;                 // k_csr3: entries of a row group's exception ring, a power of two (C3_RING; tests
-                                  // lower it to 8, swimsim_tuning.fault_inject bit 4)
+    uint32_t exw;                 // k_csr3: cap on a row group's exception ring entries (~0; tests lower it to 8,
+                                  // swimsim_tuning.fault_inject bit 4)
 };
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -252,9 +252,9 @@ __global__ void __launch_bounds__(256) k_csr_rec(DS d, const uint32_t *list, uin
 // waves 0-3 g/f lanes, 4-7 h lanes, 8-11 record stagers, 12-15 window stagers; waves w, w + 4, w + 8 and w + 12 share
 // a SIMD and rows 64 w .. 64 w + 63.
 // ---------------------------------------------------------------------------------------------------------------
-constexpr int C3_RING = 512;                       // exception ring entries per row group (a power of two)
-constexpr int C3_ENT = 2 * CSR_WINMAX + 4 * C3_RING;   // 4,096 entries: byte offsets fit the u16 codes
-constexpr int C3_TCB = 3;                          // code table buffers
+constexpr int C3_NB = 3;                           // window and code table buffers (super step t: buffer t % 3)
+constexpr int C3_ENT = 4096;               // entries: 3 windows of nwin entries, then 4 rings share the rest
+static_assert(C3_NB * CSR_WINMAX + 4 * 256 <= C3_ENT, "rings of at least 256 entries");
 static_assert(C3_ENT * CSR_ESZ <= 65536, "codes are u16 byte offsets");
 
 struct Csr3Lds {
@@ -262,10 +262,10 @@ struct Csr3Lds {
     // with EB at 64 KB every h-lane read took a v_or of its base)
     uint2 EB[C3_ENT];                      // {Mh, KH} per entry: window buffers 0 and 1, then the rings
     uint4 EA[C3_ENT];                      // {Mg, D, Mf, PF}
-    uint4 TC[C3_TCB][4][CSR_ROWS];         // codes: TC[k][q][row] = u16 codes 8q .. 8q + 7 of the row (lane-contiguous)
+    uint4 TC[C3_NB][4][CSR_ROWS];         // codes: TC[k][q][row] = u16 codes 8q .. 8q + 7 of the row (lane-contiguous)
     uint32_t XH[CSR_ROWS];                 // h lanes' final state
     uint32_t FLX[CSR_ROWS];                // rows the stagers flagged (exception slots)
-    uint32_t readyw[2], done[2];           // window stagers that filled buffer b (4 a super step); chains done with it (8)
+    uint32_t readyw[C3_NB], done[C3_NB];   // window stagers that filled buffer b (4 a super step); chains done with it (8)
     uint32_t readyr[4], doner[4];          // per row group: super steps staged by its record stager; its chains' steps
     uint32_t phs[20];
 };
@@ -333,12 +333,12 @@ __device__ __forceinline__ void c3_stage(const DS &d, const uint32_t *list, uint
     uint32_t base = csr_base(p, 0);
     // what TC[k][.][row] holds: base codes (base), or a record (~0)
     uint32_t tg0 = 0xFFFFFFFEu, tg1 = 0xFFFFFFFEu, tg2 = 0xFFFFFFFEu;
-    // the group's ring (a.exw entries, a power of two): alloc counts the entries handed out (monotone), e1 .. e3 what it
-    // was after super steps u - 1 .. u - 3
-    const uint32_t R = a.exw, ring0 = 2u * CSR_WINMAX + rwave * (uint32_t)C3_RING;
-    uint32_t alloc = 0, e1 = 0, e2 = 0, e3 = 0;
-    // (k is a compile-time constant: the loop is unrolled by 6 = window buffers x code buffers, so the tags stay in
-    // registers)
+    // the group's ring: the entries past the three windows (nwin each), a quarter each; alloc counts the entries handed
+    // out (monotone), e1 .. e3 what it was after super steps u - 1 .. u - 3, rpos the next free one
+    const uint32_t nwin = p.nph * p.Wn, Rf = ((uint32_t)C3_ENT - C3_NB * nwin) / 4u, R = min(Rf, a.exw);
+    const uint32_t ring0 = C3_NB * nwin + rwave * Rf;
+    uint32_t alloc = 0, e1 = 0, e2 = 0, e3 = 0, rpos = 0;
+    // (k is a compile-time constant: the loop is unrolled by the 3 buffers, so the tags stay in registers)
     auto tag_ref = [&](auto KC) -> uint32_t & {
         constexpr uint32_t k = decltype(KC)::value;
         if constexpr (k == 0) return tg0;
@@ -372,22 +372,32 @@ __device__ __forceinline__ void c3_stage(const DS &d, const uint32_t *list, uint
             const bool over = has && ne > 0 && sb + ne > R;
             const uint32_t need = tot > R ? wmin(over ? sb : 0xFFFFFFFFu) : tot;
             if (over) r.fl |= CSR_F_SLOTS;
-            const uint32_t pos = alloc & (R - 1u), skip = pos + need > R ? R - pos : 0u;
+            const uint32_t skip = rpos + need > R ? R - rpos : 0u;
             // the slots of super steps t - 2 and t - 1 may still be read (those of t - 3 are free: the step's wait)
             if (alloc + skip + need - e3 > R) {
                 if (t >= 2) c3_wait(&L.doner[rwave], 2u * (t - 1u));
                 if (alloc + skip + need - e2 > R && t >= 1) c3_wait(&L.doner[rwave], 2u * t);
             }
-            const uint32_t xb = ring0 + ((alloc + skip) & (R - 1u)) + sb;
+            const uint32_t xb = ring0 + (skip ? 0u : rpos) + sb;
             alloc += skip + need;
+            rpos = (skip ? 0u : rpos) + need;
+            if (rpos >= R) rpos = 0;
             if (has) {
-                L.TC[k][0][tid] = make_uint4(R1.x, R1.y, R1.z, R1.w);
-                L.TC[k][1][tid] = make_uint4(R2.x, R2.y, R2.z, R2.w);
-                L.TC[k][2][tid] = make_uint4(R3.x, R3.y, R3.z, R3.w);
-                L.TC[k][3][tid] = make_uint4(R4.x, R4.y, R4.z, R4.w);
+                // the record's window codes are window-relative: + window buffer k (halfword adds; exception codes are
+                // patched below)
+                const uint32_t wk = k * nwin * CSR_ESZ;
+                auto pk = [&](uint32_t w) {
+                    typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+                    const us2 r2 = __builtin_bit_cast(us2, w) + us2{(unsigned short)wk, (unsigned short)wk};
+                    return __builtin_bit_cast(uint32_t, r2);
+                };
+                L.TC[k][0][tid] = make_uint4(pk(R1.x), pk(R1.y), pk(R1.z), pk(R1.w));
+                L.TC[k][1][tid] = make_uint4(pk(R2.x), pk(R2.y), pk(R2.z), pk(R2.w));
+                L.TC[k][2][tid] = make_uint4(pk(R3.x), pk(R3.y), pk(R3.z), pk(R3.w));
+                L.TC[k][3][tid] = make_uint4(pk(R4.x), pk(R4.y), pk(R4.z), pk(R4.w));
                 tag_ref(KC) = 0xFFFFFFFFu;
                 if (!(r.fl & CSR_F_SLOTS)) {
-                    const uint32_t xa = (xb - b * (uint32_t)CSR_WINMAX) * CSR_ESZ;   // (relative to window buffer b)
+                    const uint32_t xa = xb * CSR_ESZ;
                     // exception codes -> the ring's slots (u16 stores into the row's codes): block i lives in
                     // TC[k][i / 8][row], halfword i % 8
                     auto patch = [&](uint32_t i, uint32_t ord) {
@@ -400,11 +410,13 @@ __device__ __forceinline__ void c3_stage(const DS &d, const uint32_t *list, uint
                         if (ne > 1) patch((at >> 8) & 31u, 1);
                         if (ne > 2) patch((at >> 16) & 31u, 2);
                         if (ne > 3) patch((at >> 24) & 31u, 3);
-                    } else {                                       // (rare) from the codes' flags, in LDS
-                        for (uint32_t i = 0; i < (uint32_t)CSR_SB; i++) {
-                            const uint32_t c = ((const uint16_t *)&L.TC[k][i >> 3][tid])[i & 7u];
-                            if (c & CSR_EXC) patch(i, c & 0x7FFFu);
-                        }
+                    } else {                                       // (rare) from the record codes' flag bits
+                        const uint32_t rw[16] = {R1.x, R1.y, R1.z, R1.w, R2.x, R2.y, R2.z, R2.w,
+                                                 R3.x, R3.y, R3.z, R3.w, R4.x, R4.y, R4.z, R4.w};
+                        uint32_t m = 0;                            // blocks that are exceptions (ordinals in block order)
+#pragma unroll
+                        for (int i = 0; i < 16; i++) m |= ((rw[i] >> 15) & 1u) << (2 * i) | (rw[i] >> 31) << (2 * i + 1);
+                        for (uint32_t ord = 0; m; ord++, m &= m - 1u) patch((uint32_t)__builtin_ctz(m), ord);
                     }
                     auto putx = [&](uint32_t e, const u32x4 &x, const u32x2 &y) {
                         *(u32x4 *)&L.EA[e] = x;
@@ -425,7 +437,7 @@ __device__ __forceinline__ void c3_stage(const DS &d, const uint32_t *list, uint
         if (!has) {
             const uint32_t want = r.live ? base : 0xFFFFFFFDu;      // (rows not hashed read entry 0)
             if (tag_ref(KC) != want) {
-                const uint32_t c0 = r.live ? base * CSR_ESZ : 0u;
+                const uint32_t c0 = r.live ? (k * nwin + base) * CSR_ESZ : 0u;
                 const uint32_t st1 = r.live ? p.nph * CSR_ESZ : 0u, st2 = 2u * st1;
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
@@ -484,18 +496,12 @@ __device__ __forceinline__ void c3_stage(const DS &d, const uint32_t *list, uint
     using I0 = std::integral_constant<uint32_t, 0>;
     using I1 = std::integral_constant<uint32_t, 1>;
     using I2 = std::integral_constant<uint32_t, 2>;
-    for (uint32_t u = 0; u < T_; u += 6) {                          // (super step u + j: window buffer j & 1, codes j % 3)
+    for (uint32_t u = 0; u < T_; u += 3) {                          // (super step u + j: buffers j)
         step(u, I0{}, I0{});
         if (u + 1 >= T_) break;
         step(u + 1, I1{}, I1{});
         if (u + 2 >= T_) break;
-        step(u + 2, I0{}, I2{});
-        if (u + 3 >= T_) break;
-        step(u + 3, I1{}, I0{});
-        if (u + 4 >= T_) break;
-        step(u + 4, I0{}, I1{});
-        if (u + 5 >= T_) break;
-        step(u + 5, I1{}, I2{});
+        step(u + 2, I2{}, I2{});
     }
 #ifdef CSR_DIAG_STAMP
     if ((threadIdx.x & 63u) == 0)
@@ -511,7 +517,7 @@ __device__ __forceinline__ void c3_stage(const DS &d, const uint32_t *list, uint
 }
 
 // the window stager (role 3): a quarter of every super step's window, entries u = tid + 256 v (both halves), from
-// two register sets (super step u -> set u & 1) loaded two super steps ahead. A wave of its own since round 5's
+// three register sets (super step u -> set u % 3) loaded three super steps ahead. A wave of its own since round 5's
 // stamps: in the record stager's loop the window took 34-43 % of the chain waves' loop, and the chains waited for it.
 __device__ __forceinline__ void c3_wstage(const CsrArgs &a, const CsrPlan &p, Csr3Lds &L, uint32_t T_) {
     const uint32_t tid = threadIdx.x & (CSR_ROWS - 1);
@@ -520,8 +526,8 @@ __device__ __forceinline__ void c3_wstage(const CsrArgs &a, const CsrPlan &p, Cs
 #endif
     // window: entries u = tid + 256 v (both halves), two register sets (super step u -> set u & 1), loaded two ahead
     constexpr int WV = CSR_WINMAX / CSR_ROWS;
-    u32x4 wA0[WV], wB0[WV];
-    u32x2 wA1[WV], wB1[WV];
+    u32x4 wA0[WV], wB0[WV], wC0[WV];
+    u32x2 wA1[WV], wB1[WV], wC1[WV];
     const uint32_t nwin = p.nph * p.Wn;
     uint32_t wsrc[WV];                                               // (phase rows of P as entry offsets: 32-bit)
     int32_t wk0[WV];
@@ -550,26 +556,30 @@ __device__ __forceinline__ void c3_wstage(const CsrArgs &a, const CsrPlan &p, Cs
         for (int v = 0; v < WV; v++) {
             const uint32_t u = tid + (uint32_t)CSR_ROWS * v;
             if (u < nwin) {
-                *(u32x4 *)&L.EA[b * CSR_WINMAX + u] = w0[v];
-                *(u32x2 *)&L.EB[b * CSR_WINMAX + u] = w1[v];
+                *(u32x4 *)&L.EA[b * nwin + u] = w0[v];
+                *(u32x2 *)&L.EB[b * nwin + u] = w1[v];
             }
         }
     };
     wload(wA0, wA1, 0);
     wload(wB0, wB1, 1);
-    auto step = [&](uint32_t u, auto BC) {
+    wload(wC0, wC1, 2);
+    // super step u = 3 j + b: register set and buffer b, loaded three super steps ahead
+    auto step = [&](uint32_t u, uint32_t j, auto BC) {
         constexpr uint32_t b = decltype(BC)::value;
-        if (u >= 2) c3_wait(&L.done[b], 8u * (u >> 1));           // every chain is done with super step u - 2
-        if constexpr (b) { wstore(wB0, wB1, 1u); wload(wB0, wB1, u + 2); }
-        else { wstore(wA0, wA1, 0u); wload(wA0, wA1, u + 2); }
+        if (j > 0) c3_wait(&L.done[b], 8u * j);                     // every chain is done with super step u - 3
+        if constexpr (b == 0) { wstore(wA0, wA1, 0u); wload(wA0, wA1, u + 3); }
+        else if constexpr (b == 1) { wstore(wB0, wB1, 1u); wload(wB0, wB1, u + 3); }
+        else { wstore(wC0, wC1, 2u); wload(wC0, wC1, u + 3); }
         c3_signal(&L.readyw[b]);
     };
-    uint32_t u = 0;
-    for (; u + 1 < T_; u += 2) {
-        step(u, std::integral_constant<uint32_t, 0>{});
-        step(u + 1, std::integral_constant<uint32_t, 1>{});
+    for (uint32_t u = 0, j = 0; u < T_; u += 3, j++) {
+        step(u, j, std::integral_constant<uint32_t, 0>{});
+        if (u + 1 >= T_) break;
+        step(u + 1, j, std::integral_constant<uint32_t, 1>{});
+        if (u + 2 >= T_) break;
+        step(u + 2, j, std::integral_constant<uint32_t, 2>{});
     }
-    if (u < T_) step(u, std::integral_constant<uint32_t, 0>{});
 }
 
 template <int W, int ROLE>                                          // ROLE 0: g/f lanes, 1: h lanes
@@ -605,9 +615,9 @@ __device__ __forceinline__ void c3_chain(const DS &d, const uint32_t *list, uint
 #endif
     C3_STAMP(tl0);
     uint32_t code[CSR_SB];
-    uint32_t k3 = 0;                                                 // code buffer of super step t: t % 3
     uint32_t pr = 0, pw = 0;                                         // the hand-over counters, as last read
-    auto step = [&](uint32_t t, auto BC) {
+    // super step t = 3 j + b: window and code buffer b
+    auto step = [&](uint32_t t, uint32_t j, auto BC) {
         constexpr uint32_t b = decltype(BC)::value;
         const uint32_t K0 = t * CSR_SB;
         C3_STAMP(ta);
@@ -615,12 +625,15 @@ __device__ __forceinline__ void c3_chain(const DS &d, const uint32_t *list, uint
         // read during the last super step's chain (an LDS round trip per read, 10 % of a light round's loop when
         // read here); only when they were short is there a wait, then an acquire fence for what they hand over
         if (pr < t + 1u) c3_wait(&L.readyr[grp], t + 1u);
-        if (pw < 4u * ((t >> 1) + 1u)) c3_wait(&L.readyw[b], 4u * ((t >> 1) + 1u));
+#ifdef CSR_DIAG_SPLITWAIT
+        C3_STAMP(tw);                                               // (diagnostics: slot 2 = the window's wait)
+#endif
+        if (pw < 4u * (j + 1u)) c3_wait(&L.readyw[b], 4u * (j + 1u));
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         C3_STAMP(tb);
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            const uint4 v = L.TC[k3][q][tid];
+            const uint4 v = L.TC[b][q][tid];
             const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
             for (int j = 0; j < 4; j++) {
@@ -630,9 +643,9 @@ __device__ __forceinline__ void c3_chain(const DS &d, const uint32_t *list, uint
         }
         C3_STAMP(tc);
         pr = __hip_atomic_load(&L.readyr[grp], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        pw = __hip_atomic_load(&L.readyw[b ^ 1u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        pw = __hip_atomic_load(&L.readyw[b == 2u ? 0u : b + 1u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         const bool full = __all(myit == 0u || K0 + CSR_SB <= myit);
-        const char *Eb = GF ? (const char *)(L.EA + b * CSR_WINMAX) : (const char *)(L.EB + b * CSR_WINMAX);
+        const char *Eb = GF ? (const char *)L.EA : (const char *)L.EB;
         auto run = [&](auto FULLC) {
             constexpr bool FULL = decltype(FULLC)::value;
             EV va[CSR_PF + 1];
@@ -659,20 +672,25 @@ __device__ __forceinline__ void c3_chain(const DS &d, const uint32_t *list, uint
         else run(std::integral_constant<bool, false>{});
         c3_signal(&L.done[b]);
         c3_signal(&L.doner[grp]);
-        k3 = k3 == 2u ? 0u : k3 + 1u;
         C3_STAMP(td);
         C3_ACC(0, td - tc);
+#ifdef CSR_DIAG_SPLITWAIT
+        C3_ACC(1, tw - ta);
+        C3_ACC(2, tb - tw);
+#else
         C3_ACC(1, tb - ta);
-#ifndef CSR_DIAG_WINDOW
+#endif
+#if !defined(CSR_DIAG_WINDOW) && !defined(CSR_DIAG_SPLITWAIT)
         C3_ACC(2, tc - tb);
 #endif
     };
-    uint32_t t = 0;
-    for (; t + 1 < T_; t += 2) {
-        step(t, std::integral_constant<uint32_t, 0>{});
-        step(t + 1, std::integral_constant<uint32_t, 1>{});
+    for (uint32_t t = 0, j = 0; t < T_; t += 3, j++) {
+        step(t, j, std::integral_constant<uint32_t, 0>{});
+        if (t + 1 >= T_) break;
+        step(t + 1, j, std::integral_constant<uint32_t, 1>{});
+        if (t + 2 >= T_) break;
+        step(t + 2, j, std::integral_constant<uint32_t, 2>{});
     }
-    if (t < T_) step(t, std::integral_constant<uint32_t, 0>{});
     C3_STAMP(tl1);
     C3_ACC(3, tl1 - tl0);
 #ifdef CSR_DIAG_STAMP
@@ -715,7 +733,7 @@ __global__ void __launch_bounds__(4 * CSR_ROWS) k_csr3(DS d, const uint32_t *lis
     if (blockIdx.x * CSR_ROWS >= cnt) return;
     const CsrPlan p = a.plan[blockIdx.x];
     if (threadIdx.x < 20 && ((p.phm >> threadIdx.x) & 1u)) L.phs[__popc(p.phm & ((1u << threadIdx.x) - 1u))] = threadIdx.x;
-    if (threadIdx.x < 2) { L.readyw[threadIdx.x] = 0; L.done[threadIdx.x] = 0; }
+    if (threadIdx.x < C3_NB) { L.readyw[threadIdx.x] = 0; L.done[threadIdx.x] = 0; }
     if (threadIdx.x < 4) { L.readyr[threadIdx.x] = 0; L.doner[threadIdx.x] = 0; }
     __syncthreads();
     const uint32_t T_ = p.feasible ? (p.maxit + CSR_SB - 1) / CSR_SB : 0u;
