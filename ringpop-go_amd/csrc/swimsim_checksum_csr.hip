@@ -14,17 +14,18 @@
 //   k_csr_plan    per workgroup of CSR_ROWS listed rows: the shift range and phases of its clean blocks -> the LDS
 //                 window geometry (Wn positions per phase), or "infeasible" (the workgroup's rows fall back)
 //   k_csr_rec     per row: one record per super step (CSR_SB blocks) that holds exception blocks: the super step's
-//                 32 codes (u16: a clean block's window entry as an LDS byte address, CSR_EXC | ordinal for an
-//                 exception block), the shift after it and where its first exceptions are
-//   k_csr3        the chains (below): 256 rows per workgroup, three waves per SIMD (the rows' g/f lanes, their h lanes,
-//                 and a stager that fills the next super step's window, codes and exception entries), handed over
+//                 32 codes (u16: a clean block's window entry as an LDS byte address), the shift after it and the
+//                 mask of its exception blocks
+//   k_csr3        the chains (below): 256 rows per workgroup, four waves per SIMD (the rows' g/f lanes, their h lanes,
+//                 a record stager that fills their codes and exception entries and a window stager), handed over
 //                 through LDS counters
-// Rows the path cannot take (scan flags, an infeasible window, a super step with more exception entries than the
-// slots) are listed and hashed by the production kernels (k_checksum3 / k_checksum_q16): bit-exact either way.
+// Rows the path cannot take (scan flags, an infeasible window, a super step with more exception entries than a
+// ring) are listed and hashed by the production kernels (k_checksum3 / k_checksum_q16): bit-exact either way.
 
 constexpr int CSR_ROWS = 256;          // rows per workgroup (4 row groups of 64)
 constexpr int CSR_SB = 32;             // blocks per super step
 constexpr int CSR_WINMAX = 1024;       // window entries per buffer: phases in use x Wn
+constexpr int C3_NB = 3;               // k_csr3's window and code table buffers (super step t: buffer t % 3)
 constexpr uint32_t CSR_ESZ = 16;       // a code's unit: an entry's byte offset in each of the two entry arrays
 constexpr int CSR_EREG = 4;            // exception entries of a record prefetched with it
 #ifndef CSR_PF_DEF
@@ -32,7 +33,6 @@ constexpr int CSR_EREG = 4;            // exception entries of a record prefetch
 #endif
 constexpr int CSR_PF = CSR_PF_DEF;     // blocks the chain's LDS reads run ahead of its arithmetic (6: 7.37 / 11.52 ms
                                        // on rounds 14 / 18 against 7.48 / 11.69 with 4 and 8.00 / 12.00 with 2)
-constexpr uint32_t CSR_EXC = 0x8000u;  // code flag: exception entry (low bits: ordinal in the super step)
 constexpr uint32_t CSR_F_PLAN = 128, CSR_F_SLOTS = 256, CSR_F_RCAP = 512;   // flags beyond k_csd_scan's
 
 struct CsrPlan {
@@ -50,9 +50,9 @@ struct CsrPlan {
 struct __attribute__((aligned(16))) CsrRec {
     uint32_t t;            // super step
     int32_t s_end;         // the row's shift after the super step
-    uint32_t pos4, ne;     // the blocks (bytes 0-3) of its first exception entries (ne <= 4), their number
+    uint32_t xmask, ne;    // its exception blocks (bit i: block i; their entries in block order), their number
     uint32_t code[16];     // 32 u16 codes, block i in the low half of code[i / 2] for even i: the byte address of a
-                           // clean block's window entry, CSR_EXC | ordinal for an exception block
+                           // clean block's entry in k_csr3's window buffer t % 3 (0 for an exception block)
 };
 
 struct CsrArgs {
@@ -192,26 +192,26 @@ __global__ void __launch_bounds__(256) k_csr_rec(DS d, const uint32_t *list, uin
                     CsrRec r;
                     int32_t s = lane ? (int32_t)hd[wv][lane - 1].y : s_prev;
                     const uint32_t K0 = t * CSR_SB;
+                    const uint32_t wbase = (t % C3_NB) * p.nph * p.Wn;     // (k_csr3's window buffer t % 3)
                     uint32_t q = lane, kn = h.x, pos = 0;
                     for (uint32_t b = 0; b < (uint32_t)CSR_SB; b++) {
                         const uint32_t j = K0 + b;
                         uint32_t c;
                         if (q < gend && kn == j) {
-                            const uint32_t o = q - lane;
-                            c = CSR_EXC | o;
-                            if (o < 4) pos |= b << (8 * o);
+                            c = 0;
+                            pos |= 1u << b;
                             s = (int32_t)hd[wv][q].y;
                             q++;
                             kn = q < gend ? hd[wv][q].x : 0xFFFFFFFFu;
                         } else {
-                            c = j < iters ? (csr_base(p, s) + b * p.nph) * CSR_ESZ : 0u;
+                            c = j < iters ? (wbase + csr_base(p, s) + b * p.nph) * CSR_ESZ : 0u;
                         }
                         if (b & 1u) r.code[b >> 1] |= c << 16;
                         else r.code[b >> 1] = c;
                     }
                     r.t = t;
                     r.s_end = s;
-                    r.pos4 = pos;
+                    r.xmask = pos;
                     r.ne = gend - lane;
                     rec[slot] = r;
                 }
@@ -252,7 +252,6 @@ __global__ void __launch_bounds__(256) k_csr_rec(DS d, const uint32_t *list, uin
 // waves 0-3 g/f lanes, 4-7 h lanes, 8-11 record stagers, 12-15 window stagers; waves w, w + 4, w + 8 and w + 12 share
 // a SIMD and rows 64 w .. 64 w + 63.
 // ---------------------------------------------------------------------------------------------------------------
-constexpr int C3_NB = 3;                           // window and code table buffers (super step t: buffer t % 3)
 constexpr int C3_ENT = 4096;               // entries: 3 windows of nwin entries, then 4 rings share the rest
 static_assert(C3_NB * CSR_WINMAX + 4 * 256 <= C3_ENT, "rings of at least 256 entries");
 static_assert(C3_ENT * CSR_ESZ <= 65536, "codes are u16 byte offsets");
@@ -383,18 +382,11 @@ __device__ __forceinline__ void c3_stage(const DS &d, const uint32_t *list, uint
             rpos = (skip ? 0u : rpos) + need;
             if (rpos >= R) rpos = 0;
             if (has) {
-                // the record's window codes are window-relative: + window buffer k (halfword adds; exception codes are
-                // patched below)
-                const uint32_t wk = k * nwin * CSR_ESZ;
-                auto pk = [&](uint32_t w) {
-                    typedef unsigned short us2 __attribute__((ext_vector_type(2)));
-                    const us2 r2 = __builtin_bit_cast(us2, w) + us2{(unsigned short)wk, (unsigned short)wk};
-                    return __builtin_bit_cast(uint32_t, r2);
-                };
-                L.TC[k][0][tid] = make_uint4(pk(R1.x), pk(R1.y), pk(R1.z), pk(R1.w));
-                L.TC[k][1][tid] = make_uint4(pk(R2.x), pk(R2.y), pk(R2.z), pk(R2.w));
-                L.TC[k][2][tid] = make_uint4(pk(R3.x), pk(R3.y), pk(R3.z), pk(R3.w));
-                L.TC[k][3][tid] = make_uint4(pk(R4.x), pk(R4.y), pk(R4.z), pk(R4.w));
+                // (the record's codes address window buffer t % 3 = k already; its exception blocks are patched below)
+                L.TC[k][0][tid] = make_uint4(R1.x, R1.y, R1.z, R1.w);
+                L.TC[k][1][tid] = make_uint4(R2.x, R2.y, R2.z, R2.w);
+                L.TC[k][2][tid] = make_uint4(R3.x, R3.y, R3.z, R3.w);
+                L.TC[k][3][tid] = make_uint4(R4.x, R4.y, R4.z, R4.w);
                 tag_ref(KC) = 0xFFFFFFFFu;
                 if (!(r.fl & CSR_F_SLOTS)) {
                     const uint32_t xa = xb * CSR_ESZ;
@@ -404,20 +396,12 @@ __device__ __forceinline__ void c3_stage(const DS &d, const uint32_t *list, uint
                         uint16_t *c16 = (uint16_t *)&L.TC[k][i >> 3][tid] + (i & 7u);
                         *c16 = (uint16_t)(xa + ord * CSR_ESZ);
                     };
-                    if (ne <= (uint32_t)CSR_EREG) {
-                        const uint32_t at = R0.z;                   // the first 4 exceptions' blocks
-                        if (ne > 0) patch(at & 31u, 0);
-                        if (ne > 1) patch((at >> 8) & 31u, 1);
-                        if (ne > 2) patch((at >> 16) & 31u, 2);
-                        if (ne > 3) patch((at >> 24) & 31u, 3);
-                    } else {                                       // (rare) from the record codes' flag bits
-                        const uint32_t rw[16] = {R1.x, R1.y, R1.z, R1.w, R2.x, R2.y, R2.z, R2.w,
-                                                 R3.x, R3.y, R3.z, R3.w, R4.x, R4.y, R4.z, R4.w};
-                        uint32_t m = 0;                            // blocks that are exceptions (ordinals in block order)
-#pragma unroll
-                        for (int i = 0; i < 16; i++) m |= ((rw[i] >> 15) & 1u) << (2 * i) | (rw[i] >> 31) << (2 * i + 1);
-                        for (uint32_t ord = 0; m; ord++, m &= m - 1u) patch((uint32_t)__builtin_ctz(m), ord);
-                    }
+                    uint32_t m = R0.z;                             // exception blocks, their entries in block order
+                    if (ne > 0) { patch((uint32_t)__builtin_ctz(m), 0); m &= m - 1u; }
+                    if (ne > 1) { patch((uint32_t)__builtin_ctz(m), 1); m &= m - 1u; }
+                    if (ne > 2) { patch((uint32_t)__builtin_ctz(m), 2); m &= m - 1u; }
+                    if (ne > 3) { patch((uint32_t)__builtin_ctz(m), 3); m &= m - 1u; }
+                    for (uint32_t ord = CSR_EREG; m; ord++, m &= m - 1u) patch((uint32_t)__builtin_ctz(m), ord);   // (rare)
                     auto putx = [&](uint32_t e, const u32x4 &x, const u32x2 &y) {
                         *(u32x4 *)&L.EA[e] = x;
                         *(u32x2 *)&L.EB[e] = y;
