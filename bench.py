@@ -233,9 +233,9 @@ def cpu_baseline(gpu_window, members, seconds_budget=50.0):
     out = subprocess.run([sys.executable, os.path.join(REPO, "tools", "cpu_baseline.py"), "--budget",
                           str(seconds_budget), "--window", gpu_window, "--members", str(members), "--variants",
                           "ref,opt,ref1,opt1"],
-                         capture_output=True, text=True, timeout=1200)
+                         stdout=subprocess.PIPE, text=True, timeout=1200)   # (its progress lines pass to stderr)
     if out.returncode != 0:
-        return {"error": out.stderr[-400:]}
+        return {"error": f"tools/cpu_baseline.py exit {out.returncode}"}
     return json.loads(out.stdout.strip().splitlines()[-1])
 
 

@@ -352,7 +352,8 @@ struct swimsim {
     CsdRow *csr_rinfo = nullptr;
     CsrPlan *csr_plan = nullptr;
     CsrRec *csr_rec = nullptr;
-    uint32_t csr_ecap = 4096, csr_rcap = 512, csr_KP = 0;    // (2,048 entries: rows far from the reference fell back)
+    // (2,048 entries: rows far from the reference fell back; 512 records: 2,620 rows of a 65,536-row round-22 launch)
+    uint32_t csr_ecap = 4096, csr_rcap = 1024, csr_KP = 0;
     uint4 *csr_ucol = nullptr;                    // the divergent columns' scan table (k_csr_ucol)
     uint32_t *csr_fbsplit = nullptr;              // fallback rows per production launch (k_csr_fbsplit)
     unsigned long long *csr_acc = nullptr;        // [8] fallback rows so far, then per reason (read by path stats)

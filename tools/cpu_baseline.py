@@ -107,6 +107,9 @@ def main():
     ap.add_argument("--budget", type=float, default=60.0, help="seconds of CPU-side timing over all four runs")
     ap.add_argument("--window", default="65536:5:20", help="GPU line's members:warmup:steps")
     ap.add_argument("--members", type=int, default=16384)
+    ap.add_argument("--members-1thread", type=int, default=8192,
+                    help="N of the one-thread runs (a one-thread reference-cost round at 65,536 takes minutes: its warmup "
+                         "alone ran past 450 s on the GPU box)")
     ap.add_argument("--variants", default="ref,opt,ref1,opt1", help="which of the four runs (ref1/opt1: one thread)")
     ap.add_argument("--variant-timeout", type=float, default=1800.0)
     ap.add_argument("--variant", default=None, help=argparse.SUPPRESS)   # child: "ref|opt:n:warmup:steps:budget"
@@ -122,14 +125,15 @@ def main():
     nthr = cores()
     n = min(args.members, gpu_n)
     b = args.budget
-    spec = lambda kind, share: f"{kind}:{n}:{warmup}:{steps}:{share * b}"
+    n1 = min(args.members_1thread, n)
+    spec = lambda kind, share, nn=n: f"{kind}:{nn}:{warmup}:{steps}:{share * b}"
     want = set(args.variants.split(","))
-    pick = lambda name, kind, share: spec(kind, share) if name in want else None
+    pick = lambda name, kind, share, nn=n: spec(kind, share, nn) if name in want else None
     vt = args.variant_timeout
     ref = run_threads(nthr, pick("ref", "ref", 0.45), vt)
     opt = run_threads(nthr, pick("opt", "opt", 0.15), vt)
-    ref1 = run_threads(1, pick("ref1", "ref", 0.25), vt)
-    opt1 = run_threads(1, pick("opt1", "opt", 0.15), vt)
+    ref1 = run_threads(1, pick("ref1", "ref", 0.25, n1), vt)
+    opt1 = run_threads(1, pick("opt1", "opt", 0.15, n1), vt)
     host = "unknown"
     try:
         with open("/proc/cpuinfo") as f:
@@ -146,13 +150,14 @@ def main():
                   f"{warmup}-{warmup + steps - 1} timed ({ref.get('seconds')} s)",
         "reference_cost": ref,
         "optimized_port": {**opt, "note": "static-order string, checksum once per round per dirty row"},
-        "reference_cost_1thread": ref1,
-        "optimized_port_1thread": opt1,
+        "reference_cost_1thread": {**ref1, "members": n1},
+        "optimized_port_1thread": {**opt1, "members": n1},
         "window_note": f"the GPU line times rounds {warmup}-{warmup + steps - 1}; each CPU run times the first rounds of "
                        f"that window that fit its share of the {b:.0f}-s budget (reference cost model, {nthr} threads: "
                        f"rounds {rr[0]}-{rr[1]}). The rounds left out are the cascade's heaviest (every dirty row's string "
                        f"rebuilt and hashed at each applying Update), so each CPU value is its rate over the lighter "
-                       f"rounds: it overstates the CPU over the whole window",
+                       f"rounds: it overstates the CPU over the whole window. The one-thread runs use N={n1} (the "
+                       f"cost per member-round grows with N, so they overstate a one-thread run at N={n} too)",
     }))
 
 
