@@ -22,7 +22,7 @@ The JSON line carries:
                  = algorithmic bytes per launch, / its average launch time (HIP events on the engine's own
                  stream), against the 8 TB/s HBM peak. `traffic` = HBM bytes per launch from the rocprofv3
                  PMC passes of THIS command cut to the same timed rounds (k_profile_mark dispatches around
-                 them; profiles/r04_pmc_summary.json; null when that summary was taken on another workload).
+                 them; profiles/r05_pmc_summary.json; null when that summary was taken on another workload).
                  `kernels` gives the same figures for the other kernels (the other checksum kernel, k_recv,
                  k_resp, k_issue); `merge_kernel` repeats k_recv, the north-star merge kernel.
   cpu_baseline : the C oracle on the GPU box's host cores (rank 0, N=1 only) at the GPU line's N, bounded sample.
@@ -43,12 +43,12 @@ VALU_PEAK_GINST = 256 * 4 * 2.4 / 2  # wave-instructions/ns: 1024 SIMDs, one wav
 KILL_ROUND = 10
 MARK_BEGIN, MARK_END = 0x5717, 0x5718   # k_profile_mark ids around the timed rounds (tools/pmc_summary.py --window)
 # kernel family (swimsim_kernel_times) -> kernel symbol in rocprofv3 output (template arguments ignored)
-# (wide launches of at least 1,024 rows run the reference-row chain kernel k_csr by default; k_checksum3 takes the rows
+# (wide launches of at least 1,024 rows run the reference-row chain kernel k_csr3 by default; k_checksum3 takes the rows
 # it leaves and the launches with the path off)
-FAMILY_KERNEL = {"checksum_wide": "swimdev::k_csr", "checksum_narrow": "swimdev::k_checksum_q16",
+FAMILY_KERNEL = {"checksum_wide": "swimdev::k_csr3", "checksum_narrow": "swimdev::k_checksum_q16",
                  "recv_merge": "swimdev::k_recv", "resp_merge": "swimdev::k_resp", "issue": "swimdev::k_issue",
                  "timers": "swimdev::k_timers"}
-PMC_SUMMARY = os.path.join(REPO, "profiles", "r04_pmc_summary.json")
+PMC_SUMMARY = os.path.join(REPO, "profiles", "r05_pmc_summary.json")
 FETCH_CALIB = os.path.join(REPO, "profiles", "r03_fetch_calib.json")
 
 

@@ -352,8 +352,7 @@ struct swimsim {
     CsdRow *csr_rinfo = nullptr;
     CsrPlan *csr_plan = nullptr;
     CsrRec *csr_rec = nullptr;
-    // (2,048 entries: rows far from the reference fell back; 512 records: 2,620 rows of a 65,536-row round-22 launch)
-    uint32_t csr_ecap = 4096, csr_rcap = 1024, csr_KP = 0;
+    uint32_t csr_ecap = 4096, csr_rcap = 1024, csr_KP = 0;   // (2,048 entries: rows far from the reference fell back)
     uint4 *csr_ucol = nullptr;                    // the divergent columns' scan table (k_csr_ucol)
     uint32_t *csr_fbsplit = nullptr;              // fallback rows per production launch (k_csr_fbsplit)
     unsigned long long *csr_acc = nullptr;        // [8] fallback rows so far, then per reason (read by path stats)
@@ -833,6 +832,9 @@ int csr_alloc(swimsim *h) {
     // (per listed row of one launch: sized for NL rows; the few launches that list more rows and dense snapshots
     // together keep the production kernels, csr_hash)
     const uint32_t rows = h->NL;
+    // records per row: 1,024 (512 left 2,620 rows of a 65,536-row round-22 launch to the production kernels); 512 past
+    // 131,072 members, where the rows' other arrays need the memory (config 5's 262,144-member shard: 10 % headroom)
+    h->csr_rcap = h->N <= 131072 ? 1024u : 512u;
     h->csr_sbw_words = ((size_t)h->N * (h->W + 32) + 256) / 4;
     h->csr_KP = (uint32_t)(h->csr_sbw_words * 4 / 20 + 2);
     const size_t nalloc0 = h->allocs.size();
