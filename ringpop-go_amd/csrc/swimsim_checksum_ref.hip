@@ -211,7 +211,12 @@ __device__ void csd_run_entries(const DS &d, const uint32_t *row, uint32_t m0, u
 }
 
 template <int W>
-__global__ void __launch_bounds__(256) k_csd_scan(DS d, const uint32_t *list, uint32_t n, CsdArgs a) {
+// (five workgroups per CU: 96 VGPRs, five waves per SIMD for a latency-bound gather; with 8 chunks in flight and four
+// waves per SIMD the path took 0.05-0.15 ms longer on real cascade rounds 14-20, with six it spilled)
+#ifndef CSD_SCAN_MINB
+#define CSD_SCAN_MINB 5
+#endif
+__global__ void __launch_bounds__(256, CSD_SCAN_MINB) k_csd_scan(DS d, const uint32_t *list, uint32_t n, CsdArgs a) {
     // CSD_SU chunks of 64 members per pass, their loads in flight together (a row is one 256-KB stream). A chunk's
     // differing members are taken together, one per lane: the shift before each is a wave prefix sum of the record
     // length differences, a member starts a new run of exception blocks when its first block lies past the previous
@@ -219,7 +224,10 @@ __global__ void __launch_bounds__(256) k_csd_scan(DS d, const uint32_t *list, ui
     // before it (prefix sums place the closed runs and their entries). Round 4's first version walked the members one
     // at a time (the whole wave, scalar): 5.9 ms per launch on a heavy cascade round. Runs wait in LDS for their
     // entries, generated (one lane per run) between passes.
-    constexpr uint32_t CSD_SU = 8, RUNCAP = 256, RUNFLUSH = 128;
+#ifndef CSD_SU_DEF
+#define CSD_SU_DEF 4
+#endif
+    constexpr uint32_t CSD_SU = CSD_SU_DEF, RUNCAP = 256, RUNFLUSH = 128;
     __shared__ uint32_t runs[4][RUNCAP][6];                         // {klo, khi, m0, o0, s_after, first entry}
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
     const uint32_t i = blockIdx.x * 4 + wv;

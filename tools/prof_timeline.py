@@ -9,8 +9,12 @@ import collections
 import csv
 import sys
 
-FAMILIES = [("k_checksum3", "cs_wide"), ("k_checksum_q16", "cs_narrow"), ("k_recv", "recv"), ("k_resp", "resp"),
+FAMILIES = [("k_csr3", "cs_csr3"), ("k_csd_scan", "cs_scan"), ("k_csr_rec", "cs_rec"), ("k_checksum3", "cs_wide"), ("k_checksum_q16", "cs_narrow"), ("k_recv", "recv"), ("k_resp", "resp"),
             ("k_issue", "issue"), ("k_fp_", "fp"), ("rocprim", "sort"), ("hipcub", "sort")]
+
+
+COLS = ("cs_csr3", "cs_scan", "cs_rec", "cs_wide", "cs_narrow", "overlap", "recv", "resp", "issue", "fp", "sort",
+        "other")
 
 
 def family(name):
@@ -44,7 +48,7 @@ def main():
     starts = [k[0] for k in ks if "k_timers" in k[2]] + [mark_t[-1]]
     out = []
     hdr = f"{'round':>5} {'wall_ms':>8} {'busy_ms':>8} {'idle_ms':>8} " + " ".join(
-        f"{f:>9}" for f in ("cs_wide", "cs_narrow", "overlap", "recv", "resp", "issue", "fp", "sort", "other"))
+        f"{f:>9}" for f in COLS)
     out.append(hdr)
     tot = collections.Counter()
     for i in range(len(starts) - 1):
@@ -63,11 +67,9 @@ def main():
         row = {"wall": wall, "busy": busy, "idle": wall - busy, "overlap": ov, **fam}
         tot.update(row)
         out.append(f"{i:>5} {wall / 1e6:8.3f} {busy / 1e6:8.3f} {(wall - busy) / 1e6:8.3f} " + " ".join(
-            f"{row.get(f, 0) / 1e6:9.3f}" for f in ("cs_wide", "cs_narrow", "overlap", "recv", "resp", "issue", "fp",
-                                                     "sort", "other")))
+            f"{row.get(f, 0) / 1e6:9.3f}" for f in COLS))
     out.append(f"{'sum':>5} {tot['wall'] / 1e6:8.3f} {tot['busy'] / 1e6:8.3f} {tot['idle'] / 1e6:8.3f} " + " ".join(
-        f"{tot.get(f, 0) / 1e6:9.3f}" for f in ("cs_wide", "cs_narrow", "overlap", "recv", "resp", "issue", "fp", "sort",
-                                                 "other")))
+        f"{tot.get(f, 0) / 1e6:9.3f}" for f in COLS))
     text = "\n".join(out)
     print(text)
     if len(sys.argv) > 2:
