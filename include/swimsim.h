@@ -80,9 +80,11 @@ typedef struct swimsim_tuning {
                                  every launch of at least 1,024 rows */
     int32_t fault_inject;     /* tests only, bits: 1 = the reference-row path's buffers fail to allocate (the production
                                  kernels stay in charge, create and step succeed); 2 = the next reference-row launch fails
-                                 with SWIMSIM_EHIP (the step returns it); 4 = 8 exception slots per stager wave (the
-                                 overflow slots and the fallback rows run); 8 = dedup keys narrowed to 3 bits (fingerprint
-                                 groups of unequal rows); default 0. Results are identical with 4 and 8. */
+                                 with SWIMSIM_EHIP (the step returns it); 4 = exception rings of 8 entries (ring waits,
+                                 wrap-arounds and the fallback rows run); 8 = dedup keys narrowed to 3 bits (fingerprint
+                                 groups of unequal rows); 16 = the reference-row kernel's stager waves at raised issue
+                                 priority (a schedule in which the chain waves drift apart); default 0. Results are
+                                 identical with 4, 8 and 16. */
 } swimsim_tuning;
 
 /* Events applied in phase E of a round (docs/ROUND_SEMANTICS.md §4). */

@@ -68,6 +68,8 @@ struct CsrArgs {
     uint32_t *fb_list, *fb_cnt;   // rows left to the production kernels
     uint32_t exw;                 // k_csr3: cap on a row group's exception ring entries (~0; tests lower it to 8,
                                   // swimsim_tuning.fault_inject bit 4)
+    uint32_t stprio;              // k_csr3: stager waves at issue priority 1 (tests: fault_inject bit 16, a schedule
+                                  // that let one kind of chain wave run super steps ahead of the other)
 };
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -241,10 +243,11 @@ __global__ void __launch_bounds__(256) k_csr_rec(DS d, const uint32_t *list, uin
 // exception entries live in a ring per row group, so a record stager runs up to two super steps ahead of its chains
 // (the stamps of the double-buffered version: its chains waited 30 % of a heavy round for it while it waited 45 % of
 // the time for them, one super step of slack against records that come in bursts). LDS counters hand the buffers
-// over: readyw[b] (window stagers that filled window buffer b: 4 per super step), done[b] (chain waves done with it:
-// 8 per super step, which the window stagers wait for), readyr[g] (super steps group g's record stager has staged)
-// and doner[g] (super steps group g's two chain waves have finished, 2 per super step: a group's codes and ring are
-// its own, so its record stager waits only for them). Codes are u16 byte offsets into the entry arrays (window
+// over: readyw[b] (window stagers that filled window buffer b: 4 per super step), done[k][b] (chain waves of kind k,
+// g/f or h, done with it: 4 per super step, which the window stagers wait for), readyr[g] (super steps group g's
+// record stager has staged) and doner[k][g] (super steps group g's chain wave of kind k has finished: a group's codes
+// and ring are its own, so its record stager waits only for them). Done counts are kept per kind because a kind's
+// waves can run super steps ahead of the other's. Codes are u16 byte offsets into the entry arrays (window
 // buffer 0, window buffer 1, then the four rings) from the super step's window buffer, so base codes do not depend on
 // which window buffer a code buffer meets.
 // A chain wave waits only until the stagers have filled the super step it needs, reads its row's 32 codes (base(s) + i
@@ -264,13 +267,27 @@ struct Csr3Lds {
     uint4 TC[C3_NB][4][CSR_ROWS];         // codes: TC[k][q][row] = u16 codes 8q .. 8q + 7 of the row (lane-contiguous)
     uint32_t XH[CSR_ROWS];                 // h lanes' final state
     uint32_t FLX[CSR_ROWS];                // rows the stagers flagged (exception slots)
-    uint32_t readyw[C3_NB], done[C3_NB];   // window stagers that filled buffer b (4 a super step); chains done with it (8)
-    uint32_t readyr[4], doner[4];          // per row group: super steps staged by its record stager; its chains' steps
+    uint32_t readyw[C3_NB];                // window stagers that filled buffer b (4 a super step)
+    uint32_t done[2][C3_NB];               // [g/f, h] chain waves done with buffer b (4 a super step each)
+    uint32_t readyr[4], doner[2][4];       // per row group: super steps staged by its record stager; done by its g/f
+                                           // and its h wave (one count per kind: one kind's waves can run steps ahead
+                                           // of the other's, and a shared count let the leader's steps stand in for
+                                           // the laggard's, which was still reading the buffer)
     uint32_t phs[20];
 };
 
 __device__ __forceinline__ void c3_wait(const uint32_t *ctr, uint32_t target) {
     while (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target) __builtin_amdgcn_s_sleep(1);
+}
+// both kinds of chain wave (g/f: ctr[0][i], h: ctr[1][i]) have reached target
+template <int NI>
+__device__ __forceinline__ void c3_wait2(const uint32_t (&ctr)[2][NI], uint32_t i, uint32_t target) {
+#ifdef C3_T_SHAREDDONE
+    c3_wait(&ctr[0][i], 2u * target);                                // (test build: round 5's racy shared count)
+#else
+    c3_wait(&ctr[0][i], target);
+    c3_wait(&ctr[1][i], target);
+#endif
 }
 __device__ __forceinline__ void c3_signal(uint32_t *ctr) {
     if ((threadIdx.x & 63u) == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -308,6 +325,7 @@ __device__ __forceinline__ void c3_stage(const DS &d, const uint32_t *list, uint
 #if defined(C3_SPRIO) && C3_SPRIO > 0
     __builtin_amdgcn_s_setprio(C3_SPRIO);
 #endif
+    if (a.stprio) __builtin_amdgcn_s_setprio(1);
     C3Row r = c3_row(d, list, cnt, a, p, tid);
     const CsrRec *rec = a.rec + (size_t)(r.valid ? r.gi : blockIdx.x * CSR_ROWS) * a.rcap;
     const uint4 *ent = a.ent + (size_t)(r.valid ? r.gi : blockIdx.x * CSR_ROWS) * a.ecap * 2;
@@ -374,8 +392,8 @@ __device__ __forceinline__ void c3_stage(const DS &d, const uint32_t *list, uint
             const uint32_t skip = rpos + need > R ? R - rpos : 0u;
             // the slots of super steps t - 2 and t - 1 may still be read (those of t - 3 are free: the step's wait)
             if (alloc + skip + need - e3 > R) {
-                if (t >= 2) c3_wait(&L.doner[rwave], 2u * (t - 1u));
-                if (alloc + skip + need - e2 > R && t >= 1) c3_wait(&L.doner[rwave], 2u * t);
+                if (t >= 2) c3_wait2(L.doner, rwave, t - 1u);
+                if (alloc + skip + need - e2 > R && t >= 1) c3_wait2(L.doner, rwave, t);
             }
             const uint32_t xb = ring0 + (skip ? 0u : rpos) + sb;
             alloc += skip + need;
@@ -457,7 +475,7 @@ __device__ __forceinline__ void c3_stage(const DS &d, const uint32_t *list, uint
     auto step = [&](uint32_t u, auto BC, auto KC) {
         constexpr uint32_t b = decltype(BC)::value;
         C3S_STAMP(s0);
-        if (u >= 3) c3_wait(&L.doner[rwave], 2u * (u - 2u));      // this group's chains are done with super step u - 3
+        if (u >= 3) c3_wait2(L.doner, rwave, u - 2u);               // this group's chains are done with super step u - 3
         C3S_STAMP(s1);
 #ifdef CSR_DIAG_STAMP
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");            // (diagnostics: slot 1 = the record loads' wait)
@@ -508,6 +526,7 @@ __device__ __forceinline__ void c3_wstage(const CsrArgs &a, const CsrPlan &p, Cs
 #if defined(C3_WPRIO) && C3_WPRIO > 0
     __builtin_amdgcn_s_setprio(C3_WPRIO);
 #endif
+    if (a.stprio) __builtin_amdgcn_s_setprio(1);
     // window: entries u = tid + 256 v (both halves), two register sets (super step u -> set u & 1), loaded two ahead
     constexpr int WV = CSR_WINMAX / CSR_ROWS;
     u32x4 wA0[WV], wB0[WV], wC0[WV];
@@ -551,7 +570,7 @@ __device__ __forceinline__ void c3_wstage(const CsrArgs &a, const CsrPlan &p, Cs
     // super step u = 3 j + b: register set and buffer b, loaded three super steps ahead
     auto step = [&](uint32_t u, uint32_t j, auto BC) {
         constexpr uint32_t b = decltype(BC)::value;
-        if (j > 0) c3_wait(&L.done[b], 8u * j);                     // every chain is done with super step u - 3
+        if (j > 0) c3_wait2(L.done, b, 4u * j);                      // every chain is done with super step u - 3
         if constexpr (b == 0) { wstore(wA0, wA1, 0u); wload(wA0, wA1, u + 3); }
         else if constexpr (b == 1) { wstore(wB0, wB1, 1u); wload(wB0, wB1, u + 3); }
         else { wstore(wC0, wC1, 2u); wload(wC0, wC1, u + 3); }
@@ -654,8 +673,13 @@ __device__ __forceinline__ void c3_chain(const DS &d, const uint32_t *list, uint
         };
         if (full) run(std::integral_constant<bool, true>{});
         else run(std::integral_constant<bool, false>{});
-        c3_signal(&L.done[b]);
-        c3_signal(&L.doner[grp]);
+#ifdef C3_T_SHAREDDONE
+        c3_signal(&L.done[0][b]);
+        c3_signal(&L.doner[0][grp]);
+#else
+        c3_signal(&L.done[ROLE][b]);
+        c3_signal(&L.doner[ROLE][grp]);
+#endif
         C3_STAMP(td);
         C3_ACC(0, td - tc);
 #ifdef CSR_DIAG_SPLITWAIT
@@ -717,8 +741,8 @@ __global__ void __launch_bounds__(4 * CSR_ROWS) k_csr3(DS d, const uint32_t *lis
     if (blockIdx.x * CSR_ROWS >= cnt) return;
     const CsrPlan p = a.plan[blockIdx.x];
     if (threadIdx.x < 20 && ((p.phm >> threadIdx.x) & 1u)) L.phs[__popc(p.phm & ((1u << threadIdx.x) - 1u))] = threadIdx.x;
-    if (threadIdx.x < C3_NB) { L.readyw[threadIdx.x] = 0; L.done[threadIdx.x] = 0; }
-    if (threadIdx.x < 4) { L.readyr[threadIdx.x] = 0; L.doner[threadIdx.x] = 0; }
+    if (threadIdx.x < C3_NB) { L.readyw[threadIdx.x] = 0; L.done[0][threadIdx.x] = 0; L.done[1][threadIdx.x] = 0; }
+    if (threadIdx.x < 4) { L.readyr[threadIdx.x] = 0; L.doner[0][threadIdx.x] = 0; L.doner[1][threadIdx.x] = 0; }
     __syncthreads();
     const uint32_t T_ = p.feasible ? (p.maxit + CSR_SB - 1) / CSR_SB : 0u;
     const uint32_t role = threadIdx.x / CSR_ROWS;

@@ -930,6 +930,7 @@ int csr_hash(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t n, 
     a.fb_list = h->csr_fb;
     a.fb_cnt = h->csr_fbcnt;
     a.exw = (h->fault_inject & 4) ? 8u : 0xFFFFFFFFu;
+    a.stprio = (h->fault_inject & 16) ? 1u : 0u;
     {
         Scope sc(h, F_CSD_SCAN);
         hipLaunchKernelGGL(k_csd_ref, dim3((h->N + 256) / 256), dim3(256), 0, h->s, h->d, list, n, h->csr_B, h->csr_Lb);

@@ -90,6 +90,28 @@ def test_mode5_on_real_cascade_rows(n, rounds):
     print(f"real rows n{n}", c.checksum_path_stats())
 
 
+def test_stager_priority_schedule_on_real_cascade_rows():
+    """swimsim_tuning.fault_inject = 16: k_csr3's stager waves at raised issue priority, a schedule in which one kind of
+    chain wave (g/f or h) runs super steps ahead of the other. Each kind must count its own steps when a stager reuses
+    a buffer: a count shared by both kinds let the leader's steps stand in for the laggard's, and the stager overwrote a
+    window or code buffer the laggard was still reading (195 wrong rows of 65,536 at cascade round 18 in this schedule).
+    The path's checksums must equal the production kernels' (swimsim_bench_checksum mode 0) on every row."""
+    n = 32768
+    wl = W.config3(n=n, rounds=21, kill_round=10)
+    c = swimsim.Cluster(n, tuning={"fault_inject": 16})
+    for r in range(20):
+        c.step(1, wl.events_for(r))
+        if r in (15, 17, 19):
+            c.bench_checksum(n, 0, reps=1)
+            ref = c.checksums().copy()
+            for rep in range(2):
+                c.bench_checksum(n, 5, reps=1)
+                got = c.checksums()
+                bad = np.nonzero(got != ref)[0]
+                assert len(bad) == 0, f"round {r} rep {rep}: {len(bad)} rows differ, first {bad[:5]}"
+    print("stager priority", c.checksum_path_stats())
+
+
 def test_csr_alloc_failure_leaves_production_kernels_in_charge():
     """swimsim_tuning.fault_inject = 1: the reference-row path's buffers fail to allocate. The failure frees what was
     allocated and clears HIP's last error, so create and every step still succeed, on the production kernels."""
