@@ -237,6 +237,21 @@ __device__ __forceinline__ void wave_finalize(const DS &d, uint32_t ol, const MA
 // Batched gathers: the loops below issue MB independent loads per lane before using any of them (a
 // message's changes are distinct members, so no load of a batch depends on a store of the same batch).
 constexpr int MB = 4;
+constexpr int SNAP_MB = 8;             // row copies (snapshots): 16-B loads in flight per lane
+
+// one wave copies n 16-B items, SNAP_MB loads in flight per lane (a loop of load-then-store waits for each load: one
+// HBM round trip per 1 KB)
+__device__ __forceinline__ void wave_copy16(uint4 *dst, const uint4 *src, uint32_t n) {
+    for (uint32_t i = lane_id(); i < n; i += 64 * SNAP_MB) {
+        uint4 v[SNAP_MB];
+#pragma unroll
+        for (int u = 0; u < SNAP_MB; u++)
+            if (i + 64u * u < n) v[u] = src[i + 64u * u];
+#pragma unroll
+        for (int u = 0; u < SNAP_MB; u++)
+            if (i + 64u * u < n) dst[i + 64u * u] = v[u];
+    }
+}
 
 // a dense message (MembershipAsChanges: full sync, reverse full sync, heal) streams the whole row. (Kept
 // inline: an out-of-line call makes every launch copy the DS argument block to scratch, 480 B per lane.)
@@ -566,10 +581,19 @@ __device__ bool wave_snapshot(const DS &d, uint32_t ol, uint32_t o, MsgDesc &out
     const uint4 *src = (const uint4 *)(d.mw + (size_t)ol * d.NP);
     uint4 *dst = (uint4 *)(d.dense + (size_t)slot * d.NP);
     int known = 0;
-    for (uint32_t i = lane_id(); i < d.NP / 4; i += 64) {
-        const uint4 v = src[i];
-        dst[i] = v;
-        known += ((v.x & 7u) != ST_UNKNOWN) + ((v.y & 7u) != ST_UNKNOWN) + ((v.z & 7u) != ST_UNKNOWN) + ((v.w & 7u) != ST_UNKNOWN);
+    // (SNAP_MB loads in flight per lane: one at a time, each copy iteration waited for its load, 256 HBM round trips for
+    // a 256-KB row, and the snapshotting senders' waves set k_issue's time: 0.4 ms a launch)
+    const uint32_t n4 = d.NP / 4;
+    for (uint32_t i = lane_id(); i < n4; i += 64 * SNAP_MB) {
+        uint4 v[SNAP_MB];
+#pragma unroll
+        for (int u = 0; u < SNAP_MB; u++) v[u] = i + u * 64 < n4 ? src[i + u * 64] : make_uint4(ST_UNKNOWN, ST_UNKNOWN, ST_UNKNOWN, ST_UNKNOWN);
+#pragma unroll
+        for (int u = 0; u < SNAP_MB; u++) {
+            if (i + u * 64 < n4) dst[i + u * 64] = v[u];
+            known += ((v[u].x & 7u) != ST_UNKNOWN) + ((v[u].y & 7u) != ST_UNKNOWN) + ((v[u].z & 7u) != ST_UNKNOWN) +
+                     ((v[u].w & 7u) != ST_UNKNOWN);
+        }
     }
     known = wsum(known);
     if (lane_id() == 0) {
@@ -1547,12 +1571,12 @@ __global__ void k_snap_rows(DS d, const uint32_t *rows, uint32_t n, uint32_t *id
     const uint32_t ol = rows[k], slot = d.dense_cap + k;
     const uint4 *src = (const uint4 *)(d.mw + (size_t)ol * d.NP);
     uint4 *dst = (uint4 *)(d.dense + (size_t)slot * d.NP);
-    for (uint32_t i = lane_id(); i < d.NP / 4; i += 64 * MB) {
-        uint4 v[MB];
+    for (uint32_t i = lane_id(); i < d.NP / 4; i += 64 * SNAP_MB) {
+        uint4 v[SNAP_MB];
 #pragma unroll
-        for (int u = 0; u < MB; u++) v[u] = i + u * 64 < d.NP / 4 ? src[i + u * 64] : make_uint4(0, 0, 0, 0);
+        for (int u = 0; u < SNAP_MB; u++) v[u] = i + u * 64 < d.NP / 4 ? src[i + u * 64] : make_uint4(0, 0, 0, 0);
 #pragma unroll
-        for (int u = 0; u < MB; u++)
+        for (int u = 0; u < SNAP_MB; u++)
             if (i + u * 64 < d.NP / 4) dst[i + u * 64] = v[u];
     }
     if (lane_id() == 0) {

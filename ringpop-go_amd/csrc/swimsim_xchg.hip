@@ -143,7 +143,7 @@ __global__ void k_x_pack(DS d, XArgs x, const uint4 *items, const uint32_t *cnt,
     const uint4 *src = md->kind == 0
                            ? d.pool + (((unsigned long long)md->off_hi << 32) | md->off_lo)
                            : (const uint4 *)(d.dense + (size_t)md->off_lo * d.NP);
-    for (uint32_t k = lane_id(); k < pb / 16u; k += 64) dst[k] = src[k];
+    wave_copy16(dst, src, pb / 16u);
 }
 
 // one wave per received parcel; srcs[s] = {segment offset, parcel count, first global parcel index}
@@ -163,7 +163,7 @@ __global__ void k_x_unpack(DS d, XArgs x, const uint8_t *buf, const ulonglong2 *
     if (h.kind == 0 && h.len) {                                    // change records → local pool
         const unsigned long long off = pool_alloc(d, h.len);
         if (off == ~0ull) return;
-        for (uint32_t q = lane_id(); q < h.len; q += 64) d.pool[off + q] = payload[q];
+        wave_copy16(d.pool + off, payload, h.len);
         md.off_lo = (uint32_t)off;
         md.off_hi = (uint32_t)(off >> 32);
     } else if (h.kind == 1) {                                      // dense snapshot → local dense pool
@@ -175,7 +175,7 @@ __global__ void k_x_unpack(DS d, XArgs x, const uint8_t *buf, const ulonglong2 *
             return;
         }
         uint4 *dst = (uint4 *)(d.dense + (size_t)slot * d.NP);
-        for (uint32_t q = lane_id(); q < d.NP / 4; q += 64) dst[q] = payload[q];
+        wave_copy16(dst, payload, d.NP / 4);
         if (lane_id() == 0) {
             d.dense_meta[slot] = make_uint4(h.meta.x, h.meta.y, h.meta.z, 0u);   // w: a local alias only
             d.dense_len[slot] = h.dlen;
