@@ -725,12 +725,23 @@ __global__ void k_hot_fill(DS d) {
     const uint32_t k0 = d.hot_cnt[1], k1 = d.hot_cnt[0];
     const size_t rb = (size_t)ol * d.NP, hb = (size_t)ol * d.HP;
     int nowhot = 0;                                                // the row's entries whose member just got a slot
-    for (uint32_t k = k0 + lane_id(); k < k1; k += 64) {
-        const uint32_t m = d.hlist[k];
-        const uint2 cell = d.dent[rb + m];
-        d.hmw[hb + k] = d.mw[rb + m];
-        d.hde[hb + k] = cell;
-        nowhot += de_p(cell.x) != DP_NONE;
+    for (uint32_t k = k0 + lane_id(); k < k1; k += 64 * MB) {      // (MB slots per lane in flight: batched gathers)
+        uint32_t m[MB], w[MB];
+        uint2 cell[MB];
+#pragma unroll
+        for (int u = 0; u < MB; u++) m[u] = k + 64u * u < k1 ? d.hlist[k + 64u * u] : 0u;
+#pragma unroll
+        for (int u = 0; u < MB; u++) {
+            cell[u] = d.dent[rb + m[u]];
+            w[u] = d.mw[rb + m[u]];
+        }
+#pragma unroll
+        for (int u = 0; u < MB; u++) {
+            if (k + 64u * u >= k1) continue;
+            d.hmw[hb + k + 64u * u] = w[u];
+            d.hde[hb + k + 64u * u] = cell[u];
+            nowhot += de_p(cell[u].x) != DP_NONE;
+        }
     }
     if (k1 > k0) {
         nowhot = wsum(nowhot);
