@@ -26,6 +26,13 @@ constexpr int CSR_ROWS = 256;          // rows per workgroup (4 row groups of 64
 constexpr int CSR_SB = 32;             // blocks per super step
 constexpr int CSR_WINMAX = 1024;       // window entries per buffer: phases in use x Wn
 constexpr int C3_NB = 3;               // k_csr3's window and code table buffers (super step t: buffer t % 3)
+#ifndef C3_CTR_AT_DEF
+#define C3_CTR_AT_DEF 26
+#endif
+// the chain block at which a chain wave reads the next super step's hand-over counters (26: 4.66 / 7.41 ms on real
+// cascade rounds 14 / 18 at 65,536 rows, against 4.79 / 7.45 read before block 0 and 4.62 / 7.44 at block 16; a read
+// that comes too early finds the stagers short and costs a wait of an LDS round trip)
+constexpr int C3_CTR_AT = C3_CTR_AT_DEF;
 constexpr uint32_t CSR_ESZ = 16;       // a code's unit: an entry's byte offset in each of the two entry arrays
 constexpr int CSR_EREG = 4;            // exception entries of a record prefetched with it
 #ifndef CSR_PF_DEF
@@ -625,8 +632,8 @@ __device__ __forceinline__ void c3_chain(const DS &d, const uint32_t *list, uint
         const uint32_t K0 = t * CSR_SB;
         C3_STAMP(ta);
         // this group's record stager has staged super step t, and the window stagers its window: the counters were
-        // read during the last super step's chain (an LDS round trip per read, 10 % of a light round's loop when
-        // read here); only when they were short is there a wait, then an acquire fence for what they hand over
+        // read near the end of the last super step's chain (an LDS round trip per read, 10 % of a light round's loop
+        // when read here); only when they were short is there a wait, then an acquire fence for what they hand over
         if (pr < t + 1u) c3_wait(&L.readyr[grp], t + 1u);
 #ifdef CSR_DIAG_SPLITWAIT
         C3_STAMP(tw);                                               // (diagnostics: slot 2 = the window's wait)
@@ -645,8 +652,6 @@ __device__ __forceinline__ void c3_chain(const DS &d, const uint32_t *list, uint
             }
         }
         C3_STAMP(tc);
-        pr = __hip_atomic_load(&L.readyr[grp], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        pw = __hip_atomic_load(&L.readyw[b == 2u ? 0u : b + 1u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         const bool full = __all(myit == 0u || K0 + CSR_SB <= myit);
         const char *Eb = GF ? (const char *)L.EA : (const char *)L.EB;
         auto run = [&](auto FULLC) {
@@ -658,6 +663,11 @@ __device__ __forceinline__ void c3_chain(const DS &d, const uint32_t *list, uint
 #pragma unroll
             for (int i = 0; i < CSR_SB; i++) {
                 if (i + CSR_PF < CSR_SB) fetch(i + CSR_PF);
+                if (i == C3_CTR_AT) {                                   // the next super step's hand-over counters
+                    pr = __hip_atomic_load(&L.readyr[grp], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    pw = __hip_atomic_load(&L.readyw[b == 2u ? 0u : b + 1u], __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
                 const EV A = va[i % (CSR_PF + 1)];
                 uint32_t n0 = X0, n1 = X1;
                 if constexpr (GF) csd_gf_step(n0, n1, A.x, A.y, A.z, A.w);
