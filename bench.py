@@ -26,7 +26,15 @@ The JSON line carries:
                  `kernels` gives the same figures for the other kernels (the other checksum kernel, k_recv,
                  k_resp, k_issue); `merge_kernel` repeats k_recv, the north-star merge kernel.
   cpu_baseline : the C oracle on the GPU box's host cores (rank 0, N=1 only) at the GPU line's N, bounded sample.
+
+--workload (1 GPU; default config3, the driver's line): the other BASELINE.json configs measured the same way, each a
+line of its own (not the headline): config2 (4,096 members, 1 % churn per round), config4 (16,384 members, 2-way
+partition then heal_partition; the line adds the rounds from the heal to convergence, from an untimed replay),
+selfstart (16,384 members that know only themselves and two seed members: full syncs and reverse full syncs) and
+config5 (incarnation bursts, 10 % of 65,536 members every 20 rounds; 262,144 needs 8 GPUs). Their roofline adds the
+dense merges (reverse full syncs, k_jobs_merge) against SURVEY.md §8(d)'s streaming bytes.
 """
+import glob
 import argparse
 import json
 import os
@@ -47,8 +55,17 @@ MARK_BEGIN, MARK_END = 0x5717, 0x5718   # k_profile_mark ids around the timed ro
 # it leaves and the launches with the path off)
 FAMILY_KERNEL = {"checksum_wide": "swimdev::k_csr3", "checksum_narrow": "swimdev::k_checksum_q16",
                  "recv_merge": "swimdev::k_recv", "resp_merge": "swimdev::k_resp", "issue": "swimdev::k_issue",
-                 "timers": "swimdev::k_timers"}
-PMC_SUMMARY = os.path.join(REPO, "profiles", "r05_pmc_summary.json")
+                 "timers": "swimdev::k_timers", "rfs_merge": "swimdev::k_jobs_merge"}
+# PMC summaries of bench.py commands (tools/pmc_summary.py); a line uses the one whose _workload is its own
+PMC_GLOB = os.path.join(REPO, "profiles", "r0*_pmc_summary*.json")
+# --workload: default members, the builder in swimsim.workloads, what the line says about it
+WORKLOADS = {
+    "config3": (65536, "config3_cascade"),
+    "config2": (4096, "config2_churn"),
+    "config4": (16384, "config4_partition_heal"),
+    "selfstart": (16384, "selfstart_full_syncs"),
+    "config5": (65536, "config5_bursts"),
+}
 FETCH_CALIB = os.path.join(REPO, "profiles", "r03_fetch_calib.json")
 
 
@@ -70,17 +87,29 @@ def fetch_factor(fam):
     return (64.0 / r if r else 1.0), "k_gather<unsigned int>"
 
 
+def pmc_summary_for(workload):
+    """the newest committed PMC summary taken on exactly this bench.py command, cut to its timed rounds"""
+    for path in sorted(glob.glob(PMC_GLOB), reverse=True):
+        try:
+            with open(path) as f:
+                t = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if t.get("_workload") == workload and t.get("_window"):
+            return path, t
+    return None, None
+
+
 def pmc_kernel(symbol, workload):
     """Per-launch PMC figures of one kernel over the timed rounds only (rocprofv3 --pmc passes of this command, cut
-    between the k_profile_mark dispatches by tools/pmc_summary.py --window), or None when the committed summary was
-    taken on another workload or without the window cut."""
+    between the k_profile_mark dispatches by tools/pmc_summary.py --window), or None when no committed summary was
+    taken on this workload with the window cut."""
+    path, t = pmc_summary_for(workload)
+    if t is None:
+        return None
     try:
-        with open(PMC_SUMMARY) as f:
-            t = json.load(f)
-        if t.get("_workload") != workload or not t.get("_window"):
-            return None
         ks = [v for k, v in t.items() if not k.startswith("_") and k.split("<")[0].strip() == symbol]
-    except (OSError, KeyError, ValueError):
+    except (KeyError, ValueError):
         return None
     n = sum(k["launches"] for k in ks)
     if not n:
@@ -88,7 +117,7 @@ def pmc_kernel(symbol, workload):
     avg = lambda key: sum(k.get(key, 0.0) * k["launches"] for k in ks) / n
     return {"launches": n, "fetch": avg("fetch_bytes_per_launch"), "write": avg("write_bytes_per_launch"),
             "valu_insts": avg("sq_insts_valu_per_launch"), "lds_insts": avg("sq_insts_lds_per_launch"),
-            "source": os.path.relpath(PMC_SUMMARY, REPO)}
+            "source": os.path.relpath(path, REPO)}
 
 
 def roofline_entry(fam, kt, units, n_members):
@@ -136,6 +165,18 @@ def roofline_entry(fam, kt, units, n_members):
     elif fam == "issue":
         out.update({"work_unit": "issued record", "units_per_launch": round(units["issued"] / nl, 1), "bytes_per_unit": 32.0,
                     "alg_bytes_per_launch": round(units["issued"] / nl * 32.0, 1)})
+    elif fam == "rfs_merge":
+        dense, applied = units.get("dense_jobs", 0.0), units.get("jobs_applied", 0.0)
+        if not dense:
+            out.update({"work_unit": "dense merge", "units_per_launch": 0.0,
+                        "note": "no reverse full sync in the window: the launches exit at once"})
+            return out
+        out.update({"work_unit": "dense merge (reverse full sync)", "units_per_launch": round(dense / nl, 2),
+                    "applied_per_launch": round(applied / nl, 1),
+                    "bytes_per_unit_basis": "SURVEY.md §8(d): a dense batch streams the row, 5 B x N per merged snapshot; "
+                    "+ 23 B per applied change (the kernel reads the 4-B snapshot word and the 4-B row word per member)",
+                    "alg_bytes_per_launch": round((dense * 5.0 * n_members + applied * 23.0) / nl, 1),
+                    "physical_read_bytes_per_launch": round(dense * 8.0 * n_members / nl, 1)})
     else:
         return out
     alg = out["alg_bytes_per_launch"] / sec / 1e9
@@ -272,7 +313,7 @@ def emit(obj):
 
 def launch_ranks(args):
     """--gpus N without a launcher: start N ranks as a child torch.distributed.run, relay its status."""
-    if not args.launch_check:
+    if not args.launch_check and not args.host_transport:   # (--host-transport: every rank on GPU 0, by design)
         have = visible_gpu_count()
         if have is not None and have < args.gpus:
             print(f"bench.py: --gpus {args.gpus} but only {have} GPU(s) visible", file=sys.stderr)
@@ -283,12 +324,88 @@ def launch_ranks(args):
     return subprocess.run(cmd, env=env).returncode
 
 
+def make_workload(name, n, total_rounds):
+    from swimsim import workloads as W
+
+    if name == "config3":
+        return W.config3(n=n, rounds=max(total_rounds, KILL_ROUND + 1), kill_round=KILL_ROUND)
+    if name == "config2":
+        return W.config2(n=n, rounds=total_rounds)
+    if name == "config4":
+        return W.config4(n=n, rounds=total_rounds)
+    if name == "selfstart":
+        return W.selfstart(n=n, seeds=2, rounds=total_rounds)
+    return W.config5(n=n, rounds=total_rounds)
+
+
+def new_cluster(swimsim, wl, device, tuning):
+    """the workload's start: converged rows, or (selfstart) rows that know only themselves plus the seed members, which
+    every node learns by MakeChange before round 0 (untimed)"""
+    eng = swimsim.Cluster(wl.n, device=device, tuning=tuning, init=wl.init)
+    for o in range(wl.n):
+        for m in wl.seed_members:
+            if m != o:
+                eng.make_change(o, m, swimsim.T0_MS, swimsim.ALIVE)
+    return eng
+
+
+def rounds_to_heal(swimsim, wl, device, tuning, heal_round):
+    """config4: an untimed replay of the workload, one round per call, until the reference's convergence test holds
+    (test_utils.go:164-199: every live node has no changes and all checksums are equal); rounds after heal_round"""
+    eng = new_cluster(swimsim, wl, device, tuning)
+    try:
+        for r in range(wl.rounds):
+            eng.step(1, wl.events_for(r))
+            if r >= heal_round and eng.converged():
+                return r + 1 - heal_round
+        return None
+    finally:
+        eng.close()
+
+
+def workload_line(args, wl, n, dt, value, live_mr, dominant, entries, kt, counters, units, eng):
+    """the JSON line of a --workload other than config3 (1 GPU): the same fields as the headline line, the dense merges'
+    roofline entry beside the dominant kernel, and (config4) the rounds from the heal to convergence"""
+    import swimsim
+
+    dom = entries.get(dominant) or {}
+    line = {
+        "metric": f"simulated member-rounds/sec, {WORKLOADS[args.workload][1]} at {n} members",
+        "value": round(value, 1), "unit": "member-rounds/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(dt * 1e3 / args.steps, 4), "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "u32",
+        "data": f"synthetic ({wl.description}; Philox seeds as swimsim.workloads)",
+        "config": {"workload": f"{WORKLOADS[args.workload][1]}: {wl.name}, rounds {args.warmup}-{args.warmup + args.steps - 1} "
+                               "timed", "members": n, "rounds_timed": args.steps, "live_member_rounds": live_mr,
+                   "parallelism": "1 GPU"},
+        "roofline": {"bound": dom_bound(dominant, dom), **dom, "dominant_family": dominant,
+                     "kernels": {f: e for f, e in entries.items() if e and f != dominant},
+                     "merge_kernel": entries.get("recv_merge"), "dense_merge_kernel": entries.get("rfs_merge")},
+        "kernel_ms": {k: round(v["avg_ms"] * v["launches"], 3) for k, v in kt.items() if v["launches"]},
+        "kernel_ms_note": "HIP-event device time over the window of the roofline's families and k_jobs_merge",
+        "counters": counters,
+        "dense_merges": {k: int(v) for k, v in units.items() if k in ("dense_resp", "dense_jobs", "jobs_applied",
+                                                                     "dense_heal")},
+        "checksum_paths": eng.checksum_path_stats(),
+    }
+    if line["roofline"]["bound"] == "valu":
+        line["roofline"]["bound_frac"] = (dom.get("valu") or {}).get("frac")
+    if args.workload == "config4":
+        eng.close()                                                # (the replay allocates a cluster of its own)
+        heal_round = min(e[0] for e in wl.events if e[1] == 6)    # EV_HEAL
+        line["rounds_to_heal"] = rounds_to_heal(swimsim, wl, 0, None, heal_round)
+        line["rounds_to_heal_basis"] = (f"rounds from the first heal (r={heal_round}) until every live node has no changes "
+                                        "and all checksums are equal (test_utils.go:164-199), untimed replay")
+    return line
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=90)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--members", type=int, default=65536)
+    ap.add_argument("--members", type=int, default=0)        # 0: the workload's default (config3: 65,536)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="config3")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ring", action="store_true")
     # diagnostics: every rank on cuda:0, shards exchanging through the gloo host transport instead of
@@ -302,6 +419,10 @@ def main():
     ap.add_argument("--launch-check", action="store_true")
     args = ap.parse_args()
 
+    if args.members <= 0:
+        args.members = WORKLOADS[args.workload][0]
+    if args.gpus > 1 and args.workload != "config3":
+        raise SystemExit("bench.py: --workload other than config3 is a 1-GPU line")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args))
     ws, rank, local = dist_env()
@@ -343,8 +464,8 @@ def main():
     n = args.members
     total_rounds = args.warmup + args.steps
     tuning = {k: v for k, v in (("cs_ref", args.cs_ref), ("cs_async_rows", args.cs_async_rows)) if v >= 0} or None
-    wl = W.config3(n=n, rounds=max(total_rounds, KILL_ROUND + 1), kill_round=KILL_ROUND)
-    nkilled = sum(1 for e in wl.events if e[1] == W.EV_KILL)
+    wl = make_workload(args.workload, n, total_rounds)
+    nkilled = sum(1 for e in wl.events if e[1] == W.EV_KILL and e[0] == KILL_ROUND)
     if ws > 1:
         from swimsim import dist as sd
 
@@ -353,7 +474,7 @@ def main():
         else:
             eng = sd.sharded_cluster(n, device=local, tuning=tuning)
     else:
-        eng = swimsim.Cluster(n, device=local, tuning=tuning)
+        eng = new_cluster(swimsim, wl, local, tuning)
 
     def barrier():
         if ws > 1:
@@ -365,7 +486,7 @@ def main():
     for r in range(args.warmup):
         eng.step(1, wl.events_for(r))
     # (level 2: HIP events around the roofline's kernels only; every other family's event pair cost the window ~10 us)
-    eng.enable_timing(2 if not args.time_all else 1)
+    eng.enable_timing(1 if args.time_all else 2 if args.workload == "config3" else 3)
     if rank == 0:
         eng.profile_mark(MARK_BEGIN)    # rocprofv3 counter passes are cut to the launches between the two marks
     barrier()
@@ -389,6 +510,8 @@ def main():
     if ws > 1:
         counters = sd.reduce_counters(counters)
     workload = {"members": n, "steps": args.steps, "warmup": args.warmup, "gpus": ws}
+    if args.workload != "config3":
+        workload["workload"] = args.workload
 
     if rank == 0:
         timed_first, timed_last = args.warmup, total_rounds - 1
@@ -399,6 +522,11 @@ def main():
         dom = entries.get(dominant) or {}
         in_window = timed_first <= KILL_ROUND <= timed_last
         faulty_from = KILL_ROUND + 25       # first suspicions at KILL_ROUND; their timers fire 25 rounds later
+        if args.workload != "config3":
+            line = workload_line(args, wl, n, dt, value, live_mr, dominant, entries, kt, counters, units, eng)
+            sys.stdout.flush()
+            emit(line)
+            return
         line = {
             "metric": "simulated member-rounds/sec at 64k members" if n == 65536 else f"simulated member-rounds/sec at {n} members",
             "value": round(value, 1),

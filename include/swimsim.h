@@ -83,8 +83,12 @@ typedef struct swimsim_tuning {
                                  with SWIMSIM_EHIP (the step returns it); 4 = exception rings of 8 entries (ring waits,
                                  wrap-arounds and the fallback rows run); 8 = dedup keys narrowed to 3 bits (fingerprint
                                  groups of unequal rows); 16 = the reference-row kernel's stager waves at raised issue
-                                 priority (a schedule in which the chain waves drift apart); default 0. Results are
-                                 identical with 4, 8 and 16. */
+                                 priority (a schedule in which the chain waves drift apart); 32 = the reference-row
+                                 path's exception entries capped at 24 per row (rows ending within the stager's
+                                 prefetch of the cap); 64 = seeded sleeps before the reference-row kernel's hand-over
+                                 waits and signals, bits 8-11 selecting the delayed roles (g/f chains, h chains,
+                                 record stagers, window stagers), bits 12-30 the seed; default 0. Results are
+                                 identical with 4, 8, 16, 32 and 64. */
 } swimsim_tuning;
 
 /* Events applied in phase E of a round (docs/ROUND_SEMANTICS.md §4). */

@@ -150,7 +150,6 @@ __global__ void __launch_bounds__(128 * G) k_checksum3(DS d, const uint32_t *lis
                 for (int i = 0; i < 5; i++) B[i * C2_ROWS] = cw[i];
                 // format this step's 4 records: every record writes NO words at its position
                 const uint4 *ta = TA[u], *tb = TB[u];
-                const uint32_t ws[4] = {cur[u].x, cur[u].y, cur[u].z, cur[u].w};
 #pragma unroll
                 for (int k = 0; k < C2_IT; k++) {
                     const uint32_t m = mb + k;

@@ -77,6 +77,8 @@ struct CsrArgs {
                                   // swimsim_tuning.fault_inject bit 4)
     uint32_t stprio;              // k_csr3: stager waves at issue priority 1 (tests: fault_inject bit 16, a schedule
                                   // that let one kind of chain wave run super steps ahead of the other)
+    uint32_t jitter;              // k_csr3 (tests: fault_inject 64): 0 off; else bits 0-3 the roles to delay (g/f, h,
+                                  // record stager, window stager), bits 8-31 the seed of their delays
 };
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -245,22 +247,24 @@ __global__ void __launch_bounds__(256) k_csr_rec(DS d, const uint32_t *list, uin
 // their loop outside the chain: staging the next super step's window, unpacking records, writing exception entries,
 // and waiting at the per-super-step barrier for the slowest of the eight (shader-clock stamps, tools/csr_stamps.py).
 // Here two more waves per SIMD do all of that ahead of the chains, the record stager (lane = row: codes, exception
-// entries) and the window stager (a quarter of the window, two super steps ahead), and no barrier is left in the
-// loop. The window is double-buffered (window buffer t & 1); the codes are triple-buffered (TC[t % 3]) and the
-// exception entries live in a ring per row group, so a record stager runs up to two super steps ahead of its chains
-// (the stamps of the double-buffered version: its chains waited 30 % of a heavy round for it while it waited 45 % of
-// the time for them, one super step of slack against records that come in bursts). LDS counters hand the buffers
-// over: readyw[b] (window stagers that filled window buffer b: 4 per super step), done[k][b] (chain waves of kind k,
-// g/f or h, done with it: 4 per super step, which the window stagers wait for), readyr[g] (super steps group g's
-// record stager has staged) and doner[k][g] (super steps group g's chain wave of kind k has finished: a group's codes
-// and ring are its own, so its record stager waits only for them). Done counts are kept per kind because a kind's
-// waves can run super steps ahead of the other's. Codes are u16 byte offsets into the entry arrays (window
-// buffer 0, window buffer 1, then the four rings) from the super step's window buffer, so base codes do not depend on
-// which window buffer a code buffer meets.
+// entries) and the window stager (a quarter of the window, three super steps ahead), and no barrier is left in the
+// loop. The window and the codes are triple-buffered (window buffer and code table t % 3) and the exception entries
+// live in a ring per row group, so a record stager runs up to two super steps ahead of its chains (the stamps of the
+// double-buffered version: its chains waited 30 % of a heavy round for it while it waited 45 % of the time for them,
+// one super step of slack against records that come in bursts). LDS counters hand the buffers over: readyw[b] (window
+// stagers that filled window buffer b: 4 per super step), done[k][b] (chain waves of kind k, g/f or h, done with it: 4
+// per super step, which the window stagers wait for), readyr[g] (super steps group g's record stager has staged) and
+// doner[k][g] (super steps group g's chain wave of kind k has finished: a group's codes and ring are its own, so its
+// record stager waits only for them). Done counts are kept per kind because a kind's waves can run super steps ahead
+// of the other's. Codes are u16 byte offsets into the entry arrays (window buffers 0, 1 and 2, then the four rings), so
+// base codes do not depend on which window buffer a code buffer meets.
 // A chain wave waits only until the stagers have filled the super step it needs, reads its row's 32 codes (base(s) + i
 // in its window buffer, or a record's codes with its exceptions patched to ring slots) and runs the chain. Roles:
 // waves 0-3 g/f lanes, 4-7 h lanes, 8-11 record stagers, 12-15 window stagers; waves w, w + 4, w + 8 and w + 12 share
-// a SIMD and rows 64 w .. 64 w + 63.
+// a SIMD and rows 64 w .. 64 w + 63. The kernel's one barrier after the loops (every role reaches it from the same
+// call site) hands the h lanes' state and the stagers' flags to the g/f waves' epilogue.
+// Tests perturb the hand-over (CsrArgs::jitter, swimsim_tuning.fault_inject 64): seeded sleeps before every counter
+// wait and signal of the selected roles, so one kind of chain wave runs ahead of the other, or a stager falls behind.
 // ---------------------------------------------------------------------------------------------------------------
 constexpr int C3_ENT = 4096;               // entries: 3 windows of nwin entries, then 4 rings share the rest
 static_assert(C3_NB * CSR_WINMAX + 4 * 256 <= C3_ENT, "rings of at least 256 entries");
@@ -298,6 +302,16 @@ __device__ __forceinline__ void c3_wait2(const uint32_t (&ctr)[2][NI], uint32_t 
 }
 __device__ __forceinline__ void c3_signal(uint32_t *ctr) {
     if ((threadIdx.x & 63u) == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// tests only (CsrArgs::jitter): a seeded, wave-uniform delay before a hand-over wait or signal of role `role` at super
+// step t (site: which wait or signal). With probability 3/8 the wave sleeps 0 .. 127 x 128 clocks, up to several super
+// steps of chain, so every order of the four roles around a buffer reuse occurs somewhere in a launch.
+__device__ __forceinline__ void c3_jitter(uint32_t jit, uint32_t role, uint32_t t, uint32_t site) {
+    if (!((jit >> role) & 1u)) return;
+    const uint32_t x = fmix32((jit >> 8) * 0x9E3779B9u ^ blockIdx.x * 0x85EBCA6Bu ^ (threadIdx.x >> 6) * 0xC2B2AE35u ^
+                              t * 0x27D4EB2Fu ^ site * 0x165667B1u);
+    if ((x & 7u) < 3u)
+        for (uint32_t k = (x >> 8) & 127u; k; k--) __builtin_amdgcn_s_sleep(2);
 }
 
 struct C3Row {                                                      // what every role knows of its row
@@ -345,7 +359,9 @@ __device__ __forceinline__ void c3_stage(const DS &d, const uint32_t *list, uint
     auto load_rec = [&](uint32_t q, uint32_t e0) {
         const u32x4 *rp = (const u32x4 *)(rec + min(q, a.rcap - 1u));
         R0 = rp[0]; R1 = rp[1]; R2 = rp[2]; R3 = rp[3]; R4 = rp[4];
-        const u32x4 *ep = (const u32x4 *)(ent + 2 * min(e0, a.ecap - (uint32_t)CSR_EREG));
+        // (no clamp: the entry array has CSR_EREG spare entries past its last row, csr_alloc, so a record whose entries
+        // start within CSR_EREG of a row's cap loads its own entries; what lies past them is never stored)
+        const u32x4 *ep = (const u32x4 *)(ent + 2 * e0);
         EA0 = ep[0]; EB0 = *(const u32x2 *)(ep + 1);
         EA1 = ep[2]; EB1 = *(const u32x2 *)(ep + 3);
         EA2 = ep[4]; EB2 = *(const u32x2 *)(ep + 5);
@@ -482,6 +498,7 @@ __device__ __forceinline__ void c3_stage(const DS &d, const uint32_t *list, uint
     auto step = [&](uint32_t u, auto BC, auto KC) {
         constexpr uint32_t b = decltype(BC)::value;
         C3S_STAMP(s0);
+        c3_jitter(a.jitter, 2, u, 0);
         if (u >= 3) c3_wait2(L.doner, rwave, u - 2u);               // this group's chains are done with super step u - 3
         C3S_STAMP(s1);
 #ifdef CSR_DIAG_STAMP
@@ -491,6 +508,7 @@ __device__ __forceinline__ void c3_stage(const DS &d, const uint32_t *list, uint
         prep(u, b, KC);
         e3 = e2; e2 = e1; e1 = alloc;
         C3S_STAMP(s3);
+        c3_jitter(a.jitter, 2, u, 1);
         c3_signal(&L.readyr[rwave]);
         C3S_STAMP(s4);
         C3S_ACC(0, s1 - s0);
@@ -577,10 +595,12 @@ __device__ __forceinline__ void c3_wstage(const CsrArgs &a, const CsrPlan &p, Cs
     // super step u = 3 j + b: register set and buffer b, loaded three super steps ahead
     auto step = [&](uint32_t u, uint32_t j, auto BC) {
         constexpr uint32_t b = decltype(BC)::value;
+        c3_jitter(a.jitter, 3, u, 0);
         if (j > 0) c3_wait2(L.done, b, 4u * j);                      // every chain is done with super step u - 3
         if constexpr (b == 0) { wstore(wA0, wA1, 0u); wload(wA0, wA1, u + 3); }
         else if constexpr (b == 1) { wstore(wB0, wB1, 1u); wload(wB0, wB1, u + 3); }
         else { wstore(wC0, wC1, 2u); wload(wC0, wC1, u + 3); }
+        c3_jitter(a.jitter, 3, u, 1);
         c3_signal(&L.readyw[b]);
     };
     for (uint32_t u = 0, j = 0; u < T_; u += 3, j++) {
@@ -594,7 +614,7 @@ __device__ __forceinline__ void c3_wstage(const CsrArgs &a, const CsrPlan &p, Cs
 
 template <int W, int ROLE>                                          // ROLE 0: g/f lanes, 1: h lanes
 __device__ __forceinline__ void c3_chain(const DS &d, const uint32_t *list, uint32_t cnt, const CsrArgs &a, const CsrPlan &p,
-                                         Csr3Lds &L, uint32_t T_) {
+                                         Csr3Lds &L, uint32_t T_, uint3 &out) {
     constexpr bool GF = ROLE == 0;
     typedef typename std::conditional<GF, u32x4, u32x2>::type EV;
     const uint32_t tid = threadIdx.x & (CSR_ROWS - 1), grp = tid >> 6;
@@ -631,6 +651,7 @@ __device__ __forceinline__ void c3_chain(const DS &d, const uint32_t *list, uint
         constexpr uint32_t b = decltype(BC)::value;
         const uint32_t K0 = t * CSR_SB;
         C3_STAMP(ta);
+        c3_jitter(a.jitter, ROLE, t, 0);
         // this group's record stager has staged super step t, and the window stagers its window: the counters were
         // read near the end of the last super step's chain (an LDS round trip per read, 10 % of a light round's loop
         // when read here); only when they were short is there a wait, then an acquire fence for what they hand over
@@ -683,6 +704,7 @@ __device__ __forceinline__ void c3_chain(const DS &d, const uint32_t *list, uint
         };
         if (full) run(std::integral_constant<bool, true>{});
         else run(std::integral_constant<bool, false>{});
+        c3_jitter(a.jitter, ROLE, t, 1);
 #ifdef C3_T_SHAREDDONE
         c3_signal(&L.done[0][b]);
         c3_signal(&L.doner[0][grp]);
@@ -718,29 +740,35 @@ __device__ __forceinline__ void c3_chain(const DS &d, const uint32_t *list, uint
 #undef C3_STAMP
 #undef C3_ACC
     if constexpr (!GF) L.XH[tid] = X0;
-    __syncthreads();                                                // (every wave: XH and the stagers' FLX)
-    if constexpr (GF) {
-        const uint32_t fl = r.fl | L.FLX[tid];
-        const bool mine = r.valid && fl == 0;
-        const uint32_t nmine = (uint32_t)__popcll(__ballot(mine));
-        if ((threadIdx.x & 63u) == 0 && nmine) ctr_add(d, C_X_CS_ROWS, (unsigned long long)nmine);
-        if (!r.valid) return;
-        if (!mine) {                                                // left to the production kernels
-            const uint32_t at = atomicAdd(a.fb_cnt, 1u);
-            a.fb_list[at] = r.id;
-            const uint32_t rr = (fl & CSD_F_SHORT) ? 0u : (fl & CSD_F_ECAP) ? 1u : (fl & CSR_F_PLAN) ? 2u
-                              : (fl & CSR_F_RCAP) ? 3u : 4u;
-            atomicAdd(a.fb_cnt + 1 + rr, 1u);
-            return;
-        }
-        fh.h = L.XH[tid]; fh.g = X0; fh.f = X1;
-        const uint32_t hv = ok ? fh.fin() : 0u;
-        if (r.is_row) {
-            d.cs[r.id] = hv;
-            d.dirty[r.id] = 0;
-        } else {
-            d.dense_cs[r.id - d.NL] = hv;
-        }
+    out = make_uint3(X0, X1, ok ? 1u : 0u);
+}
+
+// the g/f waves' epilogue, after k_csr3's barrier: the h lanes' state (XH) and the stagers' flags (FLX) are in LDS
+template <int W>
+__device__ __forceinline__ void c3_finish(const DS &d, const uint32_t *list, uint32_t cnt, const CsrArgs &a, const CsrPlan &p,
+                                          Csr3Lds &L, uint3 X) {
+    const uint32_t tid = threadIdx.x & (CSR_ROWS - 1);
+    const C3Row r = c3_row(d, list, cnt, a, p, tid);
+    const uint32_t fl = r.fl | L.FLX[tid];
+    const bool mine = r.valid && fl == 0;
+    const uint32_t nmine = (uint32_t)__popcll(__ballot(mine));
+    if ((threadIdx.x & 63u) == 0 && nmine) ctr_add(d, C_X_CS_ROWS, (unsigned long long)nmine);
+    if (!r.valid) return;
+    if (!mine) {                                                    // left to the production kernels
+        const uint32_t at = atomicAdd(a.fb_cnt, 1u);
+        a.fb_list[at] = r.id;
+        const uint32_t rr = (fl & CSD_F_SHORT) ? 0u : (fl & CSD_F_ECAP) ? 1u : (fl & CSR_F_PLAN) ? 2u
+                          : (fl & CSR_F_RCAP) ? 3u : 4u;
+        atomicAdd(a.fb_cnt + 1 + rr, 1u);
+        return;
+    }
+    FH fh{L.XH[tid], X.x, X.y};
+    const uint32_t hv = X.z ? fh.fin() : 0u;                        // (X.z: the row's string is longer than 24 bytes)
+    if (r.is_row) {
+        d.cs[r.id] = hv;
+        d.dirty[r.id] = 0;
+    } else {
+        d.dense_cs[r.id - d.NL] = hv;
     }
 }
 
@@ -756,12 +784,11 @@ __global__ void __launch_bounds__(4 * CSR_ROWS) k_csr3(DS d, const uint32_t *lis
     __syncthreads();
     const uint32_t T_ = p.feasible ? (p.maxit + CSR_SB - 1) / CSR_SB : 0u;
     const uint32_t role = threadIdx.x / CSR_ROWS;
-    if (role == 0) c3_chain<W, 0>(d, list, cnt, a, p, L, T_);
-    else if (role == 1) c3_chain<W, 1>(d, list, cnt, a, p, L, T_);
-    else if (role == 2) {
-        c3_stage(d, list, cnt, a, p, L, T_);
-        __syncthreads();                                            // (the chain waves' final barrier)
-    } else {
+    uint3 X = make_uint3(0u, 0u, 0u);
+    if (role == 0) c3_chain<W, 0>(d, list, cnt, a, p, L, T_, X);
+    else if (role == 1) c3_chain<W, 1>(d, list, cnt, a, p, L, T_, X);
+    else if (role == 2) c3_stage(d, list, cnt, a, p, L, T_);
+    else {
         c3_wstage(a, p, L, T_);
 #if defined(CSR_DIAG_STAMP) && defined(CSR_DIAG_WINDOW)
         if (threadIdx.x == 3 * CSR_ROWS) {                          // (diagnostics: window geometry per super step)
@@ -770,8 +797,9 @@ __global__ void __launch_bounds__(4 * CSR_ROWS) k_csr3(DS d, const uint32_t *lis
             ctr_add(d, C_NALL + 7, (unsigned long long)T_ * p.nph);
         }
 #endif
-        __syncthreads();
     }
+    __syncthreads();                                                // (every role: XH and the stagers' FLX)
+    if (role == 0) c3_finish<W>(d, list, cnt, a, p, L, X);
 }
 
 // launches of the path (part): 0 S_B string, 1 P table, 2 scan, 3 plan + records, 4 the chains

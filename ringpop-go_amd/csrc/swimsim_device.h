@@ -12,8 +12,8 @@
 //   tmr u32x2 [NL][NP] timer {deadline round, subject e}
 //   dbit u32 [NL][NBIT] bit m: member m has a dissemination entry (exactly: p != 0xFF)
 //   tblk u32 [NL][NB]  lower bound of the unfired timer deadlines in block b
-// Messages are pools of 16-byte change records {member | status<<24, e, source, source e}, or
-// dense row snapshots for MembershipAsChanges (disseminator.go:107-123).
+// Messages are pools of 16-byte change records {member | status<<24, e, source, source e} (plus the member's hot slot
+// in spare bits, rec_make below), or dense row snapshots for MembershipAsChanges (disseminator.go:107-123).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -39,10 +39,13 @@ enum Counter {
     // (C_X_CS_ROWS / C_X_CS_ROWS_N: rows hashed by k_checksum3 or k_cs_delta / k_checksum_q16 launches, snapshots
     // included; C_X_CSD_SCANNED: rows k_csd_scan read)
     C_X_MERGED = C_NCOUNTERS, C_X_APPLIED, C_X_ISSUED, C_X_CS_ROWS, C_X_CS_DUP,
-    C_X_MERGED_R, C_X_APPLIED_R, C_X_RISSUED, C_X_RCALLS, C_X_BUMPED, C_X_CS_ROWS_N, C_X_CSD_SCANNED, C_NALL
+    C_X_MERGED_R, C_X_APPLIED_R, C_X_RISSUED, C_X_RCALLS, C_X_BUMPED, C_X_CS_ROWS_N, C_X_CSD_SCANNED,
+    // dense messages merged (MembershipAsChanges: full-sync responses in k_resp / k_resolve, reverse full syncs in
+    // k_jobs_merge, heal lists), and the changes the reverse full syncs applied
+    C_X_DENSE_RESP, C_X_DENSE_JOBS, C_X_JOBS_APPLIED, C_X_DENSE_HEAL, C_NALL
 };
 
-constexpr int CTR_SHARDS = 64, CTR_STRIDE = 40;   // d.ctr is [CTR_SHARDS][CTR_STRIDE] u64
+constexpr int CTR_SHARDS = 64, CTR_STRIDE = 48;   // d.ctr is [CTR_SHARDS][CTR_STRIDE] u64
 static_assert(C_NALL + 8 <= CTR_STRIDE, "counter block too small (8 diagnostic slots follow C_NALL)");
 constexpr uint32_t POOL_SHARDS = 64, POOL_CUR_STRIDE = 16;   // d.pool_cur is [POOL_SHARDS][POOL_CUR_STRIDE] u64
 
@@ -150,6 +153,31 @@ struct DS {
 __device__ __forceinline__ uint32_t hot_slot(const DS &d, uint32_t m) { return d.hidx ? d.hidx[m] : SRC_NONE; }
 
 __host__ __device__ inline bool is_pingable(uint32_t st) { return st <= ST_SUSPECT; }
+
+// A change record in the message pool is 16 B: {member | status << 24 | tag_lo << 27, e | tag_hi << 24, source,
+// source e} (e < 2^24: ensure_ecap). The 13-bit tag carries the member's hot slot in the receiving handle,
+// written by the issuer, which has just read the member's cell from that slot, so the merge, the bump and the
+// receiver's RecordChange test reach the hot word without the dependent hidx lookup: 0 = not known (the consumer looks
+// it up: heal diffs), k + 1 = slot k, RT_COLD = no slot. Slots are assigned only at the start of phase I, and records
+// never outlive their round (the pool restarts every round), so a tag stays right until its record is consumed;
+// k_x_unpack re-tags imported records with the receiving shard's own slots.
+constexpr uint32_t RT_LOOKUP = 0, RT_COLD = 8191, RT_MAXSLOTS = 8128;   // (hot slots per row at most RT_MAXSLOTS)
+__host__ __device__ inline uint32_t rec_m(const uint4 &r) { return r.x & 0xFFFFFFu; }
+__host__ __device__ inline uint32_t rec_st(const uint4 &r) { return (r.x >> 24) & 7u; }
+__host__ __device__ inline uint32_t rec_e(const uint4 &r) { return r.y & 0xFFFFFFu; }
+__host__ __device__ inline uint32_t rec_tag(const uint4 &r) { return (r.x >> 27) | ((r.y >> 24) << 5); }
+__host__ __device__ inline uint32_t tag_of_slot(uint32_t hk) { return hk == SRC_NONE ? RT_COLD : hk + 1u; }
+__host__ __device__ inline uint4 rec_make(uint32_t m, uint32_t st, uint32_t e, uint32_t src, uint32_t sinc, uint32_t tag) {
+    return make_uint4(m | (st << 24) | (tag << 27), e | ((tag >> 5) << 24), src, sinc);
+}
+__host__ __device__ inline uint4 rec_retag(const uint4 &r, uint32_t tag) {
+    return make_uint4((r.x & 0x07FFFFFFu) | (tag << 27), (r.y & 0xFFFFFFu) | ((tag >> 5) << 24), r.z, r.w);
+}
+// the hot slot of a record's member in this handle (SRC_NONE: none)
+__device__ __forceinline__ uint32_t rec_slot(const DS &d, const uint4 &r) {
+    const uint32_t t = rec_tag(r);
+    return t == RT_LOOKUP ? hot_slot(d, rec_m(r)) : t == RT_COLD ? SRC_NONE : t - 1u;
+}
 
 // shard that owns observer row o (G is small: a linear scan over the shard boundaries)
 __device__ __forceinline__ uint32_t owner_of(const DS &d, uint32_t o) {

@@ -43,11 +43,13 @@ struct Timed {
 // the profiler's; their deferred-decision epilogues are F_RECVFIN
 // With the reference-row path on, F_CS_WIDE times the k_cs_delta dispatches and F_CSD_SCAN the work before them
 // (reference row, reference string, k_csd_scan); rows it leaves to the production kernels are timed as they are.
+// F_CS_FALLBACK times the production launches after a reference-row launch (the rows it left; most of them exit at once)
+// F_JOBS_MERGE times exactly the k_jobs_merge dispatches (reverse full syncs, dense merges); F_JOBS the rest of phase F
 enum Fam { F_TIMERS, F_SELECT, F_ISSUE, F_SORT, F_RECV, F_RESP, F_PINGREQ, F_JOBS, F_CS_WIDE, F_CS_NARROW, F_CSPREP,
-           F_EVENTS, F_XCHG, F_RECVFIN, F_CSD_SCAN, F_NFAM };
+           F_EVENTS, F_XCHG, F_RECVFIN, F_CSD_SCAN, F_CS_FALLBACK, F_JOBS_MERGE, F_NFAM };
 const char *kFamName[F_NFAM] = {"timers", "select", "issue", "sort", "recv_merge", "resp_merge", "pingreq",
                                 "rfs_jobs", "checksum_wide", "checksum_narrow", "checksum_prep", "events", "exchange",
-                                "recv_finish", "checksum_delta_scan"};
+                                "recv_finish", "checksum_delta_scan", "checksum_fallback", "rfs_merge"};
 
 // ---------------------------------------------------------------------------------------------
 // shard transports: how parcels move between the shards of one cluster
@@ -174,12 +176,15 @@ struct RcclPort : Transport {
     }
     int sizes_dev(const uint64_t *dsend, uint64_t *drecv, int k, hipStream_t s) override {
         if (s != st) return SWIMSIM_EINVAL;                        // one order with data() / bcast()
-        ncclGroupStart();
-        for (uint32_t p = 0; p < G; p++) {
-            ncclSend(dsend + (size_t)p * k, k, ncclUint64, (int)p, comm, st);
-            ncclRecv(drecv + (size_t)p * k, k, ncclUint64, (int)p, comm, st);
+        // (every call's status is checked; a failed enqueue still closes the group, so the communicator stays usable
+        // for the error path's teardown)
+        ncclResult_t rc = ncclGroupStart();
+        for (uint32_t p = 0; p < G && rc == ncclSuccess; p++) {
+            rc = ncclSend(dsend + (size_t)p * k, k, ncclUint64, (int)p, comm, st);
+            if (rc == ncclSuccess) rc = ncclRecv(drecv + (size_t)p * k, k, ncclUint64, (int)p, comm, st);
         }
-        return ncclGroupEnd() == ncclSuccess ? 0 : SWIMSIM_EHIP;
+        const ncclResult_t rc_end = ncclGroupEnd();
+        return rc == ncclSuccess && rc_end == ncclSuccess ? 0 : SWIMSIM_EHIP;
     }
     int data(const uint8_t *sbuf, const uint64_t *soff, const uint64_t *sbytes, uint8_t *rbuf, const uint64_t *roff,
              const uint64_t *rbytes, hipStream_t s) override {
@@ -187,12 +192,13 @@ struct RcclPort : Transport {
             if (!order && hipEventCreateWithFlags(&order, hipEventDisableTiming) != hipSuccess) return SWIMSIM_EHIP;
             if (hipEventRecord(order, st) != hipSuccess || hipStreamWaitEvent(s, order, 0) != hipSuccess) return SWIMSIM_EHIP;
         }
-        ncclGroupStart();
-        for (uint32_t p = 0; p < G; p++) {
-            if (sbytes[p]) ncclSend(sbuf + soff[p], sbytes[p], ncclUint8, (int)p, comm, s);
-            if (rbytes[p]) ncclRecv(rbuf + roff[p], rbytes[p], ncclUint8, (int)p, comm, s);
+        ncclResult_t rc = ncclGroupStart();
+        for (uint32_t p = 0; p < G && rc == ncclSuccess; p++) {
+            if (sbytes[p]) rc = ncclSend(sbuf + soff[p], sbytes[p], ncclUint8, (int)p, comm, s);
+            if (rbytes[p] && rc == ncclSuccess) rc = ncclRecv(rbuf + roff[p], rbytes[p], ncclUint8, (int)p, comm, s);
         }
-        if (ncclGroupEnd() != ncclSuccess) return SWIMSIM_EHIP;    // stream-ordered: the unpack follows on s
+        const ncclResult_t rc_end = ncclGroupEnd();
+        if (rc != ncclSuccess || rc_end != ncclSuccess) return SWIMSIM_EHIP;   // stream-ordered: the unpack follows on s
         if (s != st && (hipEventRecord(order, s) != hipSuccess || hipStreamWaitEvent(st, order, 0) != hipSuccess))
             return SWIMSIM_EHIP;
         return 0;
@@ -303,6 +309,8 @@ struct swimsim {
     uint8_t *hflag = nullptr;
     uint32_t *H = nullptr, *nh = nullptr;
     uint32_t *keys_in = nullptr, *vals_out = nullptr;    // sorted inbox: receiver column, sender-value column
+    uint4 *pinfo = nullptr;                       // per sorted inbox pair: the sender's snapshot (k_pair_info), 32 B
+    uint32_t inbox_n = 0;                         // pairs of the last sorted inbox
     uint32_t *ukeys = nullptr, *counts = nullptr, *offs = nullptr, *nruns = nullptr, *info = nullptr;
     void *cub_tmp = nullptr;
     size_t cub_bytes = 0;
@@ -582,6 +590,7 @@ int read_counters(swimsim *h, uint64_t *out /* [CTR_STRIDE] */) {
 // --- sorting the (receiver << 32 | sender value) inbox keys and run-length encoding by receiver ---
 int sort_inbox(swimsim *h, uint32_t n, uint32_t *host_info) {
     Scope sc(h, F_SORT);
+    h->inbox_n = n;
     int endbit = 1;
     while ((1u << endbit) <= h->N) endbit++;
     size_t bytes = h->cub_bytes;
@@ -859,7 +868,9 @@ int csr_alloc(swimsim *h) {
         (rc = dalloc(h, &h->csr_fb, (size_t)rows, "csr fallback list")) ||
         (rc = dalloc(h, &h->csr_fbcnt, 8, "csr fallback count and reasons")) ||
         (rc = dalloc(h, &h->csr_rinfo, (size_t)rows, "csr row info")) ||
-        (rc = dalloc(h, &h->csr_ent, (size_t)rows * h->csr_ecap * 2, "csr exception entries")) ||
+        // (CSR_EREG spare entries past the last row: k_csr3's record stager loads a record's first CSR_EREG entries
+        // with it, wherever in the row's cap they start)
+        (rc = dalloc(h, &h->csr_ent, ((size_t)rows * h->csr_ecap + CSR_EREG) * 2, "csr exception entries")) ||
         (rc = dalloc(h, &h->csr_plan, (size_t)rows / CSR_ROWS + 1, "csr plans")) ||
         (rc = dalloc(h, &h->csr_rec, (size_t)rows * h->csr_rcap, "csr records")) ||
         (rc = dalloc(h, &h->csr_nrec, (size_t)rows, "csr record counts")) ||
@@ -931,6 +942,8 @@ int csr_hash(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t n, 
     a.fb_cnt = h->csr_fbcnt;
     a.exw = (h->fault_inject & 4) ? 8u : 0xFFFFFFFFu;
     a.stprio = (h->fault_inject & 16) ? 1u : 0u;
+    // (fault_inject 64: bits 8-11 the roles k_csr3 delays, bits 12-30 their seed)
+    a.jitter = (h->fault_inject & 64) ? (((uint32_t)h->fault_inject >> 8) & 15u) | ((uint32_t)h->fault_inject >> 12 << 8) : 0u;
     {
         Scope sc(h, F_CSD_SCAN);
         hipLaunchKernelGGL(k_csd_ref, dim3((h->N + 256) / 256), dim3(256), 0, h->s, h->d, list, n, h->csr_B, h->csr_Lb);
@@ -954,7 +967,7 @@ int csr_hash(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t n, 
     h->csr_launches++;
     // rows the path left: the production kernels, counts from the device (a launch with nothing to hash exits at
     // once; timed with the preparation so that the checksum families' launch counts stay those of real work)
-    Scope sc(h, F_CSPREP);
+    Scope sc(h, F_CS_FALLBACK);
     hipLaunchKernelGGL(k_csr_fbsplit, dim3(1), dim3(64), 0, h->s, h->csr_fbcnt, h->csr_fbsplit, h->csr_acc);
     launch_checksum_kind(h->d, h->csr_fb, h->csr_fbsplit, std::min(n, 4096u), CS_NARROW, h->s);
     if (n > 4096u) launch_checksum_kind(h->d, h->csr_fb + 4096, h->csr_fbsplit + 1, std::min(n - 4096u, 8192u), CS_NARROW, h->s);
@@ -1192,7 +1205,13 @@ int run_waves(swimsim *h, int phase, uint32_t nruns_valid, uint32_t maxcount) {
     a.defer_cnt = h->defer_cnt;
     a.fsflag = h->fsflag;
     a.r = h->round;
+    a.pinfo = h->pinfo;
     hipMemsetAsync(h->defer_cnt, 0, 4, h->s);
+    {
+        Scope sc(h, F_SORT);
+        hipLaunchKernelGGL(k_pair_info, dim3(blocks_for_threads(h->inbox_n)), dim3(256), 0, h->s, h->d, h->vals_out, h->inbox_n,
+                           phase, a.sdesc, a.sI, a.sC, a.sS, h->pinfo);
+    }
     {
         Scope sc(h, F_RECV);
         hipLaunchKernelGGL(k_recv, dim3(blocks_for_waves(nruns_valid)), dim3(SWIM_WAVE_BLOCK), 0, h->s, h->d, a);
@@ -1524,10 +1543,12 @@ int step_one(swimsim *h, const swimsim_event *ev, size_t nev) {
                            h->needcnt, h->xitems, h->xcnt, h->xcap);
         if (int rc = xchg(h)) return rc;
     }
+    for (uint32_t q = 0; q < h->maxjobs; q++) {
+        Scope sc(h, F_JOBS_MERGE);
+        hipLaunchKernelGGL(k_jobs_merge, dim3(blocks_for_waves(h->NL)), dim3(SWIM_WAVE_BLOCK), 0, h->s, h->d, q, h->snapdesc, r);
+    }
     {
         Scope sc(h, F_JOBS);
-        for (uint32_t q = 0; q < h->maxjobs; q++)
-            hipLaunchKernelGGL(k_jobs_merge, dim3(blocks_for_waves(h->NL)), dim3(SWIM_WAVE_BLOCK), 0, h->s, h->d, q, h->snapdesc, r);
         hipLaunchKernelGGL(k_jobs_reset, dim3(blocks_for_threads(std::max(h->NL, h->N))), dim3(256), 0, h->s, h->d,
                            h->need);
     }
@@ -1687,6 +1708,7 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
     if (tun && tun->cs_narrow_rows >= 0) h->cs_narrow_rows = (uint32_t)tun->cs_narrow_rows;
     if (tun && tun->cs_ref >= 0) h->csr_mode = tun->cs_ref;
     if (tun && tun->fault_inject > 0) h->fault_inject = tun->fault_inject;
+    if (h->fault_inject & 32) h->csr_ecap = 24;      // (tests: rows whose exception entries end within CSR_EREG of the cap)
 #ifdef SWIMSIM_DIAG                                 // diagnostics library only: the reference-row path
     if (const char *v = getenv("SWIMSIM_CS_DELTA")) h->csd_mode = atoi(v);
     if (const char *v = getenv("SWIMSIM_CS_DELTA_MAXDIFF")) h->csd_maxdiff = (uint32_t)strtoul(v, nullptr, 10);
@@ -1726,7 +1748,7 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
         // turns them off (results are the same either way)
         uint32_t hp = std::min<uint32_t>(2048u, h->NP);
         if (tun && tun->hot_slots >= 0) hp = std::min<uint32_t>((uint32_t)tun->hot_slots, h->NP);
-        hp = (hp + 63) & ~63u;
+        hp = std::min<uint32_t>((hp + 63) & ~63u, RT_MAXSLOTS);   // (a change record's tag names at most RT_MAXSLOTS)
         d.hidx = nullptr; d.hlist = nullptr; d.hmw = nullptr; d.hde = nullptr; d.hotnew = nullptr; d.hot_cnt = nullptr;
         d.HP = 0;
         if (hp) {
@@ -1816,6 +1838,7 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
         (rc = dalloc(h, &h->H, NLK, "H")) || (rc = dalloc(h, &h->nh, h->NL, "nh")) ||
         (rc = dalloc(h, &h->keys, KC, "keys")) || (rc = dalloc(h, &h->keys_sorted, KC, "keys_sorted")) ||
         (rc = dalloc(h, &h->keys_in, KC, "receivers")) || (rc = dalloc(h, &h->vals_out, KC, "vals_out")) ||
+        (rc = dalloc(h, &h->pinfo, (size_t)KC * 2, "inbox pair snapshots")) ||
         (rc = dalloc(h, &h->ukeys, KC, "ukeys")) || (rc = dalloc(h, &h->counts, KC, "counts")) ||
         (rc = dalloc(h, &h->offs, KC, "offs")) || (rc = dalloc(h, &h->nruns, 1, "nruns")) ||
         (rc = dalloc(h, &h->info, 8, "info")) || (rc = dalloc(h, &h->list, 3 * KC + 2 * (size_t)h->NL + 64, "list")) ||
@@ -2572,9 +2595,11 @@ int swimsim_enable_timing(swimsim_t *h, int32_t enable) {
     drain_timing(h);
     h->timing = enable != 0;
     // 1: every family; 2: the kernels the bench line's roofline reports (checksum chains, merges, issue): the other
-    // families' event pairs cost the timed window about 10 us each (a dozen per round)
-    h->timing_mask = enable == 2 ? (1u << F_CS_WIDE) | (1u << F_CS_NARROW) | (1u << F_RECV) | (1u << F_RESP) | (1u << F_ISSUE)
-                                 : (1u << F_NFAM) - 1u;
+    // families' event pairs cost the timed window about 10 us each (a dozen per round); 3: those and the reverse full
+    // syncs' dense merges (k_jobs_merge, maxjobs launches per round)
+    const uint32_t m2 = (1u << F_CS_WIDE) | (1u << F_CS_NARROW) | (1u << F_RECV) | (1u << F_RESP) | (1u << F_ISSUE) |
+                        (1u << F_CS_FALLBACK);
+    h->timing_mask = enable == 2 ? m2 : enable == 3 ? m2 | (1u << F_JOBS_MERGE) : (1u << F_NFAM) - 1u;
     for (int f = 0; f < F_NFAM; f++) { h->fam_ms[f] = 0; h->fam_n[f] = 0; }
     uint64_t c[CTR_STRIDE];
     if (int rc = read_counters(h, c)) return rc;
@@ -2619,6 +2644,9 @@ int swimsim_kernel_times(swimsim_t *h, const char **names, double *avg_ms, uint6
             if (f == F_ISSUE) b = issued * 32.0;
             if (f == F_RECV) b = merge_bytes + recv_issue_bytes;   // k_recv merges (and the few other
             if (f == F_RESP) b = resp_bytes;                        // merges) + its issue; k_resp
+            // reverse full syncs: SURVEY.md §8(d) dense batches stream the row, 5 B x N per merged snapshot, + 23 B per
+            // applied change
+            if (f == F_JOBS_MERGE) b = delta(C_X_DENSE_JOBS) * 5.0 * h->N + delta(C_X_JOBS_APPLIED) * 23.0;
             alg_bytes[f] = b;
         }
     }
@@ -2634,10 +2662,12 @@ int swimsim_kernel_units(swimsim_t *h, const char **names, double *values, size_
     static const char *kn[] = {"cs_rows_wide", "cs_rows_narrow", "cs_dup_rows", "recv_merged", "recv_applied",
                                "recv_issued", "recv_calls", "resp_merged", "resp_applied", "resp_bumped", "issued",
                                "bitmap_words_per_row", "diag_stamp0", "diag_stamp1", "diag_stamp2", "diag_stamp3",
-                               "hot_slots", "diag_stamp4", "diag_stamp5", "diag_stamp6", "diag_stamp7"};
+                               "hot_slots", "diag_stamp4", "diag_stamp5", "diag_stamp6", "diag_stamp7",
+                               "dense_resp", "dense_jobs", "jobs_applied", "dense_heal"};
     const int ki[] = {C_X_CS_ROWS, C_X_CS_ROWS_N, C_X_CS_DUP, C_X_MERGED, C_X_APPLIED, C_X_RISSUED, C_X_RCALLS,
                       C_X_MERGED_R, C_X_APPLIED_R, C_X_BUMPED, C_X_ISSUED, -1, C_NALL, C_NALL + 1, C_NALL + 2, C_NALL + 3,
-                      -2, C_NALL + 4, C_NALL + 5, C_NALL + 6, C_NALL + 7};
+                      -2, C_NALL + 4, C_NALL + 5, C_NALL + 6, C_NALL + 7, C_X_DENSE_RESP, C_X_DENSE_JOBS, C_X_JOBS_APPLIED,
+                      C_X_DENSE_HEAL};
     uint32_t hot = 0;                                              // hot slots in use now (not a delta)
     if (h->d.hot_cnt) {
         HIPCHK(h, hipMemcpyAsync(&hot, h->d.hot_cnt, 4, hipMemcpyDeviceToHost, h->s));

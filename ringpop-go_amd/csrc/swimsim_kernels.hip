@@ -116,10 +116,12 @@ __device__ __forceinline__ void colmark(const DS &d, uint32_t m) {
     if (!(__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit)) atomicOr(w, bit);
 }
 
-// cur = the row word d.mw[ol][m] (callers batch these loads)
+// cur = the row word d.mw[ol][m] (callers batch these loads), hk_in = m's hot slot (SRC_NONE: none; HK_LAZY: looked up
+// here, only when the change applies)
+constexpr uint32_t HK_LAZY = 0xFFFFFFFEu;
 __device__ __forceinline__ void merge_change_w(const DS &d, uint32_t ol, uint32_t o, uint32_t m, uint32_t cur, uint32_t cst,
                                                uint32_t ce, uint32_t csrc, uint32_t csinc, uint32_t now_e, uint32_t sched_r,
-                                               MAcc &acc) {
+                                               MAcc &acc, uint32_t hk_in = HK_LAZY) {
     const size_t idx = (size_t)ol * d.NP + m;
     const uint32_t cur_st = cur & 7u;
     uint32_t nst, ne, nsrc, nsinc;
@@ -136,7 +138,7 @@ __device__ __forceinline__ void merge_change_w(const DS &d, uint32_t ol, uint32_
         return;
     }
     const uint32_t nw_ = (ne << 3) | nst;
-    const uint32_t hk = hot_slot(d, m);
+    const uint32_t hk = hk_in == HK_LAZY ? hot_slot(d, m) : hk_in;
     const size_t hx = (size_t)ol * d.HP + hk;
     d.mw[idx] = nw_;
     if (hk != SRC_NONE) d.hmw[hx] = nw_;
@@ -230,6 +232,69 @@ __device__ __forceinline__ void wave_finalize(const DS &d, uint32_t ol, const MA
         fold_row(d, ol, dping, ddc, napp, nref, ev, dl, ml, inv, dfp, next_update, dnh);
         if (np && cset < 2) ctr_add(d, cset ? C_X_MERGED_R : C_X_MERGED, (unsigned long long)np);
         if (napp && cset < 2) ctr_add(d, cset ? C_X_APPLIED_R : C_X_APPLIED, (unsigned long long)napp);
+        if (napp && cset == 3) ctr_add(d, C_X_JOBS_APPLIED, (unsigned long long)napp);
+    }
+    __threadfence_block();
+}
+
+// The row scalars of observer row ol while one wave runs the row's Updates (a receiver's wave in k_recv, a sender's in
+// k_resp: no other wave writes them during the launch). They are loaded once, together with the first message's
+// records, kept current in registers and written back as they change, so an Update's epilogue (fold_row's reads),
+// IssueAsReceiver's count, maxP and cold-entry test and the full-sync branch's dirty / checksum reads cost no round
+// trip of their own (round 6: each was a dependent load on every message's path).
+struct RowPre {
+    int32_t nhe, ping, dcnt, clast, maxp;
+    uint32_t clen, dirty, cs, cpslot;
+    unsigned long long fp, useq;
+};
+// (wave-uniform by construction: readfirstlane tells the compiler so, and the copy lives in scalar registers instead of
+// 13 vector registers that k_recv's merge and issue loops would otherwise spill)
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+__device__ __forceinline__ unsigned long long uni64(unsigned long long x) {
+    return ((unsigned long long)uni((uint32_t)(x >> 32)) << 32) | uni((uint32_t)x);
+}
+__device__ __forceinline__ RowPre row_pre(const DS &d, uint32_t ol) {
+    RowPre p;
+    p.nhe = (int32_t)uni((uint32_t)d.nhe[ol]); p.ping = (int32_t)uni((uint32_t)d.ping[ol]);
+    p.dcnt = (int32_t)uni((uint32_t)d.dcnt[ol]); p.clast = (int32_t)uni((uint32_t)d.clast[ol]);
+    p.maxp = (int32_t)uni((uint32_t)d.maxp[ol]);
+    p.clen = uni(d.clen[ol]); p.dirty = uni(d.dirty[ol]); p.cs = uni(d.cs[ol]); p.cpslot = uni(d.cpslot[ol]);
+    p.fp = uni64(d.fp[ol]);
+    p.useq = d.useq ? uni64(d.useq[ol]) : 0ull;
+    return p;
+}
+
+// fold_row on the registers (every lane computes the same values; lane 0 writes what changed)
+__device__ __forceinline__ void fold_row_pre(const DS &d, uint32_t ol, RowPre &p, int dping, int ddc, int napp, int nref,
+                                             int evict, int dlen, int maxlast, int inval, unsigned long long dfp, int dnh) {
+    if (!(dnh | dping | ddc | napp | evict | dlen | inval) && !dfp && maxlast <= -1 && !nref) return;
+    const bool l0 = lane_id() == 0;
+    if (napp && d.useq) { p.useq += 1ull; if (l0) d.useq[ol] = p.useq; }
+    if (dnh) { p.nhe += dnh; if (l0) d.nhe[ol] = p.nhe; }
+    if (dfp) { p.fp += dfp; if (l0) d.fp[ol] = p.fp; }
+    if (dping) { p.ping += dping; if (l0) d.ping[ol] = p.ping; }
+    if (ddc) { p.dcnt += ddc; if (l0) d.dcnt[ol] = p.dcnt; }
+    if (napp) {
+        p.maxp = (int32_t)d.pfactor * digits10(p.ping);            // AdjustMaxPropagations
+        if (l0) { d.maxp[ol] = p.maxp; ctr_add(d, C_APPLIED, (unsigned long long)napp); }
+    }
+    if (napp || evict) { p.dirty = 1; if (l0) d.dirty[ol] = 1; }  // ComputeChecksum pending
+    if (dlen) { p.clen += (uint32_t)dlen; if (l0) d.clen[ol] = p.clen; }
+    if (maxlast > p.clast) { p.clast = maxlast; if (l0) d.clast[ol] = maxlast; }
+    else if (inval) { p.clast = -2; if (l0) d.clast[ol] = -2; }   // rescanned by the checksum kernel
+    if (nref && l0) ctr_add(d, C_REFUTES, (unsigned long long)nref);
+}
+
+__device__ __forceinline__ void wave_finalize_pre(const DS &d, uint32_t ol, const MAcc &acc, int cset, RowPre &p) {
+    const int dping = wsum(acc.dping), ddc = wsum(acc.ddc), napp = wsum(acc.napp), nref = wsum(acc.nref);
+    const int ev = wsum(acc.evict), np = wsum(acc.nproc), dl = wsum(acc.dlen), ml = wmax(acc.maxlast);
+    const int inv = wmax(acc.inval), dnh = wsum(acc.dnh);
+    const unsigned long long dfp = wsum64(acc.dfp);
+    fold_row_pre(d, ol, p, dping, ddc, napp, nref, ev, dl, ml, inv, dfp, dnh);
+    if (lane_id() == 0) {
+        if (np && cset < 2) ctr_add(d, cset ? C_X_MERGED_R : C_X_MERGED, (unsigned long long)np);
+        if (napp && cset < 2) ctr_add(d, cset ? C_X_APPLIED_R : C_X_APPLIED, (unsigned long long)napp);
+        if (napp && cset == 3) ctr_add(d, C_X_JOBS_APPLIED, (unsigned long long)napp);
     }
     __threadfence_block();
 }
@@ -279,11 +344,9 @@ __device__ __forceinline__ void wave_merge_dense(const DS &d, uint32_t ol, uint3
 }
 
 // merge a whole message into row ol (wave-wide; the changes of one message are distinct members)
-// cset selects the measurement counters (0: k_recv's C_X_MERGED/C_X_APPLIED, 1: k_resp's pair, 2: none)
-__device__ void wave_merge_msg(const DS &d, uint32_t ol, uint32_t o, const MsgDesc &md, uint32_t now_e, uint32_t sched_r,
-                               int cset = 0) {
-    MAcc acc;
-    acc_begin(d, ol, acc);
+// (dctr >= 0: the measurement counter a dense message adds one to)
+__device__ __forceinline__ void wave_merge_body(const DS &d, uint32_t ol, uint32_t o, const MsgDesc &md, uint32_t now_e,
+                                                uint32_t sched_r, MAcc &acc, int dctr) {
     const uint32_t *rowp = d.mw + (size_t)ol * d.NP;
     const uint32_t *hrow = d.hmw + (size_t)ol * d.HP;
     if (md.kind == 0) {
@@ -296,29 +359,48 @@ __device__ void wave_merge_msg(const DS &d, uint32_t ol, uint32_t o, const MsgDe
                 const uint32_t i = base + u * 64 + lane_id();
                 rec[u] = i < md.len ? d.pool[off + i] : make_uint4(0xFFFFFFFFu, 0, 0, 0);
             }
+            // (the record's tag names the member's hot slot: the row word is the second load of the chain, not the
+            // third after an hidx lookup)
 #pragma unroll
-            for (int u = 0; u < MB; u++) hk[u] = rec[u].x != 0xFFFFFFFFu ? hot_slot(d, rec[u].x & 0xFFFFFFu) : SRC_NONE;
+            for (int u = 0; u < MB; u++) hk[u] = rec[u].x != 0xFFFFFFFFu ? rec_slot(d, rec[u]) : SRC_NONE;
 #pragma unroll
             for (int u = 0; u < MB; u++)
-                cur[u] = rec[u].x == 0xFFFFFFFFu ? 0u : hk[u] != SRC_NONE ? hrow[hk[u]] : rowp[rec[u].x & 0xFFFFFFu];
+                cur[u] = rec[u].x == 0xFFFFFFFFu ? 0u : hk[u] != SRC_NONE ? hrow[hk[u]] : rowp[rec_m(rec[u])];
 #pragma unroll
             for (int u = 0; u < MB; u++)
                 if (rec[u].x != 0xFFFFFFFFu)
-                    merge_change_w(d, ol, o, rec[u].x & 0xFFFFFFu, cur[u], rec[u].x >> 24, rec[u].y, rec[u].z, rec[u].w, now_e,
-                                   sched_r, acc);
+                    merge_change_w(d, ol, o, rec_m(rec[u]), cur[u], rec_st(rec[u]), rec_e(rec[u]), rec[u].z, rec[u].w, now_e,
+                                   sched_r, acc, hk[u]);
         }
     } else if (md.kind == 1) {
         wave_merge_dense(d, ol, o, md, now_e, sched_r, acc);
+        if (dctr >= 0 && lane_id() == 0) ctr_add(d, dctr, 1ull);
     }
     __threadfence_block();
+}
+// cset selects the measurement counters (0: k_recv's C_X_MERGED/C_X_APPLIED, 1: k_resp's pair, 2: none, 3: the reverse
+// full syncs' C_X_JOBS_APPLIED)
+__device__ void wave_merge_msg(const DS &d, uint32_t ol, uint32_t o, const MsgDesc &md, uint32_t now_e, uint32_t sched_r,
+                               int cset = 0, int dctr = -1) {
+    MAcc acc;
+    acc_begin(d, ol, acc);
+    wave_merge_body(d, ol, o, md, now_e, sched_r, acc, dctr);
     wave_finalize(d, ol, acc, cset);
 }
+// the same on a wave's register copy of the row scalars (RowPre)
+__device__ __forceinline__ void wave_merge_msg_pre(const DS &d, uint32_t ol, uint32_t o, const MsgDesc &md, uint32_t now_e,
+                                                   uint32_t sched_r, int cset, RowPre &p, int dctr = -1) {
+    MAcc acc;
+    acc.tag = p.useq;
+    wave_merge_body(d, ol, o, md, now_e, sched_r, acc, dctr);
+    wave_finalize_pre(d, ol, acc, cset, p);
+}
 
-// bumpPiggybackCounters over a sparse list (disseminator.go:135-149)
-__device__ void wave_bump(const DS &d, uint32_t ol, const MsgDesc &md) {
-    if (md.kind != 0) return;
+// bumpPiggybackCounters over a sparse list (disseminator.go:135-149); returns the wave's deleted entries (all, and those
+// of members without a hot slot) for the caller to fold into the row's counts
+__device__ __forceinline__ int2 wave_bump_body(const DS &d, uint32_t ol, const MsgDesc &md, int maxp) {
+    if (md.kind != 0) return make_int2(0, 0);
     const unsigned long long off = ((unsigned long long)md.off_hi << 32) | md.off_lo;
-    const int maxp = d.maxp[ol];
     uint32_t *dx = (uint32_t *)(d.dent + (size_t)ol * d.NP);       // word 0 of each entry, stride 2
     uint32_t *hx = (uint32_t *)(d.hde + (size_t)ol * d.HP);        // the same in the hot columns
     int del = 0, delnh = 0;
@@ -327,10 +409,11 @@ __device__ void wave_bump(const DS &d, uint32_t ol, const MsgDesc &md) {
 #pragma unroll
         for (int u = 0; u < MB; u++) {
             const uint32_t i = base + u * 64 + lane_id();
-            m[u] = i < md.len ? (d.pool[off + i].x & 0xFFFFFFu) : 0xFFFFFFFFu;
+            const uint2 xy = i < md.len ? *(const uint2 *)(d.pool + off + i) : make_uint2(0xFFFFFFFFu, 0u);
+            const uint4 r = make_uint4(xy.x, xy.y, 0u, 0u);
+            m[u] = xy.x != 0xFFFFFFFFu ? rec_m(r) : 0xFFFFFFFFu;
+            hk[u] = xy.x != 0xFFFFFFFFu ? rec_slot(d, r) : SRC_NONE;    // (the record's tag: no hidx lookup)
         }
-#pragma unroll
-        for (int u = 0; u < MB; u++) hk[u] = m[u] != 0xFFFFFFFFu ? hot_slot(d, m[u]) : SRC_NONE;
 #pragma unroll
         for (int u = 0; u < MB; u++)
             x[u] = m[u] == 0xFFFFFFFFu ? DE_NONE : hk[u] != SRC_NONE ? hx[(size_t)hk[u] * 2] : dx[(size_t)m[u] * 2];
@@ -351,10 +434,20 @@ __device__ void wave_bump(const DS &d, uint32_t ol, const MsgDesc &md) {
             else dx[(size_t)m[u] * 2] = nx;
         }
     }
-    del = wsum(del);
-    delnh = wsum(delnh);
-    if (lane_id() == 0 && del) d.dcnt[ol] -= del;
-    if (lane_id() == 0 && delnh) d.nhe[ol] -= delnh;
+    return make_int2(wsum(del), wsum(delnh));
+}
+__device__ void wave_bump(const DS &d, uint32_t ol, const MsgDesc &md) {
+    if (md.kind != 0) return;
+    const int2 dd = wave_bump_body(d, ol, md, d.maxp[ol]);
+    if (lane_id() == 0 && dd.x) d.dcnt[ol] -= dd.x;
+    if (lane_id() == 0 && dd.y) d.nhe[ol] -= dd.y;
+    __threadfence_block();
+}
+__device__ __forceinline__ void wave_bump_pre(const DS &d, uint32_t ol, const MsgDesc &md, RowPre &p) {
+    if (md.kind != 0) return;
+    const int2 dd = wave_bump_body(d, ol, md, p.maxp);
+    if (dd.x) { p.dcnt -= dd.x; if (lane_id() == 0) d.dcnt[ol] = p.dcnt; }
+    if (dd.y) { p.nhe -= dd.y; if (lane_id() == 0) d.nhe[ol] = p.nhe; }
     __threadfence_block();
 }
 
@@ -363,26 +456,26 @@ __device__ void wave_bump(const DS &d, uint32_t ol, const MsgDesc &md) {
 // serialised the 65,536 issues of a cascade round. A wave starts at the sub-pool of its wave id and moves on
 // to the next one only when its records do not fit, so the pool fails only when every sub-pool is full. A
 // sub-pool's cursor only moves when the records fit (compare-and-swap), so a failed attempt strands no space;
-// swimsim_create requires every sub-pool to hold N records, the longest message.
+// swimsim_create requires every sub-pool to hold N records, the longest message. (A fetch-add instead, one round trip
+// fewer, stranded each overflowing attempt's sub-pool tail: config 4's heal messages then overflowed a sharded pool.
+// k_recv hides the allocation's round trips behind its merge instead, recv_one_pre.)
+__device__ __forceinline__ unsigned long long pool_alloc_lane0(const DS &d, uint32_t n) {
+    const unsigned long long sub = d.pool_cap / POOL_SHARDS;
+    for (uint32_t t = 0, s = wave_gid() % POOL_SHARDS; t < POOL_SHARDS; t++, s = (s + 1) % POOL_SHARDS) {
+        unsigned long long *cur = d.pool_cur + (size_t)s * POOL_CUR_STRIDE;
+        unsigned long long old = __hip_atomic_load(cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while (old + n <= sub) {
+            const unsigned long long seen = atomicCAS(cur, old, old + n);
+            if (seen == old) return s * sub + old;
+            old = seen;
+        }
+    }
+    atomicOr(d.err, E_POOL);
+    return ~0ull;
+}
 __device__ __forceinline__ unsigned long long pool_alloc(const DS &d, uint32_t n) {
     unsigned long long off = 0;
-    if (lane_id() == 0 && n) {
-        const unsigned long long sub = d.pool_cap / POOL_SHARDS;
-        off = ~0ull;
-        for (uint32_t t = 0, s = wave_gid() % POOL_SHARDS; t < POOL_SHARDS && off == ~0ull; t++, s = (s + 1) % POOL_SHARDS) {
-            unsigned long long *cur = d.pool_cur + (size_t)s * POOL_CUR_STRIDE;
-            unsigned long long old = __hip_atomic_load(cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            while (old + n <= sub) {
-                const unsigned long long seen = atomicCAS(cur, old, old + n);
-                if (seen == old) {
-                    off = s * sub + old;
-                    break;
-                }
-                old = seen;
-            }
-        }
-        if (off == ~0ull) atomicOr(d.err, E_POOL);
-    }
+    if (lane_id() == 0 && n) off = pool_alloc_lane0(d, n);
     return bcast64(off);
 }
 
@@ -399,17 +492,12 @@ __device__ __forceinline__ uint32_t wscan_excl(uint32_t v, uint32_t &total) {
 // (sender, sinc), bump the rest (p++, delete at maxP). Otherwise IssueAsSender
 // (disseminator.go:128-133,201-215). Records are in member order within a lane's range; the order of
 // a message does not matter (its changes are distinct members).
+// (the body: cnt entries, maxP, the walk, the slots in use and the pool offset of cnt records are the caller's;
+// returns the records written, and for RECV the deleted entries in del / delnh, wave sums)
 template <bool RECV>
-__device__ uint32_t wave_issue_t(const DS &d, uint32_t ol, uint32_t sender, uint32_t sinc, MsgDesc &out) {
-    // (the row's reads in one round trip, before the pool allocation's returning atomic)
-    const uint32_t cnt = (uint32_t)d.dcnt[ol];
-    const int maxp = RECV ? d.maxp[ol] : 0;
-    const bool hotwalk = d.hidx && d.nhe[ol] == 0;
-    const uint32_t nslots = d.hidx ? d.hot_cnt[0] : 0u;
-    out.kind = 0; out.len = 0; out.off_lo = out.off_hi = 0;
-    if (cnt == 0) return 0;
-    const unsigned long long off = pool_alloc(d, cnt);
-    if (off == ~0ull) return 0;
+__device__ __forceinline__ uint32_t wave_issue_body(const DS &d, uint32_t ol, uint32_t sender, uint32_t sinc, MsgDesc &out,
+                                                    uint32_t cnt, int maxp, bool hotwalk, uint32_t nslots,
+                                                    unsigned long long off, int &del_out, int &delnh_out) {
     const size_t rb = (size_t)ol * d.NP, hb = (size_t)ol * d.HP;
     uint32_t *bits = d.dbit + (size_t)ol * d.NBIT;
     uint32_t pos = 0;
@@ -442,7 +530,7 @@ __device__ uint32_t wave_issue_t(const DS &d, uint32_t ol, uint32_t sender, uint
             for (int u = 0; u < MB; u++) {
                 if (!keep[u]) continue;
                 const uint32_t st = (wv[u] & 7u) == ST_UNKNOWN ? ST_TOMB : (wv[u] & 7u);   // evicted: (tombstone, inc)
-                if (at < cnt) d.pool[off + at] = make_uint4(m[u] | (st << 24), wv[u] >> 3, de_src(ce[u].x), ce[u].y);
+                if (at < cnt) d.pool[off + at] = rec_make(m[u], st, wv[u] >> 3, de_src(ce[u].x), ce[u].y, base + u * 64 + lane_id() + 1u);
                 at++;
                 if (RECV) {                                                   // bump
                     const uint32_t k = base + u * 64 + lane_id();
@@ -519,7 +607,7 @@ __device__ uint32_t wave_issue_t(const DS &d, uint32_t ol, uint32_t sender, uint
             for (int k = 0; k < MB; k++) {
                 if (!keep[k]) continue;
                 const uint32_t st = (wv[k] & 7u) == ST_UNKNOWN ? ST_TOMB : (wv[k] & 7u);   // evicted: (tombstone, inc)
-                if (at < cnt) d.pool[off + at] = make_uint4(m[k] | (st << 24), wv[k] >> 3, sr[k].x, sr[k].y);
+                if (at < cnt) d.pool[off + at] = rec_make(m[k], st, wv[k] >> 3, sr[k].x, sr[k].y, tag_of_slot(hk[k]));
                 at++;
                 if (RECV) {                                                   // bump
                     uint32_t nx;
@@ -546,18 +634,36 @@ __device__ uint32_t wave_issue_t(const DS &d, uint32_t ol, uint32_t sender, uint
         }
     }
     if (RECV) {
-        del = wsum(del);
-        delnh = wsum(delnh);
-        if (lane_id() == 0 && del) d.dcnt[ol] -= del;
-        if (lane_id() == 0 && delnh) d.nhe[ol] -= delnh;
+        del_out = wsum(del);
+        delnh_out = wsum(delnh);
     } else if (pos != cnt && lane_id() == 0) {
         atomicOr(d.err, E_COUNT);
     }
-    __threadfence_block();
     out.off_lo = (uint32_t)off;
     out.off_hi = (uint32_t)(off >> 32);
     out.len = min(pos, cnt);
     return out.len;
+}
+
+template <bool RECV>
+__device__ uint32_t wave_issue_t(const DS &d, uint32_t ol, uint32_t sender, uint32_t sinc, MsgDesc &out) {
+    // (the row's reads in one round trip, before the pool allocation's returning atomic)
+    const uint32_t cnt = (uint32_t)d.dcnt[ol];
+    const int maxp = RECV ? d.maxp[ol] : 0;
+    const bool hotwalk = d.hidx && d.nhe[ol] == 0;
+    const uint32_t nslots = d.hidx ? d.hot_cnt[0] : 0u;
+    out.kind = 0; out.len = 0; out.off_lo = out.off_hi = 0;
+    if (cnt == 0) return 0;
+    const unsigned long long off = pool_alloc(d, cnt);
+    if (off == ~0ull) return 0;
+    int del = 0, delnh = 0;
+    const uint32_t n = wave_issue_body<RECV>(d, ol, sender, sinc, out, cnt, maxp, hotwalk, nslots, off, del, delnh);
+    if (RECV) {
+        if (lane_id() == 0 && del) d.dcnt[ol] -= del;
+        if (lane_id() == 0 && delnh) d.nhe[ol] -= delnh;
+    }
+    __threadfence_block();
+    return n;
 }
 
 // issueChanges / IssueAsSender (disseminator.go:128-133,201-215): snapshot of every entry
@@ -1011,19 +1117,21 @@ __global__ void k_issue(DS d, int mode, const int32_t *tgt, const uint8_t *faile
     if (mode == 0 && tgt[ol] < 0) return;
     if (mode == 1 && !failed[ol]) return;
     const uint32_t o = d.lo + ol;
+    // (the row's other reads go with the issue's own first loads: nothing below waits for a round trip of its own)
+    const uint32_t dirty = d.dirty[ol], cpslot = d.cpslot[ol], cs = d.cs[ol], selfw = d.mw[(size_t)ol * d.NP + o];
     MsgDesc md;
     wave_issue(d, ol, md);
     uint32_t slot = SRC_NONE;
-    if (sS && d.dirty[ol]) {
+    if (sS && dirty) {
         MsgDesc sn;
         if (wave_snapshot(d, ol, o, sn)) slot = sn.off_lo;
     } else if (sS) {
-        slot = d.cpslot[ol];                                     // clean, checksum still on the side stream
+        slot = cpslot;                                           // clean, checksum still on the side stream
     }
     if (lane_id() == 0) {
         sdesc[o] = md;                                               // message descriptors are indexed by
-        sI[o] = d.mw[(size_t)ol * d.NP + o] >> 3;                    // global sender id (remote senders'
-        sC[o] = slot == SRC_NONE ? d.cs[ol] : 0u;                    // messages are imported there)
+        sI[o] = selfw >> 3;                                          // global sender id (remote senders'
+        sC[o] = slot == SRC_NONE ? cs : 0u;                          // messages are imported there)
         if (sS) sS[o] = slot;
         if (mode == 0) {
             ctr_add(d, C_PINGS, 1ull);
@@ -1146,6 +1254,8 @@ __global__ void k_runs_info(const uint32_t *ukeys, const uint32_t *counts, const
 // ---------------------------------------------------------------------------------------------
 struct RecvArgs {
     const uint32_t *ukeys, *counts, *offs, *vals;   // run-length encoded sorted inbox
+    const uint4 *pinfo;                             // per inbox pair (k_pair_info): {sender's message descriptor},
+                                                    // {I_o, C_o, lazy slot, sender value}
     uint32_t nruns_max;
     int phase;                                      // 0: direct ping (phase D), 1: ping-req (Q2)
     const MsgDesc *sdesc;                           // sender snapshots (by global sender id)
@@ -1159,38 +1269,76 @@ struct RecvArgs {
     uint32_t r;
 };
 
+// the inbox pairs' sender snapshots in pair order (one thread per pair, after the inbox sort): a receiver's wave then
+// reads its message's descriptor and the sender's I_o, C_o and lazy slot with one load that depends only on its run's
+// offset, instead of the pair's sender value and then four arrays indexed by it (two dependent round trips)
+__global__ void k_pair_info(const DS d, const uint32_t *vals, uint32_t n, int phase, const MsgDesc *sdesc, const uint32_t *sI,
+                            const uint32_t *sC, const uint32_t *sS, uint4 *pinfo) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t v = vals[i], sender = phase == 0 ? v : v / d.K;
+    if (sender >= d.N) return;                                     // (sentinel keys: no receiver reads them)
+    const MsgDesc md = sdesc[sender];
+    pinfo[2 * (size_t)i] = make_uint4(md.off_lo, md.off_hi, md.len, md.kind);
+    pinfo[2 * (size_t)i + 1] = make_uint4(sI[sender], sC[sender], sS ? sS[sender] : SRC_NONE, v);
+}
+
 // the full-sync branch of IssueAsReceiver (disseminator.go:161-180): taken iff the filtered list is
 // empty and checksums differ. A dirty receiver snapshots its row (the full-sync payload) and the
 // decision waits for one batched checksum of all snapshots after the last wave. Reverse full syncs
 // are queued afterwards in inbox order (k_build_jobs).
-__device__ __forceinline__ void recv_one(const DS &d, const RecvArgs &a, uint32_t j, uint32_t sender, uint32_t resp_idx,
-                         uint32_t pair) {
+// On the receiver's register copy of its row scalars (RowPre). The response's records are reserved before the
+// merge with a bound (the entries before it + the message's changes), so the pool cursor's round trips run beside the
+// merge's gathers. The bound may be twice the need, so a round of long buffers would fill the pool with it (config 4's
+// heal rounds did, sharded): a dense message, or a bound above 4,096 records or a sixteenth of a sub-pool, allocates
+// the exact count after the merge (at most 4,096 spare records per receiver).
+__device__ __forceinline__ void recv_one_pre(const DS &d, const RecvArgs &a, uint32_t j, const uint4 pi0, const uint4 pi1,
+                                             uint32_t pair, uint32_t nslots, RowPre &p) {
     const uint32_t ol = j - d.lo;
-    const uint32_t sender_row = sender;                             // descriptor index = global sender id
-    wave_merge_msg(d, ol, j, a.sdesc[sender_row], a.r, a.r);
+    const uint32_t v = pi1.w, sender = a.phase == 0 ? v : v / d.K, resp_idx = v;
+    MsgDesc md;
+    md.off_lo = pi0.x; md.off_hi = pi0.y; md.len = pi0.z; md.kind = pi0.w;
+    const uint64_t bound = (uint64_t)(uint32_t)p.dcnt + md.len;
+    const bool early = md.kind == 0 && bound > 0 && bound <= min(4096ull, d.pool_cap / POOL_SHARDS / 16);
+    unsigned long long roff = 0;
+    if (early && lane_id() == 0) roff = pool_alloc_lane0(d, (uint32_t)bound);   // (read after the merge)
+    wave_merge_msg_pre(d, ol, j, md, a.r, a.r, 0, p);
     MsgDesc resp;
-    const uint32_t kept = wave_issue_recv(d, ol, sender, a.sI[sender_row], resp);
+    resp.kind = 0; resp.len = 0; resp.off_lo = resp.off_hi = 0;
+    uint32_t kept = 0;
+    const uint32_t cnt = (uint32_t)p.dcnt;
+    if (cnt) {
+        const unsigned long long off = early ? bcast64(roff) : pool_alloc(d, cnt);
+        if (off != ~0ull) {
+            int del = 0, delnh = 0;
+            kept = wave_issue_body<true>(d, ol, sender, pi1.x, resp, cnt, p.maxp, d.hidx && p.nhe == 0, nslots, off, del,
+                                         delnh);
+            if (del) { p.dcnt -= del; if (lane_id() == 0) d.dcnt[ol] = p.dcnt; }
+            if (delnh) { p.nhe -= delnh; if (lane_id() == 0) d.nhe[ol] = p.nhe; }
+            __threadfence_block();
+        }
+    }
     if (lane_id() == 0) {
         ctr_add(d, C_X_RISSUED, (unsigned long long)kept);
         ctr_add(d, C_X_RCALLS, 1ull);
     }
     if (kept == 0) {
-        const uint32_t scs = a.sC[sender_row];
-        const uint32_t sslot = a.sS ? a.sS[sender_row] : SRC_NONE;
-        const bool rdirty = d.dirty[ol] != 0;
-        const uint32_t rpend = rdirty ? SRC_NONE : d.cpslot[ol];   // clean; its checksum is on the side stream
+        const uint32_t scs = pi1.y;
+        const uint32_t sslot = a.sS ? pi1.z : SRC_NONE;
+        const bool rdirty = p.dirty != 0;
+        const uint32_t rpend = rdirty ? SRC_NONE : p.cpslot;          // clean; its checksum is on the side stream
         if (rdirty || rpend != SRC_NONE || sslot != SRC_NONE) {
             // a checksum is not known yet: snapshot the receiver (the full-sync payload if the decision goes that
             // way) and decide after the batched checksum of every deferred snapshot
             if (wave_snapshot(d, ol, j, resp) && lane_id() == 0) {
                 if (rpend != SRC_NONE) d.dense_meta[resp.off_lo].w = rpend + 1u;   // read after the side stream
-                else if (!rdirty) d.dense_cs[resp.off_lo] = d.cs[ol];
+                else if (!rdirty) d.dense_cs[resp.off_lo] = p.cs;
                 a.defer[atomicAdd(a.defer_cnt, 1u)] =
                     make_uint4(resp_idx | (rdirty ? 0x80000000u : 0u), resp.off_lo, sslot != SRC_NONE ? sslot : scs,
                                pair | (sslot != SRC_NONE ? 0x80000000u : 0u));
             }
             resp.kind = 2;
-        } else if (d.cs[ol] != scs) {
+        } else if (p.cs != scs) {
             wave_snapshot(d, ol, j, resp);
             if (lane_id() == 0) {
                 if (a.phase == 0) a.fsflag[pair] = 1;
@@ -1203,7 +1351,7 @@ __device__ __forceinline__ void recv_one(const DS &d, const RecvArgs &a, uint32_
         if (resp.kind != 2) ctr_add(d, C_MSG_CHANGES, (unsigned long long)resp.len);
         if (a.phase == 1) {
             ctr_add(d, C_HELPER_CALLS, 1ull);
-            ctr_add(d, C_MSG_CHANGES, (unsigned long long)a.sdesc[sender_row].len);
+            ctr_add(d, C_MSG_CHANGES, (unsigned long long)md.len);
         }
     }
 }
@@ -1211,10 +1359,11 @@ __device__ __forceinline__ void recv_one(const DS &d, const RecvArgs &a, uint32_
 // One wave per receiver runs its whole inbox in sender order. Receivers are independent within the
 // phase: a receiver writes only its own row, dissemination buffer and timers, and reads only the
 // senders' issue-time snapshots (S_o, I_o, C_o). So this equals the wave-by-wave schedule of
-// docs/ROUND_SEMANTICS.md §4 D, without a launch per inbox position.
+// docs/ROUND_SEMANTICS.md §4 D, without a launch per inbox position. The receiver's row scalars are loaded once
+// (RowPre) beside its first pair's snapshot, and the next pair's snapshot is loaded while a message is merged.
 // launch bounds: 256 threads (SWIM_WAVE_BLOCK) and at least RECV_MIN_WAVES waves per SIMD. The receive waves are
-// gather-latency bound (each message is a chain of dependent loads: record, hot index, row word, then the stores), so
-// resident waves, not registers, set the pace
+// gather-latency bound (each message is a chain of dependent loads: pair snapshot, record, row word, then the stores),
+// so resident waves, not registers, set the pace
 #ifndef RECV_MIN_WAVES
 #define RECV_MIN_WAVES 4
 #endif
@@ -1224,10 +1373,11 @@ __global__ void __launch_bounds__(256, RECV_MIN_WAVES) k_recv(DS d, RecvArgs a) 
     const uint32_t key = a.ukeys[u];
     if (key >= d.N) return;
     const uint32_t n = a.counts[u], off = a.offs[u];
+    RowPre p = row_pre(d, key - d.lo);
+    const uint32_t nslots = d.hidx ? d.hot_cnt[0] : 0u;
     for (uint32_t w = 0; w < n; w++) {
         const uint32_t pair = off + w;
-        const uint32_t v = a.vals[pair];
-        recv_one(d, a, key, a.phase == 0 ? v : v / d.K, v, pair);
+        recv_one_pre(d, a, key, a.pinfo[2 * (size_t)pair], a.pinfo[2 * (size_t)pair + 1], pair, nslots, p);
     }
 }
 
@@ -1445,11 +1595,14 @@ __global__ void k_resp(DS d, const int32_t *tgt, const uint8_t *failed, const Ms
     if (ol >= d.NL) return;
     if (tgt[ol] < 0 || failed[ol]) return;
     const uint32_t o = d.lo + ol;
-    wave_bump(d, ol, sdesc[o]);
-    wave_merge_msg(d, ol, o, rdesc[o], r, r, 1);
+    // (the row scalars, both descriptors: one round trip; RowPre carries them through the bump and the merge)
+    RowPre p = row_pre(d, ol);
+    const MsgDesc sd = sdesc[o], rd = rdesc[o];
+    wave_bump_pre(d, ol, sd, p);
+    wave_merge_msg_pre(d, ol, o, rd, r, r, 1, p, C_X_DENSE_RESP);
     if (lane_id() == 0) {
         ctr_add(d, C_PINGS_OK, 1ull);
-        if (sdesc[o].kind == 0) ctr_add(d, C_X_BUMPED, (unsigned long long)sdesc[o].len);
+        if (sd.kind == 0) ctr_add(d, C_X_BUMPED, (unsigned long long)sd.len);
     }
 }
 
@@ -1466,7 +1619,7 @@ __global__ void k_resolve(DS d, const int32_t *tgt, const uint8_t *failed, const
             errs++;
             wave_bump(d, ol, sdesc2[o]);                            // bump only on error (105-106)
         } else {
-            wave_merge_msg(d, ol, o, rdesc2[(size_t)o * K + q], r, r, 2);
+            wave_merge_msg(d, ol, o, rdesc2[(size_t)o * K + q], r, r, 2, C_X_DENSE_RESP);
         }
     }
     if (lane_id() == 0) {
@@ -1503,7 +1656,7 @@ __global__ void k_jobs_merge(DS d, uint32_t q, const MsgDesc *snapdesc, uint32_t
     const uint32_t ol = wave_gid();
     if (ol >= d.NL || d.njobs[ol] <= q) return;
     const uint32_t src = d.jobs[(size_t)ol * d.maxjobs + q];
-    wave_merge_msg(d, ol, d.lo + ol, snapdesc[src], r, r, 2);
+    wave_merge_msg(d, ol, d.lo + ol, snapdesc[src], r, r, 3, C_X_DENSE_JOBS);
     if (lane_id() == 0) ctr_add(d, C_RFS_DONE, 1ull);
 }
 
@@ -1667,8 +1820,8 @@ __global__ void k_heal_diff(DS d, const MsgDesc *ma, const MsgDesc *mb, MsgDesc 
             }
         }
         const unsigned long long ma_ = __ballot(wa), mb_ = __ballot(wb);
-        if (wa && oa != ~0ull) d.pool[oa + pa + __popcll(ma_ & lanemask_lt())] = make_uint4(m | (ST_SUSPECT << 24), b >> 3, SRC_NONE, 0);
-        if (wb && ob != ~0ull) d.pool[ob + pb + __popcll(mb_ & lanemask_lt())] = make_uint4(m | (ST_SUSPECT << 24), a >> 3, SRC_NONE, 0);
+        if (wa && oa != ~0ull) d.pool[oa + pa + __popcll(ma_ & lanemask_lt())] = rec_make(m, ST_SUSPECT, b >> 3, SRC_NONE, 0, RT_LOOKUP);
+        if (wb && ob != ~0ull) d.pool[ob + pb + __popcll(mb_ & lanemask_lt())] = rec_make(m, ST_SUSPECT, a >> 3, SRC_NONE, 0, RT_LOOKUP);
         pa += __popcll(ma_);
         pb += __popcll(mb_);
     }
@@ -1686,7 +1839,7 @@ __global__ void k_sender_info(DS d, uint32_t ol, uint32_t *out) {
 }
 
 __global__ void k_apply_msg(DS d, uint32_t ol, const MsgDesc *md, uint32_t r) {
-    wave_merge_msg(d, ol, d.lo + ol, *md, r, r, 2);
+    wave_merge_msg(d, ol, d.lo + ol, *md, r, r, 2, C_X_DENSE_HEAL);
 }
 
 // sendPingWithChanges o → t whose response is discarded (heal_partition.go:97-124): target runs

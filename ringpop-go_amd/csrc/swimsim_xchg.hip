@@ -163,7 +163,18 @@ __global__ void k_x_unpack(DS d, XArgs x, const uint8_t *buf, const ulonglong2 *
     if (h.kind == 0 && h.len) {                                    // change records → local pool
         const unsigned long long off = pool_alloc(d, h.len);
         if (off == ~0ull) return;
-        wave_copy16(d.pool + off, payload, h.len);
+        // (re-tagged with this shard's hot slots: the sender's tags name the sender shard's slots, DS record format)
+        for (uint32_t i = lane_id(); i < h.len; i += 64 * SNAP_MB) {
+            uint4 v[SNAP_MB];
+            uint32_t hk[SNAP_MB];
+#pragma unroll
+            for (int u = 0; u < SNAP_MB; u++) v[u] = i + 64u * u < h.len ? payload[i + 64u * u] : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+            for (int u = 0; u < SNAP_MB; u++) hk[u] = i + 64u * u < h.len ? hot_slot(d, rec_m(v[u])) : SRC_NONE;
+#pragma unroll
+            for (int u = 0; u < SNAP_MB; u++)
+                if (i + 64u * u < h.len) d.pool[off + i + 64u * u] = rec_retag(v[u], tag_of_slot(hk[u]));
+        }
         md.off_lo = (uint32_t)off;
         md.off_hi = (uint32_t)(off >> 32);
     } else if (h.kind == 1) {                                      // dense snapshot → local dense pool

@@ -564,7 +564,7 @@ class Cluster:
     # (rows the reference-row path left to the production kernels, by reason; the diagnostics library's round-3 path
     # reports its own reasons in the same slots: entry batch in "record_cap", jump slots and window misses in 5 and 6)
     CSD_REASONS = ("short", "entry_cap", "window_plan", "record_cap", "exception_slots", "reserved5", "reserved6",
-                   "reserved7")
+                   "declined_launches")
 
     def checksum_path_stats(self):
         dl, fb = C.c_uint64(), C.c_uint64()

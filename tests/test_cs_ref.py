@@ -169,3 +169,48 @@ def test_dedup_fingerprint_collision_groups():
             ora.step(ev)
             bad = np.nonzero(eng.checksums() != ora.checksums())[0]
             assert len(bad) == 0, f"{wl.name} round {r}: {len(bad)} checksums differ"
+
+
+def test_entry_cap_tail_rows_every_round():
+    """swimsim_tuning.fault_inject = 32: at most 24 exception entries per row, so many rows end within the record
+    stager's 4-entry prefetch of the cap (k_csr3 loads a record's first CSR_EREG entries with it; a clamp to cap - 4
+    used to load the wrong entries for a record starting there). Rows past the cap go to the production kernels.
+    Bit-exact either way, every round."""
+    for wl, rounds in ((W.config3(n=2048, rounds=40, kill_round=5), 40), (W.config2(n=2048, rounds=25), 25)):
+        eng = swimsim.Cluster(wl.n, tuning={"cs_ref": 2, "cs_async": 0, "fault_inject": 32})
+        ora = OracleSim(wl.n)
+        for r in range(rounds):
+            ev = wl.events_for(r)
+            eng.step(1, ev)
+            ora.step(ev)
+            bad = np.nonzero(eng.checksums() != ora.checksums())[0]
+            assert len(bad) == 0, f"{wl.name} round {r}: {len(bad)} checksums differ, first rows {bad[:5]}"
+        st = eng.checksum_path_stats()
+        print("entry cap 24", wl.name, st)
+        assert st["delta_launches"] >= 4, st
+
+
+# (role bits of fault_inject 64: 1 g/f chains, 2 h chains, 4 record stagers, 8 window stagers)
+JITTER_CASES = [(1, 11), (2, 12), (4, 13), (8, 14), (3, 15), (15, 16)]
+
+
+@pytest.mark.parametrize("roles,seed", JITTER_CASES)
+def test_perturbed_handover_on_real_cascade_rows(roles, seed):
+    """swimsim_tuning.fault_inject = 64: seeded sleeps before k_csr3's hand-over waits and signals in the selected roles,
+    so the g/f chains run ahead of the h chains (roles 2), the h chains ahead (1), a record stager (4) or a window stager
+    (8) falls behind, or all of them drift (15). Every order must give the production kernels' checksums at 32,768 real
+    cascade rows (swimsim_bench_checksum mode 5 against mode 0). A build with one done count shared by both kinds of
+    chain wave (-DC3_T_SHAREDDONE, round 5's race) fails this test."""
+    n = 32768
+    wl = W.config3(n=n, rounds=21, kill_round=10)
+    c = swimsim.Cluster(n, tuning={"fault_inject": 64 | (roles << 8) | (seed << 12)})
+    for r in range(20):
+        c.step(1, wl.events_for(r))
+        if r in (15, 18):
+            c.bench_checksum(n, 0, reps=1)
+            ref = c.checksums().copy()
+            c.bench_checksum(n, 5, reps=1)
+            got = c.checksums()
+            bad = np.nonzero(got != ref)[0]
+            assert len(bad) == 0, f"roles {roles} round {r}: {len(bad)} rows differ, first {bad[:5]}"
+    print("perturbed hand-over", roles, c.checksum_path_stats())

@@ -49,3 +49,36 @@ def test_two_processes(name):
 @pytest.mark.parametrize("name", ["config2", "config5"])
 def test_three_processes(name):
     _run(3, name)
+
+
+def _bench(extra, timeout=300):
+    """bench.py as the driver starts it (a child process; --gpus N > 1 starts its own torch.distributed.run)"""
+    repo = os.path.dirname(HERE)
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    out = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--members", "4096", "--warmup", "6",
+                          "--steps", "8", "--no-cpu-baseline", "--no-ring"] + extra, env=env, cwd=repo,
+                         capture_output=True, text=True, timeout=timeout)
+    assert out.returncode == 0, (out.stdout + out.stderr)[-4000:]
+    from test_bench_launch import json_objects
+
+    lines = [l for l in json_objects(out.stdout) if "metric" in l]
+    assert len(lines) == 1, out.stdout[-2000:]
+    return lines[0]
+
+
+def test_bench_two_ranks_host_transport_matches_one_gpu_line():
+    """The driver's multi-GPU bench line, rehearsed on one GPU: `bench.py --gpus 2 --host-transport` passes the GPU-count
+    gate, starts two ranks through torch.distributed.run, each holding half of the observer rows on cuda:0 and
+    exchanging every cross-shard parcel through the gloo host transport (the RCCL port's call sequence), times the
+    window max over ranks and prints one line with the exchange block. Its protocol counters (summed over the ranks)
+    must equal the 1-GPU line's on the same window (ping_sender.go:90: the exchanged requests and responses are the
+    RPCs of the reference)."""
+    one = _bench(["--gpus", "1"])
+    two = _bench(["--gpus", "2", "--host-transport"])
+    assert two["n_gpus"] == 2 and one["n_gpus"] == 1
+    assert "host transport" in two["config"]["parallelism"]
+    ex = two["exchange"]
+    assert ex["bytes_rank0"] > 0 and ex["exchanges_rank0"] > 0, ex
+    assert two["counters"] == one["counters"], (one["counters"], two["counters"])
+    assert two["config"]["live_member_rounds"] == one["config"]["live_member_rounds"]
+    print("1 GPU", one["value"], "2 ranks (host transport)", two["value"], "exchange", ex)

@@ -1,8 +1,9 @@
 """The reference-row checksum path (tools/diag/swimsim_checksum_delta.hip: k_csd_scan + k_cs_delta) against the CPU
 oracle. The path lives in the diagnostics library only (round 4: it did not pay over the cascade), so
 these tests run when that library is the one loaded:
-    SWIMSIM_LIBRARY=tools/libswimsim_diag.so python -m pytest tests/test_cs_delta.py -m gpu
-and skip otherwise.
+    SWIMSIM_LIBRARY=tools/libswimsim_diag.so python -m pytest tools/diag/test_cs_delta.py
+and skip otherwise. (Kept here, beside the diagnostics sources, since round 6: in tests/ they always skipped on the
+product library.)
 
 The path is forced onto every phase-C launch of at least 1,024 rows (SWIMSIM_CS_DELTA=2, synchronous phase C so
 every launch goes through it) at sizes where the oracle runs every round: the cascade (rows a few records apart),
@@ -10,11 +11,15 @@ churn (incarnation bumps: longer and shorter records), a partition (rows half a 
 plans fail and the rows go to the production kernels) and a self-only start. Bit-exact per round, as every
 other checksum kernel (memberlist.go:83-128). """
 import os
+import sys
 
 import numpy as np
 import pytest
 
-from oracle_ffi import OracleSim
+_REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [os.path.join(_REPO, "tests"), os.path.join(_REPO, "ringpop-go_amd")]
+
+from oracle_ffi import OracleSim  # noqa: E402
 import swimsim
 from swimsim import workloads as W
 

@@ -1,6 +1,6 @@
 """Per-kernel, per-launch PMC figures from rocprofv3 --pmc passes of bench.py (one directory per pass).
 
-usage: python tools/pmc_summary.py [--workload MEMBERS:STEPS:WARMUP:GPUS] [--window] <out.json> <pass_dir> [<pass_dir> ...]
+usage: python tools/pmc_summary.py [--workload MEMBERS:STEPS:WARMUP:GPUS[:NAME]] [--window] <out.json> <pass_dir> [<pass_dir> ...]
 --workload records the bench.py command the passes profiled (bench.py uses the summary only for that workload).
 --window keeps only the dispatches between the first and the last k_profile_mark dispatch of each pass (bench.py
 marks its timed rounds), so the per-launch figures cover exactly the launches its HIP-event timings cover.
@@ -37,8 +37,11 @@ def main():
     argv = sys.argv[1:]
     workload = None
     if argv and argv[0] == "--workload":
-        m, st, w, g = (int(x) for x in argv[1].split(":"))
+        f = argv[1].split(":")
+        m, st, w, g = (int(x) for x in f[:4])
         workload = {"members": m, "steps": st, "warmup": w, "gpus": g}
+        if len(f) > 4 and f[4] != "config3":                      # (bench.py --workload; config3 is the default)
+            workload["workload"] = f[4]
         argv = argv[2:]
     window = False
     if argv and argv[0] == "--window":
