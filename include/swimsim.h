@@ -87,8 +87,10 @@ typedef struct swimsim_tuning {
                                  path's exception entries capped at 24 per row (rows ending within the stager's
                                  prefetch of the cap); 64 = seeded sleeps before the reference-row kernel's hand-over
                                  waits and signals, bits 8-11 selecting the delayed roles (g/f chains, h chains,
-                                 record stagers, window stagers), bits 12-30 the seed; default 0. Results are
-                                 identical with 4, 8, 16, 32 and 64. */
+                                 record stagers, window stagers), bits 12-30 the seed; 128 = no side-stream buffer
+                                 set for the reference-row path (side launches keep the narrow kernel); 256 = side
+                                 launches of 1,024 rows and more take that path (4,097 by default); default 0.
+                                 Results are identical with 4, 8, 16, 32, 64, 128 and 256. */
 } swimsim_tuning;
 
 /* Events applied in phase E of a round (docs/ROUND_SEMANTICS.md §4). */

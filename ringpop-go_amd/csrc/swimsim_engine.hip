@@ -249,6 +249,25 @@ struct HostPort : Transport {
     int bcast(void *buf, size_t bytes, uint32_t root) override { return t.bcast(t.ctx, buf, bytes, root) ? SWIMSIM_EHIP : 0; }
 };
 
+// the reference-row checksum path's buffers for one stream's launches (swimsim_checksum_csr.hip), allocated by csr_alloc
+struct CsrSet {
+    bool ready = false, failed = false;
+    uint32_t rows = 0;                            // listed rows a launch may hold
+    uint32_t *B = nullptr, *Lb = nullptr, *OB = nullptr, *SBw = nullptr, *fb = nullptr, *fbcnt = nullptr, *nrec = nullptr;
+    uint4 *ent = nullptr, *P = nullptr;
+    CsdRow *rinfo = nullptr;
+    CsrPlan *plan = nullptr;
+    CsrRec *rec = nullptr;
+    uint4 *ucol = nullptr;                        // the divergent columns' scan table (k_csr_ucol)
+    uint32_t *fbsplit = nullptr;                  // fallback rows per production launch (k_csr_fbsplit)
+    unsigned long long *acc = nullptr;            // [8] fallback rows so far, then per reason (read by path stats)
+    void *cub_tmp = nullptr;                      // its own scan temporary (side set; the main set shares the handle's)
+    size_t cub_bytes = 0;
+    // the divergent-column lists (k_ucols) for the side set, whose launches run beside main-stream work that rebuilds
+    // DS's own; null for the main set
+    uint32_t *ucl = nullptr, *uhk = nullptr, *ucold = nullptr, *ucnt = nullptr;
+};
+
 }  // namespace
 
 struct swimsim {
@@ -352,19 +371,13 @@ struct swimsim {
     // (on for wide launches by default: the bench window runs 9.51 against 10.48 ms per round)
     int csr_mode = 1;                             // swimsim_tuning.cs_ref: 0 off, 1 wide launches, 2 every launch of
                                                   // at least CSD_MIN_ROWS rows
-    bool csr_ready = false, csr_failed = false;
-    uint32_t *csr_B = nullptr, *csr_Lb = nullptr, *csr_OB = nullptr, *csr_SBw = nullptr, *csr_fb = nullptr,
-             *csr_fbcnt = nullptr, *csr_nrec = nullptr;
+    // two buffer sets (CsrSet): csr for main-stream launches, csr2 for the side stream's round-end launches of more than
+    // 4,096 rows (round 6: with one set the side stream could not take the path)
+    CsrSet csr, csr2;
     size_t csr_sbw_words = 0;
-    uint4 *csr_ent = nullptr, *csr_P = nullptr;
-    CsdRow *csr_rinfo = nullptr;
-    CsrPlan *csr_plan = nullptr;
-    CsrRec *csr_rec = nullptr;
     uint32_t csr_ecap = 4096, csr_rcap = 1024, csr_KP = 0;   // (2,048 entries: rows far from the reference fell back)
-    uint4 *csr_ucol = nullptr;                    // the divergent columns' scan table (k_csr_ucol)
-    uint32_t *csr_fbsplit = nullptr;              // fallback rows per production launch (k_csr_fbsplit)
-    unsigned long long *csr_acc = nullptr;        // [8] fallback rows so far, then per reason (read by path stats)
     uint64_t csr_launches = 0;
+    uint32_t csr_side_min = 4097;                 // side launches of at least this many rows take the path (csr2)
     int fault_inject = 0;                         // swimsim_tuning.fault_inject (tests)
     bool colx_stale = false;                      // raw row writes marked every column: rebuilt at the next step
 #ifdef SWIMSIM_DIAG
@@ -831,21 +844,29 @@ int csd_hash(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t n, 
 
 // the reference-row path (swimsim_checksum_csr.hip) for a launch of n rows (n known on the host)
 bool csr_wanted(swimsim *h, uint32_t n, CsKind kind) {
-    if (h->csr_mode == 0 || h->csr_failed || n < CSD_MIN_ROWS || h->N < 1024) return false;
+    if (h->csr_mode == 0 || h->csr.failed || n < CSD_MIN_ROWS || h->N < 1024) return false;
     return kind == CS_WIDE || h->csr_mode == 2;
 }
 
-int csr_alloc(swimsim *h) {
-    if (h->csr_ready) return 0;
-    if (h->csr_failed) return 1;
-    // (per listed row of one launch: sized for NL rows; the few launches that list more rows and dense snapshots
-    // together keep the production kernels, csr_hash)
-    const uint32_t rows = h->NL;
+// side-stream launches (round-end checksums of at most snap_cap rows) take the path above 4,096 rows: there the narrow
+// kernel needs a second pass of workgroups (one per CU), and k_csr3's 256 rows per workgroup leave the
+// chip to the main stream (the deferred decisions' narrow launch had waited behind the side launch for CUs)
+bool csr_side_wanted(swimsim *h, uint32_t n) {
+    return h->csr_mode != 0 && !h->csr2.failed && h->csr2.rows && n >= h->csr_side_min && n <= h->csr2.rows &&
+           h->N >= 1024;
+}
+
+// c: the buffer set (h->csr or h->csr2), for launches of at most `rows` listed rows
+int csr_alloc(swimsim *h, CsrSet &c, uint32_t rows) {
+    if (c.ready) return 0;
+    if (c.failed) return 1;
+    const bool side = &c == &h->csr2;
     // records per row: 1,024 (512 left 2,620 rows of a 65,536-row round-22 launch to the production kernels); 512 past
     // 131,072 members, where the rows' other arrays need the memory (config 5's 262,144-member shard: 10 % headroom)
     h->csr_rcap = h->N <= 131072 ? 1024u : 512u;
     h->csr_sbw_words = ((size_t)h->N * (h->W + 32) + 256) / 4;
     h->csr_KP = (uint32_t)(h->csr_sbw_words * 4 / 20 + 2);
+    c.rows = rows;
     const size_t nalloc0 = h->allocs.size();
     const uint64_t bytes0 = h->alloc_bytes;
     // a failure frees what this call allocated and clears HIP's last error (a failed hipMalloc leaves it set, and
@@ -855,42 +876,52 @@ int csr_alloc(swimsim *h) {
         h->allocs.resize(nalloc0);
         h->alloc_bytes = bytes0;
         (void)hipGetLastError();
-        h->csr_failed = true;
+        c.failed = true;
+        c.rows = 0;
         h->err.clear();
         return rc;
     };
     int rc = 0;
-    if ((rc = dalloc(h, &h->csr_B, (size_t)h->NP, "csr reference row")) ||
-        (rc = dalloc(h, &h->csr_Lb, (size_t)h->N + 1, "csr reference lengths")) ||
-        (rc = dalloc(h, &h->csr_OB, (size_t)h->N + 1, "csr reference offsets")) ||
-        (rc = dalloc(h, &h->csr_SBw, h->csr_sbw_words, "csr reference string")) ||
-        (rc = dalloc(h, &h->csr_P, (size_t)20 * h->csr_KP * 2, "csr premix table")) ||
-        (rc = dalloc(h, &h->csr_fb, (size_t)rows, "csr fallback list")) ||
-        (rc = dalloc(h, &h->csr_fbcnt, 8, "csr fallback count and reasons")) ||
-        (rc = dalloc(h, &h->csr_rinfo, (size_t)rows, "csr row info")) ||
+    if ((rc = dalloc(h, &c.B, (size_t)h->NP, "csr reference row")) ||
+        (rc = dalloc(h, &c.Lb, (size_t)h->N + 1, "csr reference lengths")) ||
+        (rc = dalloc(h, &c.OB, (size_t)h->N + 1, "csr reference offsets")) ||
+        (rc = dalloc(h, &c.SBw, h->csr_sbw_words, "csr reference string")) ||
+        (rc = dalloc(h, &c.P, (size_t)20 * h->csr_KP * 2, "csr premix table")) ||
+        (rc = dalloc(h, &c.fb, (size_t)rows, "csr fallback list")) ||
+        (rc = dalloc(h, &c.fbcnt, 8, "csr fallback count and reasons")) ||
+        (rc = dalloc(h, &c.rinfo, (size_t)rows, "csr row info")) ||
         // (CSR_EREG spare entries past the last row: k_csr3's record stager loads a record's first CSR_EREG entries
         // with it, wherever in the row's cap they start)
-        (rc = dalloc(h, &h->csr_ent, ((size_t)rows * h->csr_ecap + CSR_EREG) * 2, "csr exception entries")) ||
-        (rc = dalloc(h, &h->csr_plan, (size_t)rows / CSR_ROWS + 1, "csr plans")) ||
-        (rc = dalloc(h, &h->csr_rec, (size_t)rows * h->csr_rcap, "csr records")) ||
-        (rc = dalloc(h, &h->csr_nrec, (size_t)rows, "csr record counts")) ||
-        (rc = dalloc(h, &h->csr_ucol, (size_t)h->N, "csr divergent column table")) ||
+        (rc = dalloc(h, &c.ent, ((size_t)rows * h->csr_ecap + CSR_EREG) * 2, "csr exception entries")) ||
+        (rc = dalloc(h, &c.plan, (size_t)rows / CSR_ROWS + 1, "csr plans")) ||
+        (rc = dalloc(h, &c.rec, (size_t)rows * h->csr_rcap, "csr records")) ||
+        (rc = dalloc(h, &c.nrec, (size_t)rows, "csr record counts")) ||
+        (rc = dalloc(h, &c.ucol, (size_t)h->N, "csr divergent column table")) ||
         (rc = (h->fault_inject & 1) ? h->fail(SWIMSIM_ENOMEM, "injected allocation failure") : 0) ||
-        (rc = dalloc(h, &h->csr_fbsplit, 4, "csr fallback split")) ||
-        (rc = dalloc(h, &h->csr_acc, 8, "csr path statistics")))
+        (rc = dalloc(h, &c.fbsplit, 4, "csr fallback split")) ||
+        (rc = dalloc(h, &c.acc, 8, "csr path statistics")))
+        return undo(rc);
+    if (side && ((rc = dalloc(h, &c.ucl, (size_t)h->N, "csr side divergent columns")) ||
+                 (rc = dalloc(h, &c.uhk, (size_t)h->N, "csr side divergent column slots")) ||
+                 (rc = dalloc(h, &c.ucold, (size_t)h->N, "csr side cold columns")) ||
+                 (rc = dalloc(h, &c.ucnt, 2, "csr side column counts"))))
         return undo(rc);
     size_t need = 0;
-    hipcub::DeviceScan::ExclusiveSum(nullptr, need, h->csr_Lb, h->csr_OB, (int)h->N + 1, h->s);
+    hipcub::DeviceScan::ExclusiveSum(nullptr, need, c.Lb, c.OB, (int)h->N + 1, h->s);
     void *p = nullptr;
-    if (need > h->cub_bytes && (rc = dalloc(h, (uint8_t **)&p, need, "cub temp (csr)"))) return undo(rc);
-    if (hipMemsetAsync(h->csr_acc, 0, 8 * sizeof(unsigned long long), h->s) != hipSuccess) return undo(SWIMSIM_EHIP);
-    if (p) {                                                       // (committed only here: undo frees p)
+    if ((side || need > h->cub_bytes) && (rc = dalloc(h, (uint8_t **)&p, need, "cub temp (csr)"))) return undo(rc);
+    if (hipMemsetAsync(c.acc, 0, 8 * sizeof(unsigned long long), h->s) != hipSuccess) return undo(SWIMSIM_EHIP);
+    if (side) {
+        c.cub_tmp = p;
+        c.cub_bytes = need;
+    } else if (p) {                                                // (committed only here: undo frees p)
         h->cub_tmp = p;
         h->cub_bytes = need;
     }
-    h->csr_ready = true;
+    c.ready = true;
     return 0;
 }
+int csr_alloc(swimsim *h) { return csr_alloc(h, h->csr, h->NL); }
 
 // rows k_csr left (csr_fbcnt[0], reasons in [1..7]): the production launches' counts (<= 4,096 rows: the narrow kernel
 // at 16 records per step; the next 8,192: at 8; the rest: the wide kernel) and the running statistics, on the device
@@ -905,74 +936,83 @@ __global__ void k_csr_fbsplit(uint32_t *fbcnt, uint32_t *split, unsigned long lo
     if (t < 8 && nf) acc[t] += fbcnt[t];
 }
 
-// hash the n listed rows (count on the device) by the reference-row path. Returns 0 when every row is hashed (rows the
-// path leaves go to the production kernels here), 1 when the path is unavailable (the caller hashes them), < 0 on a
-// HIP error (h->err set). Nothing here waits for the device: the rows the chains leave are counted on the device and
-// the production launches take their counts from there.
-int csr_hash(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t n, int chains = 4) {
-    if (n > h->NL) return 1;
-    if (csr_alloc(h)) return 1;
+// hash the n listed rows (count on the device) by the reference-row path, with buffer set c on stream st. Returns 0 when
+// every row is hashed (rows the path leaves go to the production kernels here), 1 when the path is unavailable (the
+// caller hashes them), < 0 on a HIP error (h->err set). Nothing here waits for the device: the rows the chains leave are
+// counted on the device and the production launches take their counts from there.
+int csr_hash(swimsim *h, CsrSet &c, const uint32_t *list, const uint32_t *cnt, uint32_t n, hipStream_t st, int chains = 4) {
+    const bool side = &c == &h->csr2;
+    if (n > (side ? c.rows : h->NL)) return 1;
+    if (side ? !c.ready : csr_alloc(h, c, h->NL)) return 1;
     if (h->fault_inject & 2) {                                     // tests: one injected HIP failure
         h->fault_inject &= ~2;
         return h->fail(SWIMSIM_EHIP, "csr_hash: injected HIP error");
     }
+    // (the side set's kernels see DS with its own divergent-column lists: main-stream work rebuilds DS's lists while a
+    // side launch runs; side launches hash snapshots only, which have no hot slots, so the lists' slots are not used)
+    DS d = h->d;
+    if (side) { d.ucl = c.ucl; d.uhk = c.uhk; d.ucold = c.ucold; d.ucnt = c.ucnt; }
+    void *cub = side ? c.cub_tmp : h->cub_tmp;
+    size_t cub_bytes = side ? c.cub_bytes : h->cub_bytes;
     CsdArgs ca{};
-    ca.B = h->csr_B;
-    ca.OB = h->csr_OB;
-    ca.SBw = h->csr_SBw;
+    ca.B = c.B;
+    ca.OB = c.OB;
+    ca.SBw = c.SBw;
     ca.sbw_words = (uint32_t)h->csr_sbw_words;
-    ca.ent = h->csr_ent;
-    ca.rinfo = h->csr_rinfo;
+    ca.ent = c.ent;
+    ca.rinfo = c.rinfo;
     ca.ecap = h->csr_ecap;
-    ca.ulist = h->d.ucl;
-    ca.ucnt = h->d.ucnt;
-    ca.ucol = h->csr_ucol;
-    ca.uhk = h->d.uhk;
+    ca.ulist = d.ucl;
+    ca.ucnt = d.ucnt;
+    ca.ucol = c.ucol;
+    ca.uhk = side ? nullptr : d.uhk;
     CsrArgs a{};
-    a.P = h->csr_P;
+    a.P = c.P;
     a.KP = h->csr_KP;
-    a.ent = h->csr_ent;
-    a.rinfo = h->csr_rinfo;
+    a.ent = c.ent;
+    a.rinfo = c.rinfo;
     a.ecap = h->csr_ecap;
-    a.plan = h->csr_plan;
-    a.rec = h->csr_rec;
-    a.nrec = h->csr_nrec;
+    a.plan = c.plan;
+    a.rec = c.rec;
+    a.nrec = c.nrec;
     a.rcap = h->csr_rcap;
-    a.fb_list = h->csr_fb;
-    a.fb_cnt = h->csr_fbcnt;
+    a.fb_list = c.fb;
+    a.fb_cnt = c.fbcnt;
     a.exw = (h->fault_inject & 4) ? 8u : 0xFFFFFFFFu;
     a.stprio = (h->fault_inject & 16) ? 1u : 0u;
     // (fault_inject 64: bits 8-11 the roles k_csr3 delays, bits 12-30 their seed)
     a.jitter = (h->fault_inject & 64) ? (((uint32_t)h->fault_inject >> 8) & 15u) | ((uint32_t)h->fault_inject >> 12 << 8) : 0u;
     {
-        Scope sc(h, F_CSD_SCAN);
-        hipLaunchKernelGGL(k_csd_ref, dim3((h->N + 256) / 256), dim3(256), 0, h->s, h->d, list, n, h->csr_B, h->csr_Lb);
-        size_t bytes = h->cub_bytes;
-        HIPCHK(h, hipcub::DeviceScan::ExclusiveSum(h->cub_tmp, bytes, h->csr_Lb, h->csr_OB, (int)h->N + 1, h->s));
-        HIPCHK(h, hipMemsetAsync(h->csr_SBw, 0, h->csr_sbw_words * 4, h->s));
-        hipLaunchKernelGGL(k_ucols, dim3(1), dim3(1024), 0, h->s, h->d);
-        hipLaunchKernelGGL(k_csr_ucol, dim3((h->N + 255) / 256), dim3(256), 0, h->s, h->d.ucl, h->d.ucnt, h->csr_B,
-                           h->csr_OB, h->csr_ucol);
-        launch_csr(h->d, list, n, cnt, ca, a, h->s, 0);
-        launch_csr(h->d, list, n, cnt, ca, a, h->s, 1);
-        launch_csr(h->d, list, n, cnt, ca, a, h->s, 2);
-        launch_csr(h->d, list, n, cnt, ca, a, h->s, 3);
-        HIPCHK(h, hipMemsetAsync(h->csr_fbcnt, 0, 32, h->s));
-        hipLaunchKernelGGL(k_ctr_add, dim3(1), dim3(1), 0, h->s, h->d, (int)C_X_CSD_SCANNED, (unsigned long long)n);
+        Scope sc(h, F_CSD_SCAN, st);
+        hipLaunchKernelGGL(k_csd_ref, dim3((h->N + 256) / 256), dim3(256), 0, st, d, list, n, c.B, c.Lb);
+        size_t bytes = cub_bytes;
+        HIPCHK(h, hipcub::DeviceScan::ExclusiveSum(cub, bytes, c.Lb, c.OB, (int)h->N + 1, st));
+        HIPCHK(h, hipMemsetAsync(c.SBw, 0, h->csr_sbw_words * 4, st));
+        hipLaunchKernelGGL(k_ucols, dim3(1), dim3(1024), 0, st, d);
+        hipLaunchKernelGGL(k_csr_ucol, dim3((h->N + 255) / 256), dim3(256), 0, st, d.ucl, d.ucnt, c.B, c.OB, c.ucol);
+        launch_csr(d, list, n, cnt, ca, a, st, 0);
+        launch_csr(d, list, n, cnt, ca, a, st, 1);
+        launch_csr(d, list, n, cnt, ca, a, st, 2);
+        launch_csr(d, list, n, cnt, ca, a, st, 3);
+        HIPCHK(h, hipMemsetAsync(c.fbcnt, 0, 32, st));
+        hipLaunchKernelGGL(k_ctr_add, dim3(1), dim3(1), 0, st, d, (int)C_X_CSD_SCANNED, (unsigned long long)n);
     }
     {
-        Scope sc(h, F_CS_WIDE);
-        launch_csr(h->d, list, n, cnt, ca, a, h->s, chains);
+        Scope sc(h, F_CS_WIDE, st);
+        launch_csr(d, list, n, cnt, ca, a, st, chains);
     }
     h->csr_launches++;
     // rows the path left: the production kernels, counts from the device (a launch with nothing to hash exits at
-    // once; timed with the preparation so that the checksum families' launch counts stay those of real work)
-    Scope sc(h, F_CS_FALLBACK);
-    hipLaunchKernelGGL(k_csr_fbsplit, dim3(1), dim3(64), 0, h->s, h->csr_fbcnt, h->csr_fbsplit, h->csr_acc);
-    launch_checksum_kind(h->d, h->csr_fb, h->csr_fbsplit, std::min(n, 4096u), CS_NARROW, h->s);
-    if (n > 4096u) launch_checksum_kind(h->d, h->csr_fb + 4096, h->csr_fbsplit + 1, std::min(n - 4096u, 8192u), CS_NARROW, h->s);
-    if (n > 12288u) launch_checksum_kind(h->d, h->csr_fb + 12288, h->csr_fbsplit + 2, n - 12288u, CS_WIDE, h->s);
+    // once; timed apart, F_CS_FALLBACK, so that the checksum families' launch counts stay those of real work)
+    Scope sc(h, F_CS_FALLBACK, st);
+    hipLaunchKernelGGL(k_csr_fbsplit, dim3(1), dim3(64), 0, st, c.fbcnt, c.fbsplit, c.acc);
+    launch_checksum_kind(d, c.fb, c.fbsplit, std::min(n, 4096u), CS_NARROW, st);
+    if (n > 4096u) launch_checksum_kind(d, c.fb + 4096, c.fbsplit + 1, std::min(n - 4096u, 8192u), CS_NARROW, st);
+    if (n > 12288u) launch_checksum_kind(d, c.fb + 12288, c.fbsplit + 2, n - 12288u, CS_WIDE, st);
     return 0;
+}
+int csr_hash(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t n, int chains = 4) {
+    return csr_hash(h, h->csr, list, cnt, n, h->s, chains);
 }
 
 // one FarmHash dispatch over the rows listed (count on the device; nrows = the count if the host
@@ -1000,6 +1040,10 @@ int hash_rows(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t ma
     if (!st && nrows != ~0u && csr_wanted(h, n, kind)) {          // the reference-row path (swimsim_checksum_csr.hip)
         const int rc = csr_hash(h, list, cnt, n);
         if (rc <= 0) return rc;                                    // done, or failed (h->err)
+    }
+    if (st && nrows != ~0u && csr_side_wanted(h, n)) {            // the same on the side stream, its own buffers
+        const int rc = csr_hash(h, h->csr2, list, cnt, n, st);
+        if (rc <= 0) return rc;
     }
 #ifdef SWIMSIM_DIAG
     if (!st && nrows != ~0u && csd_wanted(h, n, kind)) {          // diagnostics library: round 3's reference-row path
@@ -1709,6 +1753,7 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
     if (tun && tun->cs_ref >= 0) h->csr_mode = tun->cs_ref;
     if (tun && tun->fault_inject > 0) h->fault_inject = tun->fault_inject;
     if (h->fault_inject & 32) h->csr_ecap = 24;      // (tests: rows whose exception entries end within CSR_EREG of the cap)
+    if (h->fault_inject & 256) h->csr_side_min = 1024;   // (tests: side launches of 1,024 rows and more take the path)
 #ifdef SWIMSIM_DIAG                                 // diagnostics library only: the reference-row path
     if (const char *v = getenv("SWIMSIM_CS_DELTA")) h->csd_mode = atoi(v);
     if (const char *v = getenv("SWIMSIM_CS_DELTA_MAXDIFF")) h->csd_maxdiff = (uint32_t)strtoul(v, nullptr, 10);
@@ -1891,6 +1936,17 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
     // several GB inside a round, which sometimes took over a second (3 of 12 bench runs at 77-92 ms per round).
     // Failure is not an error: the production kernels stay in charge.
     if (h->csr_mode != 0 && h->N >= 1024 && h->NL > h->cs_narrow_rows && h->NL >= CSD_MIN_ROWS) (void)csr_alloc(h);
+    // the side set, when round-end side launches can list more rows than the narrow kernel takes in one pass
+    // (only with 12 % of the device left after it: config 5's 262,144-member shard keeps its 10 % headroom)
+    if (h->csr_mode != 0 && h->N >= 1024 && h->cs_async && h->snap_cap >= h->csr_side_min && !(h->fault_inject & 128)) {
+        const uint32_t rcap = h->N <= 131072 ? 1024u : 512u;
+        const uint64_t kp = ((uint64_t)h->N * (h->W + 32) + 256) / 20 + 2;
+        const uint64_t need = (uint64_t)h->snap_cap * ((uint64_t)h->csr_ecap * 32 + rcap * sizeof(CsrRec) + 64) +
+                              kp * 20 * 32 + (uint64_t)h->N * 64 + (64ull << 20);
+        size_t fr = 0, tot = 0;
+        if (hipMemGetInfo(&fr, &tot) == hipSuccess && fr > need && fr - need >= tot / 100 * 12)
+            (void)csr_alloc(h, h->csr2, h->snap_cap);
+    }
     if (hipGetLastError() != hipSuccess) return bail(SWIMSIM_EHIP);
     *out = h;
     return SWIMSIM_OK;
@@ -2835,9 +2891,12 @@ int swimsim_checksum_path_stats(swimsim_t *h, uint64_t *delta_launches, uint64_t
     }
 #else                                       // the product's reference-row path (swimsim_checksum_csr.hip)
     unsigned long long acc[8] = {0};
-    if (h->csr_ready) {                     // counted on the device (k_csr_fbsplit)
-        HIPCHK(h, hipMemcpyAsync(acc, h->csr_acc, sizeof acc, hipMemcpyDeviceToHost, h->s));
+    for (CsrSet *c : {&h->csr, &h->csr2}) {
+        if (!c->ready) continue;            // counted on the device (k_csr_fbsplit), both buffer sets
+        unsigned long long a2[8];
+        HIPCHK(h, hipMemcpyAsync(a2, c->acc, sizeof a2, hipMemcpyDeviceToHost, h->s));
         HIPCHK(h, hipStreamSynchronize(h->s));
+        for (int i = 0; i < 8; i++) acc[i] += a2[i];
     }
     if (delta_launches) *delta_launches = h->csr_launches;
     if (fallback_rows) *fallback_rows = acc[0];

@@ -459,10 +459,18 @@ __device__ __forceinline__ void wave_bump_pre(const DS &d, uint32_t ol, const Ms
 // swimsim_create requires every sub-pool to hold N records, the longest message. (A fetch-add instead, one round trip
 // fewer, stranded each overflowing attempt's sub-pool tail: config 4's heal messages then overflowed a sharded pool.
 // k_recv hides the allocation's round trips behind its merge instead, recv_one_pre.)
+// Messages of at most sub / 256 records take one fetch-add instead (one round trip instead of two): an attempt that
+// overflows leaves the cursor past its sub-pool's end, which strands less than sub / 256 records of that sub-pool, once.
 __device__ __forceinline__ unsigned long long pool_alloc_lane0(const DS &d, uint32_t n) {
     const unsigned long long sub = d.pool_cap / POOL_SHARDS;
+    const bool small = n <= sub / 256;
     for (uint32_t t = 0, s = wave_gid() % POOL_SHARDS; t < POOL_SHARDS; t++, s = (s + 1) % POOL_SHARDS) {
         unsigned long long *cur = d.pool_cur + (size_t)s * POOL_CUR_STRIDE;
+        if (small) {
+            const unsigned long long old = atomicAdd(cur, (unsigned long long)n);
+            if (old + n <= sub) return s * sub + old;
+            continue;
+        }
         unsigned long long old = __hip_atomic_load(cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         while (old + n <= sub) {
             const unsigned long long seen = atomicCAS(cur, old, old + n);

@@ -104,3 +104,36 @@ def test_async_equals_sync_path():
         assert sync.digest() == asy.digest(), f"state differs after round {r0 + 10}"
     assert sync.counters() == asy.counters()
     assert np.array_equal(sync.rows()[0], asy.rows()[0])
+
+
+def test_side_stream_reference_row_path_vs_oracle():
+    """The reference-row path on the side stream (its own buffer set, csr2): round-end launches of at least 1,024 rows
+    (swimsim_tuning.fault_inject 256; 4,097 by default) hash their snapshots by k_csd_scan + k_csr3 on the side stream
+    while the next rounds run. Bit-exact against the oracle at every chunk boundary of the cascade (memberlist.go:83-128),
+    and the path did run (every wide-path launch here is a side launch: a 4,096-row main launch is narrow)."""
+    wl = W.config3(n=4096, rounds=40, kill_round=5)
+    eng, ora = make_pair(wl.n, tuning={"fault_inject": 256})
+    run_chunked(eng, ora, wl.n, wl.rounds, wl.events, chunk=5)
+    st = eng.checksum_path_stats()
+    print("side-stream reference-row path", st)
+    assert st["delta_launches"] >= 1, st
+
+
+def test_side_stream_reference_row_path_equals_narrow_kernel():
+    """At 16,384 members, where the oracle is slow: the same cascade with the side set (fault_inject 256) and without
+    it (128: side launches keep the narrow kernel) gives identical checksums, state digests and counters at every chunk
+    boundary."""
+    wl = W.config3(n=16384, rounds=30, kill_round=5)
+    a = swimsim.Cluster(wl.n, tuning={"fault_inject": 256})
+    b = swimsim.Cluster(wl.n, tuning={"fault_inject": 128})
+    for r0 in range(0, wl.rounds, 5):
+        ev = [e for e in wl.events if r0 <= e[0] < r0 + 5]
+        a.step(5, ev)
+        b.step(5, ev)
+        bad = np.nonzero(a.checksums() != b.checksums())[0]
+        assert len(bad) == 0, f"after round {r0 + 5}: {len(bad)} checksums differ, first {bad[:5]}"
+        assert a.digest() == b.digest()
+    assert a.counters() == b.counters()
+    sa, sb = a.checksum_path_stats(), b.checksum_path_stats()
+    print("side set", sa, "none", sb)
+    assert sa["delta_launches"] > sb["delta_launches"], (sa, sb)

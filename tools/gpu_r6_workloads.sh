@@ -15,22 +15,18 @@ for w in ${WORKLOADS:-config2 config4 selfstart config5}; do
     rc=$?; echo "bench $w rc=$rc" >> gpurun_out/wl/$w.err; [ $rc -eq 0 ] || exit $rc
   fi
   if [ "$MODE" = prof ] || [ "$MODE" = all ]; then
-    timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/wl/prof_$w -o run --output-format csv \
-      -- python3 bench.py $a > gpurun_out/wl/prof_$w.log 2>&1
-    rc=$?; echo "rocprof $w rc=$rc" >> gpurun_out/wl/prof_$w.log; [ $rc -eq 0 ] || exit $rc
-    python3 tools/prof_window.py $(ls gpurun_out/wl/prof_$w/*/run_kernel_trace.csv gpurun_out/wl/prof_$w/run_kernel_trace.csv 2>/dev/null | head -n 1) \
-      gpurun_out/wl/prof_${w}_window_stats.csv || exit 1
+    bash tools/gpu_r6_prof.sh $w $a || exit 1
   fi
   if [ "$MODE" = pmc ] || [ "$MODE" = all ]; then
     i=0
     for pass in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS"; do
       i=$((i+1))
-      timeout -k 10 -s KILL 300 rocprofv3 --pmc $pass --kernel-trace -d gpurun_out/wl/pmc_${w}_$i -o run \
+      timeout -k 10 -s KILL 300 rocprofv3 --pmc $pass --kernel-trace -d /tmp/pmc_${w}_$i -o run \
         --output-format csv -- python3 bench.py $a > gpurun_out/wl/pmc_${w}_$i.log 2>&1
       rc=$?; echo "pmc $w pass $i rc=$rc" >> gpurun_out/wl/pmc_${w}_$i.log; [ $rc -eq 0 ] || exit $rc
     done
     dirs=""
-    for k in $(seq 1 $i); do dirs="$dirs $(dirname $(ls gpurun_out/wl/pmc_${w}_$k/*/run_counter_collection.csv gpurun_out/wl/pmc_${w}_$k/run_counter_collection.csv 2>/dev/null | head -n 1))"; done
+    for k in $(seq 1 $i); do dirs="$dirs $(dirname $(ls /tmp/pmc_${w}_$k/*/run_counter_collection.csv /tmp/pmc_${w}_$k/run_counter_collection.csv 2>/dev/null | head -n 1))"; done
     python3 tools/pmc_summary.py --workload ${WLS[$w]} --window gpurun_out/wl/pmc_summary_$w.json $dirs || exit 1
   fi
 done
