@@ -557,6 +557,7 @@ def main():
                                "are not timed in the window (bench.py --time-all; profiles/ holds rocprofv3 kernel stats)"),
             "counters": counters,
             "checksum_paths": eng.checksum_path_stats(),
+            "deferred_decisions": {k: int(units.get(k, 0)) for k in ("defer", "defer_eq", "defer_rep", "defer_norow")},
         }
         if line["roofline"]["bound"] == "valu":
             line["roofline"]["bound_frac"] = (dom.get("valu") or {}).get("frac")

@@ -42,7 +42,10 @@ enum Counter {
     C_X_MERGED_R, C_X_APPLIED_R, C_X_RISSUED, C_X_RCALLS, C_X_BUMPED, C_X_CS_ROWS_N, C_X_CSD_SCANNED,
     // dense messages merged (MembershipAsChanges: full-sync responses in k_resp / k_resolve, reverse full syncs in
     // k_jobs_merge, heal lists), and the changes the reverse full syncs applied
-    C_X_DENSE_RESP, C_X_DENSE_JOBS, C_X_JOBS_APPLIED, C_X_DENSE_HEAL, C_NALL
+    C_X_DENSE_RESP, C_X_DENSE_JOBS, C_X_JOBS_APPLIED, C_X_DENSE_HEAL,
+    // deferred full-sync decisions (k_defer_eq): all, settled by row equality, with no issue-time row to compare with
+    // (C_X_DEFER_REP: settled against a clean row of the sender's issue-time checksum, k_cs_reps)
+    C_X_DEFER, C_X_DEFER_EQ, C_X_DEFER_NOROW, C_X_DEFER_REP, C_NALL
 };
 
 constexpr int CTR_SHARDS = 64, CTR_STRIDE = 48;   // d.ctr is [CTR_SHARDS][CTR_STRIDE] u64

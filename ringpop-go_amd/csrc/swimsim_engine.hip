@@ -337,6 +337,8 @@ struct swimsim {
     uint4 *defer = nullptr;
     uint32_t *defer_cnt = nullptr;
     uint8_t *defer_eq = nullptr;                  // deferred decision settled by row equality
+    unsigned long long *rep_tab = nullptr;        // checksum representatives (k_cs_reps), rep_mask + 1 entries
+    uint32_t rep_mask = 0, rep_gen = 0;
     uint32_t *exh_list = nullptr, *exh_cnt = nullptr, *scratch = nullptr;
     uint8_t *need = nullptr, *fsflag = nullptr;
     uint4 *evbuf = nullptr;
@@ -484,6 +486,8 @@ void drain_timing(swimsim *h) {
 constexpr uint32_t kWavesPerBlock = SWIM_WAVE_BLOCK / 64;
 inline uint32_t blocks_for_waves(uint32_t waves) { return waves ? (waves + kWavesPerBlock - 1) / kWavesPerBlock : 1; }
 inline uint32_t blocks_for_threads(uint32_t n) { return n ? (n + 255) / 256 : 1; }
+// checksum representatives' table: a power of two of at least twice the rows
+inline uint32_t rep_slots(uint32_t nl) { uint32_t s = 1024; while (s < 2 * nl) s <<= 1; return s; }
 
 // incarnation steps the checksum tables can hold: the wide formatter addresses d.rtail8 by member word ((e << 3) | status)
 // with 32-byte entries and a 32-bit byte offset, so 2^24 incarnation steps (2^32 bytes) is the limit
@@ -1198,8 +1202,13 @@ int resolve_deferred(swimsim *h, int phase, MsgDesc *rdesc, uint32_t maxn) {
         Scope sc(h, F_CSPREP);
         HIPCHK(h, hipMemsetAsync(h->cnt, 0, 8, h->s));
         hipLaunchKernelGGL(k_ucols, dim3(1), dim3(1024), 0, h->s, h->d);   // (k_defer_eq compares by them)
+        if (h->rep_tab) {                                          // (exits at once when nothing was deferred)
+            h->rep_gen = h->rep_gen % 255u + 1u;
+            hipLaunchKernelGGL(k_cs_reps, dim3(blocks_for_threads(h->NL)), dim3(256), 0, h->s, h->d, h->defer_cnt, h->rep_tab,
+                               h->rep_mask, h->rep_gen);
+        }
         hipLaunchKernelGGL(k_defer_eq, dim3(blocks_for_waves(maxn)), dim3(SWIM_WAVE_BLOCK), 0, h->s, h->d, h->defer, h->defer_cnt,
-                           phase, h->defer_eq);
+                           phase, h->defer_eq, h->rep_tab, h->rep_mask, h->rep_gen);
         hipLaunchKernelGGL(k_defer_ids, dim3(blocks_for_threads(maxn)), dim3(256), 0, h->s, h->d, h->defer,
                            h->defer_cnt, h->defer_eq, h->list, h->cnt);
     }
@@ -1889,12 +1898,15 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
         (rc = dalloc(h, &h->info, 8, "info")) || (rc = dalloc(h, &h->list, 3 * KC + 2 * (size_t)h->NL + 64, "list")) ||
         (rc = dalloc(h, &h->cnt, 2, "cnt")) || (rc = dalloc(h, &h->defer, KC + 2 * (size_t)h->NL + 64, "defer")) ||
         (rc = dalloc(h, &h->defer_eq, KC + 2 * (size_t)h->NL + 64, "defer eq")) ||
+        (rc = dalloc(h, &h->rep_tab, (size_t)rep_slots(h->NL), "checksum representatives")) ||
         (rc = dalloc(h, &h->defer_cnt, 1, "defer_cnt")) || (rc = dalloc(h, &h->exh_list, h->NL, "exh_list")) ||
         (rc = dalloc(h, &h->exh_cnt, 1, "exh_cnt")) || (rc = dalloc(h, &h->scratch, (size_t)64 * (h->NP / 32), "scratch")) ||
         (rc = dalloc(h, &h->need, h->N, "need")) || (rc = dalloc(h, &h->digest_buf, 4, "digest")) ||
         (rc = dalloc(h, &h->fsflag, KC, "fsflag")) || (rc = dalloc(h, &h->hsics, 4, "hsics")) ||
         (rc = dalloc(h, &h->npairs, 1, "npairs")))
         return bail(rc);
+    h->rep_mask = rep_slots(h->NL) - 1u;
+    hipMemset(h->rep_tab, 0, (size_t)rep_slots(h->NL) * 8);      // (generation 0: every entry empty)
     h->evcap = 4 * h->N + 64;
     if ((rc = dalloc(h, &h->evbuf, h->evcap, "events")) || (rc = dalloc(h, &h->ev_applied, h->evcap, "ev_applied")))
         return bail(rc);
@@ -2107,6 +2119,9 @@ int swimsim_step(swimsim_t *h, uint32_t nrounds, const swimsim_event *events, si
     if (!h) return SWIMSIM_EINVAL;
     if (h->G == 1 && h->NL != h->N) return h->fail(SWIMSIM_EINVAL, "a partial observer range needs a shard transport");
     if (h->colx_stale && nrounds) {                                // (no snapshot is alive between step calls)
+        // the rebuild reads the live rows only: every step call ends with the side stream drained, and dense snapshots
+        // live within one round, so none can hold a word the rebuilt bitmap would not cover
+        if (h->side_pending) return h->fail(SWIMSIM_EINVAL, "internal: divergent-column rebuild with side checksums pending");
         hipLaunchKernelGGL(k_colx_rebuild, dim3(blocks_for_threads(h->NP)), dim3(256), 0, h->s, h->d);
         h->colx_stale = false;
     }
@@ -2719,11 +2734,12 @@ int swimsim_kernel_units(swimsim_t *h, const char **names, double *values, size_
                                "recv_issued", "recv_calls", "resp_merged", "resp_applied", "resp_bumped", "issued",
                                "bitmap_words_per_row", "diag_stamp0", "diag_stamp1", "diag_stamp2", "diag_stamp3",
                                "hot_slots", "diag_stamp4", "diag_stamp5", "diag_stamp6", "diag_stamp7",
-                               "dense_resp", "dense_jobs", "jobs_applied", "dense_heal"};
+                               "dense_resp", "dense_jobs", "jobs_applied", "dense_heal", "defer", "defer_eq", "defer_norow",
+                               "defer_rep"};
     const int ki[] = {C_X_CS_ROWS, C_X_CS_ROWS_N, C_X_CS_DUP, C_X_MERGED, C_X_APPLIED, C_X_RISSUED, C_X_RCALLS,
                       C_X_MERGED_R, C_X_APPLIED_R, C_X_BUMPED, C_X_ISSUED, -1, C_NALL, C_NALL + 1, C_NALL + 2, C_NALL + 3,
                       -2, C_NALL + 4, C_NALL + 5, C_NALL + 6, C_NALL + 7, C_X_DENSE_RESP, C_X_DENSE_JOBS, C_X_JOBS_APPLIED,
-                      C_X_DENSE_HEAL};
+                      C_X_DENSE_HEAL, C_X_DEFER, C_X_DEFER_EQ, C_X_DEFER_NOROW, C_X_DEFER_REP};
     uint32_t hot = 0;                                              // hot slots in use now (not a delta)
     if (h->d.hot_cnt) {
         HIPCHK(h, hipMemcpyAsync(&hot, h->d.hot_cnt, 4, hipMemcpyDeviceToHost, h->s));

@@ -344,9 +344,18 @@ __device__ __forceinline__ void wave_merge_dense(const DS &d, uint32_t ol, uint3
 }
 
 // merge a whole message into row ol (wave-wide; the changes of one message are distinct members)
-// (dctr >= 0: the measurement counter a dense message adds one to)
+// the first MB records per lane of a sparse message, loaded ahead (k_resp issues them with the bump's loads)
+__device__ __forceinline__ void merge_first(const DS &d, const MsgDesc &md, uint4 (&rec)[MB]) {
+    const unsigned long long off = ((unsigned long long)md.off_hi << 32) | md.off_lo;
+#pragma unroll
+    for (int u = 0; u < MB; u++) {
+        const uint32_t i = u * 64 + lane_id();
+        rec[u] = md.kind == 0 && i < md.len ? d.pool[off + i] : make_uint4(0xFFFFFFFFu, 0, 0, 0);
+    }
+}
+// (dctr >= 0: the measurement counter a dense message adds one to; pre0: the first batch from merge_first, or null)
 __device__ __forceinline__ void wave_merge_body(const DS &d, uint32_t ol, uint32_t o, const MsgDesc &md, uint32_t now_e,
-                                                uint32_t sched_r, MAcc &acc, int dctr) {
+                                                uint32_t sched_r, MAcc &acc, int dctr, const uint4 *pre0 = nullptr) {
     const uint32_t *rowp = d.mw + (size_t)ol * d.NP;
     const uint32_t *hrow = d.hmw + (size_t)ol * d.HP;
     if (md.kind == 0) {
@@ -357,7 +366,7 @@ __device__ __forceinline__ void wave_merge_body(const DS &d, uint32_t ol, uint32
 #pragma unroll
             for (int u = 0; u < MB; u++) {
                 const uint32_t i = base + u * 64 + lane_id();
-                rec[u] = i < md.len ? d.pool[off + i] : make_uint4(0xFFFFFFFFu, 0, 0, 0);
+                rec[u] = pre0 && base == 0 ? pre0[u] : i < md.len ? d.pool[off + i] : make_uint4(0xFFFFFFFFu, 0, 0, 0);
             }
             // (the record's tag names the member's hot slot: the row word is the second load of the chain, not the
             // third after an hidx lookup)
@@ -389,10 +398,11 @@ __device__ void wave_merge_msg(const DS &d, uint32_t ol, uint32_t o, const MsgDe
 }
 // the same on a wave's register copy of the row scalars (RowPre)
 __device__ __forceinline__ void wave_merge_msg_pre(const DS &d, uint32_t ol, uint32_t o, const MsgDesc &md, uint32_t now_e,
-                                                   uint32_t sched_r, int cset, RowPre &p, int dctr = -1) {
+                                                   uint32_t sched_r, int cset, RowPre &p, int dctr = -1,
+                                                   const uint4 *pre0 = nullptr) {
     MAcc acc;
     acc.tag = p.useq;
-    wave_merge_body(d, ol, o, md, now_e, sched_r, acc, dctr);
+    wave_merge_body(d, ol, o, md, now_e, sched_r, acc, dctr, pre0);
     wave_finalize_pre(d, ol, acc, cset, p);
 }
 
@@ -1518,22 +1528,74 @@ __device__ bool wave_rows_differ(const DS &d, const uint32_t *a, const uint32_t 
 // issue-time row (word for word) is "no full sync" without hashing either side. The sender's
 // issue-time row is its issue snapshot (pending C_o, local or side slot) or, for a sender that was
 // clean at issue and is still clean, its current row. Remote senders and heal pings are not checked.
-__global__ void k_defer_eq(DS d, const uint4 *defer, const uint32_t *defer_cnt, int phase, uint8_t *eq) {
+// Checksum representatives (round 6). A sender that was clean at issue gave its checksum C_o, but its row may have
+// changed since (it received pings of its own in phase D): then no issue-time row was left to compare with, and the
+// decision hashed the receiver's snapshot (a one-row chain, 3.3 ms, on the round's critical path in the cascade's
+// suspect wave). Any row whose content is unchanged since it was hashed to C_o has the sender's issue-time content, up
+// to a checksum collision that the word comparison itself rules out: the receiver's snapshot equal to such a row has
+// checksum C_o exactly. k_cs_reps indexes the clean rows of known checksum by that checksum (open addressing, 8-bit
+// build generation in the top byte, so the table is never cleared: an entry of another build reads as empty, and every
+// hit is verified against the row); it runs only when the phase deferred a decision.
+__device__ __forceinline__ uint32_t rep_hash(uint32_t cs, uint32_t mask) { return fmix32(cs ^ 0x9E3779B9u) & mask; }
+constexpr uint32_t REP_PROBES = 64;
+__global__ void k_cs_reps(DS d, const uint32_t *defer_cnt, unsigned long long *tab, uint32_t mask, uint32_t gen) {
+    const uint32_t ol = blockIdx.x * blockDim.x + threadIdx.x;
+    if (*defer_cnt == 0 || ol >= d.NL) return;
+    if (d.dirty[ol] || d.cpslot[ol] != SRC_NONE) return;
+    const uint32_t cs = d.cs[ol];
+    const unsigned long long mine = ((unsigned long long)gen << 56) | ((unsigned long long)ol << 32) | cs;
+    for (uint32_t q = 0, s = rep_hash(cs, mask); q < REP_PROBES; q++, s = (s + 1) & mask) {
+        unsigned long long cur = __hip_atomic_load(tab + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while ((uint32_t)(cur >> 56) != gen) {                      // empty for this build: claim it
+            const unsigned long long seen = atomicCAS(tab + s, cur, mine);
+            if (seen == cur) return;
+            cur = seen;
+        }
+        if ((uint32_t)cur == cs) return;                           // this checksum has a representative
+    }
+}
+// a clean local row whose current checksum is cs, or SRC_NONE
+__device__ __forceinline__ uint32_t rep_find(const DS &d, const unsigned long long *tab, uint32_t mask, uint32_t gen,
+                                             uint32_t cs) {
+    for (uint32_t q = 0, s = rep_hash(cs, mask); q < REP_PROBES; q++, s = (s + 1) & mask) {
+        const unsigned long long cur = tab[s];
+        if ((uint32_t)(cur >> 56) != gen) return SRC_NONE;
+        if ((uint32_t)cur != cs) continue;
+        const uint32_t r = (uint32_t)(cur >> 32) & 0xFFFFFFu;
+        return r < d.NL && !d.dirty[r] && d.cpslot[r] == SRC_NONE && d.cs[r] == cs ? r : SRC_NONE;
+    }
+    return SRC_NONE;
+}
+
+__global__ void k_defer_eq(DS d, const uint4 *defer, const uint32_t *defer_cnt, int phase, uint8_t *eq,
+                           const unsigned long long *tab, uint32_t mask, uint32_t gen) {
     const uint32_t i = wave_gid();
     if (i >= *defer_cnt) return;
     const uint4 e = defer[i];
     const uint32_t ri = e.x & 0x7FFFFFFFu, sender = phase == 1 ? ri / d.K : ri;
     const uint32_t *srow = nullptr;
+    bool viarep = false;
     if (phase != 2) {
         if (e.w & 0x80000000u) {
             if (!(e.z & 0x80000000u)) srow = d.dense + (size_t)e.z * d.NP;
         } else if (sender >= d.lo && sender < d.lo + d.NL && !d.dirty[sender - d.lo]) {
             srow = d.mw + (size_t)(sender - d.lo) * d.NP;
+        } else if (tab) {                                          // C_o = e.z known: a representative of it
+            const uint32_t r = rep_find(d, tab, mask, gen, e.z);
+            if (r != SRC_NONE) {
+                srow = d.mw + (size_t)r * d.NP;
+                viarep = true;
+            }
         }
     }
     bool same = false;
     if (srow) same = !wave_rows_differ(d, d.dense + (size_t)e.y * d.NP, srow, nullptr, nullptr);
-    if (lane_id() == 0) eq[i] = same ? 1 : 0;
+    if (lane_id() == 0) {
+        eq[i] = same ? 1 : 0;
+        ctr_add(d, C_X_DEFER, 1ull);
+        if (same) ctr_add(d, viarep ? C_X_DEFER_REP : C_X_DEFER_EQ, 1ull);
+        if (!srow) ctr_add(d, C_X_DEFER_NOROW, 1ull);
+    }
 }
 
 __global__ void k_recv_finish(DS d, const uint4 *defer, const uint32_t *defer_cnt, MsgDesc *rdesc, int phase,
@@ -1606,8 +1668,10 @@ __global__ void k_resp(DS d, const int32_t *tgt, const uint8_t *failed, const Ms
     // (the row scalars, both descriptors: one round trip; RowPre carries them through the bump and the merge)
     RowPre p = row_pre(d, ol);
     const MsgDesc sd = sdesc[o], rd = rdesc[o];
+    uint4 rec0[MB];                                                 // (the response's first records ride with the bump's
+    merge_first(d, rd, rec0);                                       // loads: the pool is read-only here)
     wave_bump_pre(d, ol, sd, p);
-    wave_merge_msg_pre(d, ol, o, rd, r, r, 1, p, C_X_DENSE_RESP);
+    wave_merge_msg_pre(d, ol, o, rd, r, r, 1, p, C_X_DENSE_RESP, rec0);
     if (lane_id() == 0) {
         ctr_add(d, C_PINGS_OK, 1ull);
         if (sd.kind == 0) ctr_add(d, C_X_BUMPED, (unsigned long long)sd.len);

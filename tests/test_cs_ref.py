@@ -214,3 +214,26 @@ def test_perturbed_handover_on_real_cascade_rows(roles, seed):
             bad = np.nonzero(got != ref)[0]
             assert len(bad) == 0, f"roles {roles} round {r}: {len(bad)} rows differ, first {bad[:5]}"
     print("perturbed hand-over", roles, c.checksum_path_stats())
+
+
+def test_colx_rebuild_after_raw_writes_every_round():
+    """Raw row writes (swimsim_set_member; the reference's memberlist.Update applied without gossip) mark every column
+    divergent, and the next step rebuilds DS::colx from the rows (k_colx_rebuild). The reference-row path (forced on
+    every launch), the dedup comparison under 3-bit fingerprints (fault_inject 8) and the deferred decisions then compare
+    rows over the rebuilt columns only: bit-exact against the oracle every round, with raw writes between rounds on a
+    converged cluster and in the middle of the cascade."""
+    wl = W.config3(n=2048, rounds=36, kill_round=5)
+    eng = swimsim.Cluster(wl.n, tuning={"cs_ref": 2, "cs_async": 0, "fault_inject": 8})
+    ora = OracleSim(wl.n)
+    writes = {0: [(3, 7, 1, 1)], 12: [(100, 5, 0, 3), (101, 6, 2, 2)], 20: [(7, 9, 1, 4)]}
+    for r in range(wl.rounds):
+        for (o, m, st, k) in writes.get(r, ()):
+            inc = swimsim.T0_MS + k * 200
+            eng.set_member(o, m, st, inc)
+            ora.set_member(o, m, st, inc)
+        ev = wl.events_for(r)
+        eng.step(1, ev)
+        ora.step(ev)
+        bad = np.nonzero(eng.checksums() != ora.checksums())[0]
+        assert len(bad) == 0, f"round {r}: {len(bad)} checksums differ, first rows {bad[:5]}"
+        assert eng.digest() == ora.digest(), f"round {r}: state digest differs"

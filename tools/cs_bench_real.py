@@ -19,11 +19,13 @@ modes = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else [0]
 reps = int(sys.argv[4]) if len(sys.argv) > 4 else 2
 rows_list = [int(x) for x in sys.argv[5].split(",")] if len(sys.argv) > 5 else [n]
 wl = W.config3(n=n, rounds=R + 1, kill_round=10)
-c = swimsim.Cluster(n)
+# CS_TUNING='{"fault_inject": 512}' (a JSON object of swimsim_tuning fields): an engine variant, same results
+c = swimsim.Cluster(n, tuning=json.loads(os.environ["CS_TUNING"]) if os.environ.get("CS_TUNING") else None)
 for r in range(R):
     c.step(1, wl.events_for(r))
 ref = c.checksums().copy()
-out = {"n": n, "round": R, "library": os.path.basename(os.environ.get("SWIMSIM_LIBRARY", "libswimsim.so"))}
+out = {"n": n, "round": R, "library": os.path.basename(os.environ.get("SWIMSIM_LIBRARY", "libswimsim.so")),
+       "tuning": os.environ.get("CS_TUNING", "")}
 for rows in rows_list:
     for mode in modes:
         out[f"rows{rows}_mode{mode}_ms"] = round(c.bench_checksum(rows, mode, reps=reps), 3)
