@@ -557,7 +557,8 @@ def main():
                                "are not timed in the window (bench.py --time-all; profiles/ holds rocprofv3 kernel stats)"),
             "counters": counters,
             "checksum_paths": eng.checksum_path_stats(),
-            "deferred_decisions": {k: int(units.get(k, 0)) for k in ("defer", "defer_eq", "defer_rep", "defer_norow")},
+            "deferred_decisions": {k: int(units.get(k, 0)) for k in ("defer", "defer_eq", "defer_rep", "defer_undo",
+                                                                              "defer_norow")},
         }
         if line["roofline"]["bound"] == "valu":
             line["roofline"]["bound_frac"] = (dom.get("valu") or {}).get("frac")

@@ -89,8 +89,9 @@ typedef struct swimsim_tuning {
                                  waits and signals, bits 8-11 selecting the delayed roles (g/f chains, h chains,
                                  record stagers, window stagers), bits 12-30 the seed; 128 = no side-stream buffer
                                  set for the reference-row path (side launches keep the narrow kernel); 256 = side
-                                 launches of 1,024 rows and more take that path (4,097 by default); default 0.
-                                 Results are identical with 4, 8, 16, 32, 64, 128 and 256. */
+                                 launches of 1,024 rows and more take that path (4,097 by default); 1024 = one
+                                 generation of side-stream snapshot slots (phase C waits for the previous round's side
+                                 launch); default 0. Results are identical with 4, 8, 16, 32, 64, 128, 256 and 1024. */
 } swimsim_tuning;
 
 /* Events applied in phase E of a round (docs/ROUND_SEMANTICS.md §4). */

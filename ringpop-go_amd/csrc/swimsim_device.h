@@ -45,7 +45,8 @@ enum Counter {
     C_X_DENSE_RESP, C_X_DENSE_JOBS, C_X_JOBS_APPLIED, C_X_DENSE_HEAL,
     // deferred full-sync decisions (k_defer_eq): all, settled by row equality, with no issue-time row to compare with
     // (C_X_DEFER_REP: settled against a clean row of the sender's issue-time checksum, k_cs_reps)
-    C_X_DEFER, C_X_DEFER_EQ, C_X_DEFER_NOROW, C_X_DEFER_REP, C_NALL
+    // (C_X_DEFER_UNDO: settled against the sender's row with this phase's logged merges undone, d.ulog)
+    C_X_DEFER, C_X_DEFER_EQ, C_X_DEFER_NOROW, C_X_DEFER_REP, C_X_DEFER_UNDO, C_NALL
 };
 
 constexpr int CTR_SHARDS = 64, CTR_STRIDE = 48;   // d.ctr is [CTR_SHARDS][CTR_STRIDE] u64
@@ -150,7 +151,14 @@ struct DS {
     // them: ucl = every colx column in member order (ucnt[0] of them) with its hot slot uhk (SRC_NONE: none), ucold =
     // the colx columns without a hot slot (ucnt[1], any order). Rows are equal iff equal at the hot slots and ucold.
     uint32_t *ucl, *uhk, *ucold, *ucnt;
+    // the words a receive phase's merges overwrote (k_recv, phases D and Q2): per row up to ULOG_CAP {member, old word}
+    // in apply order and their count (ULOG_CAP + 1: more, not usable). A row that was clean when it issued its message
+    // and changed only in the phase since is its issue-time row with the first old word of each logged member restored
+    // (k_defer_eq); nullptr: off
+    uint2 *ulog;
+    uint32_t *ulog_cnt;
 };
+constexpr uint32_t ULOG_CAP = 64;
 
 // hot slot of member m, SRC_NONE when m has none (or hot columns are off)
 __device__ __forceinline__ uint32_t hot_slot(const DS &d, uint32_t m) { return d.hidx ? d.hidx[m] : SRC_NONE; }

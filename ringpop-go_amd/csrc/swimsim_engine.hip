@@ -283,12 +283,17 @@ struct swimsim {
     hipStream_t s = nullptr;
     // phase C of a round can hash its rows on a side stream while the next round runs
     hipStream_t side = nullptr;
-    hipEvent_t ev_snap = nullptr, ev_side = nullptr;
+    hipEvent_t ev_snap = nullptr, ev_side[2] = {nullptr, nullptr};
     bool cs_async = true, side_pending = false;
+    // two generations of side slots (round 6): phase C of round r + 1 snapshots into the half round r did not use, so it
+    // need not wait for round r's side launch; a half is retired (its checksums copied into cs[], its rows' cpslot
+    // cleared) when it is reused, or by any full sync_side. side_halves = 1 (memory) keeps one generation.
+    bool side_pend[2] = {false, false};
+    uint32_t side_halves = 1, side_gen = 0;
     uint32_t cs_narrow_rows = CS_NARROW_ROWS;     // checksum launches of at most this many rows: narrow kernel
     uint32_t snap_cap = 0;
-    uint32_t *side_ids = nullptr, *side_cnt = nullptr;
-    uint2 *side_map = nullptr;
+    uint32_t *side_ids = nullptr, *side_cnt = nullptr;   // [halves][snap_cap], [halves]
+
     DS d{};
     // host mirrors
     std::vector<uint8_t> live;
@@ -1086,18 +1091,35 @@ void hot_update(swimsim *h) {
     hipLaunchKernelGGL(k_hot_fill, dim3(blocks_for_waves(h->NL)), dim3(SWIM_WAVE_BLOCK), 0, h->s, h->d);
 }
 
-// order the main stream after the side-stream checksums of the previous phase C; from here on every
-// row's cs[] is current and no row refers to a side slot
+// retire side half g: order the main stream after its launch, copy its checksums into cs[] of the rows that still refer
+// to it (rows that changed since were listed by a later phase C, which cleared or replaced their cpslot)
+int retire_half(swimsim *h, uint32_t g) {
+    if (!h->side_pend[g]) return 0;
+    HIPCHK(h, hipStreamWaitEvent(h->s, h->ev_side[g], 0));
+    const uint32_t lo = h->d.dense_cap + g * h->snap_cap;
+    hipLaunchKernelGGL(k_side_retire, dim3(blocks_for_threads(h->NL)), dim3(256), 0, h->s, h->d, lo, lo + h->snap_cap);
+    h->side_pend[g] = false;
+    h->side_pending = h->side_pend[0] || h->side_pend[1];
+    return 0;
+}
+
+// order the main stream after every side-stream checksum launch; from here on every row's cs[] is current and no row
+// refers to a side slot
 int sync_side(swimsim *h) {
     if (!h->side_pending) return 0;
-    HIPCHK(h, hipStreamWaitEvent(h->s, h->ev_side, 0));
-    HIPCHK(h, hipMemsetAsync(h->d.cpslot, 0xFF, (size_t)h->NL * 4, h->s));
-    h->side_pending = false;
+    for (uint32_t g = 0; g < 2; g++)
+        if (int rc = retire_half(h, (h->side_gen + g) % 2)) return rc;       // (the older generation first)
     return 0;
 }
 
 int checksum_dirty(swimsim *h, int mode, bool async = false) {
-    if (int rc = sync_side(h)) return rc;
+    // phase C (async) reuses side half side_gen only: the other half's launch, from the round before, may still run
+    const uint32_t g = h->side_gen;
+    if (async && h->cs_async && h->side_halves == 2) {
+        if (int rc = retire_half(h, g)) return rc;
+    } else if (int rc = sync_side(h)) {
+        return rc;
+    }
     HIPCHK(h, hipMemsetAsync(h->cnt, 0, 4, h->s));
     {
         Scope sc(h, F_CSPREP);
@@ -1112,19 +1134,21 @@ int checksum_dirty(swimsim *h, int mode, bool async = false) {
     // async: snapshot the rows to hash, mark every dirty row clean (cpslot = the slot carrying its
     // checksum) and hash the snapshots on the side stream; the round reads cs[] only after sync_side
     auto go_side = [&](const uint32_t *rows, uint32_t n2, const uint32_t *vals, const uint32_t *dups) -> int {
+        uint32_t *ids = h->side_ids + (size_t)g * h->snap_cap, *icnt = h->side_cnt + g;
         {
             Scope sc(h, F_CSPREP);
             hipLaunchKernelGGL(k_snap_rows, dim3(blocks_for_waves(std::max(n2, 1u))), dim3(SWIM_WAVE_BLOCK), 0, h->s, h->d, rows, n2,
-                               h->side_ids, h->side_cnt);
-            hipLaunchKernelGGL(k_snap_dups, dim3(blocks_for_threads(n)), dim3(256), 0, h->s, h->d, vals, n, dups,
-                               h->side_map);
+                               ids, icnt, h->d.dense_cap + g * h->snap_cap);
+            hipLaunchKernelGGL(k_snap_dups, dim3(blocks_for_threads(n)), dim3(256), 0, h->s, h->d, vals, n, dups);
+            hipLaunchKernelGGL(k_ctr_add, dim3(1), dim3(1), 0, h->s, h->d, (int)C_X_CS_DUP, (unsigned long long)(n - n2));
         }
         HIPCHK(h, hipEventRecord(h->ev_snap, h->s));
         HIPCHK(h, hipStreamWaitEvent(h->side, h->ev_snap, 0));
-        if (int rc = hash_rows(h, h->side_ids, h->side_cnt, n2, n2, h->side)) return rc;
-        hipLaunchKernelGGL(k_side_scatter, dim3(blocks_for_threads(n)), dim3(256), 0, h->side, h->d, h->side_map, n, n2);
-        HIPCHK(h, hipEventRecord(h->ev_side, h->side));
+        if (int rc = hash_rows(h, ids, icnt, n2, n2, h->side)) return rc;
+        HIPCHK(h, hipEventRecord(h->ev_side[g], h->side));
+        h->side_pend[g] = true;
         h->side_pending = true;
+        h->side_gen = (g + 1) % h->side_halves;
         return 0;
     };
     const bool side_ok = async && h->cs_async;
@@ -1752,7 +1776,8 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
     if (hipStreamCreateWithFlags(&h->s, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_snap, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&h->ev_side, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&h->ev_side[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&h->ev_side[1], hipEventDisableTiming) != hipSuccess) {
         h->err = "hipStreamCreate / hipEventCreate failed";
         return bail(SWIMSIM_EHIP);
     }
@@ -1862,14 +1887,16 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
         uint64_t async_rows = CS_ASYNC_ROWS;
         if (tun && tun->cs_async_rows >= 0) async_rows = (uint64_t)tun->cs_async_rows;
         h->snap_cap = h->cs_async ? (uint32_t)std::min<uint64_t>(std::min<uint64_t>(async_rows, h->NL), snap_mem) : 0u;
+        // two generations when a second half fits the same budget (tests: fault_inject 1024 keeps one)
+        h->side_halves = h->snap_cap && snap_mem >= 2ull * h->snap_cap && !(h->fault_inject & 1024) ? 2u : 1u;
     }
-    const size_t nslots = (size_t)d.dense_cap + h->snap_cap;
+    const size_t nslots = (size_t)d.dense_cap + (size_t)h->side_halves * h->snap_cap;
     if ((rc = dalloc(h, &d.dense, nslots * h->NP, "dense snapshots")) ||
         (rc = dalloc(h, &d.dense_meta, nslots, "dense meta")) || (rc = dalloc(h, &d.dense_cur, 1, "dense cursor")) ||
         (rc = dalloc(h, &d.dense_len, nslots, "dense len")) || (rc = dalloc(h, &d.dense_last, nslots, "dense last")) ||
         (rc = dalloc(h, &d.dense_cs, nslots, "dense cs")) ||
-        (rc = dalloc(h, &h->side_ids, std::max<uint32_t>(h->snap_cap, 1), "side ids")) ||
-        (rc = dalloc(h, &h->side_cnt, 1, "side count")) || (rc = dalloc(h, &h->side_map, h->NL, "side map")))
+        (rc = dalloc(h, &h->side_ids, (size_t)h->side_halves * std::max<uint32_t>(h->snap_cap, 1), "side ids")) ||
+        (rc = dalloc(h, &h->side_cnt, 2, "side count")))
         return bail(rc);
     // work buffers. Message descriptors are indexed by global observer id (a shard imports the
     // messages of remote senders there); inbox arrays hold local pairs plus imported ones.
@@ -1899,6 +1926,8 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
         (rc = dalloc(h, &h->cnt, 2, "cnt")) || (rc = dalloc(h, &h->defer, KC + 2 * (size_t)h->NL + 64, "defer")) ||
         (rc = dalloc(h, &h->defer_eq, KC + 2 * (size_t)h->NL + 64, "defer eq")) ||
         (rc = dalloc(h, &h->rep_tab, (size_t)rep_slots(h->NL), "checksum representatives")) ||
+        (rc = dalloc(h, &h->d.ulog, (size_t)h->NL * ULOG_CAP, "receive-phase undo log")) ||
+        (rc = dalloc(h, &h->d.ulog_cnt, (size_t)h->NL, "receive-phase undo log counts")) ||
         (rc = dalloc(h, &h->defer_cnt, 1, "defer_cnt")) || (rc = dalloc(h, &h->exh_list, h->NL, "exh_list")) ||
         (rc = dalloc(h, &h->exh_cnt, 1, "exh_cnt")) || (rc = dalloc(h, &h->scratch, (size_t)64 * (h->NP / 32), "scratch")) ||
         (rc = dalloc(h, &h->need, h->N, "need")) || (rc = dalloc(h, &h->digest_buf, 4, "digest")) ||
@@ -1906,6 +1935,7 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
         (rc = dalloc(h, &h->npairs, 1, "npairs")))
         return bail(rc);
     h->rep_mask = rep_slots(h->NL) - 1u;
+    hipMemset(h->d.ulog_cnt, 0xFF, (size_t)h->NL * 4);            // (no row has a usable log before its first receive)
     hipMemset(h->rep_tab, 0, (size_t)rep_slots(h->NL) * 8);      // (generation 0: every entry empty)
     h->evcap = 4 * h->N + 64;
     if ((rc = dalloc(h, &h->evbuf, h->evcap, "events")) || (rc = dalloc(h, &h->ev_applied, h->evcap, "ev_applied")))
@@ -1977,7 +2007,8 @@ int swimsim_destroy(swimsim_t *h) {
     h->xp.reset();
     if (h->hinfo) hipHostFree(h->hinfo);
     if (h->ev_snap) hipEventDestroy(h->ev_snap);
-    if (h->ev_side) hipEventDestroy(h->ev_side);
+    for (hipEvent_t e : h->ev_side)
+        if (e) hipEventDestroy(e);
     if (h->side) hipStreamDestroy(h->side);
     if (h->s) hipStreamDestroy(h->s);
     delete h;
@@ -2653,7 +2684,7 @@ int swimsim_memory(swimsim_t *h, swimsim_memory_t *out) {
     out->dissemination = rows * sizeof(uint2) + (uint64_t)h->NL * h->d.NBIT * 4;
     out->timers = rows * 9 + (uint64_t)h->NL * h->d.NB * 4;
     out->message_pool = h->d.pool_cap * 16;
-    out->dense_snapshots = ((uint64_t)h->d.dense_cap + h->snap_cap) * h->NP * 4;
+    out->dense_snapshots = ((uint64_t)h->d.dense_cap + (uint64_t)h->side_halves * h->snap_cap) * h->NP * 4;
     out->total = h->alloc_bytes + h->sbuf_cap + h->rbuf_cap;
     out->dense_cap = h->d.dense_cap;
     out->side_cap = h->snap_cap;
@@ -2735,11 +2766,11 @@ int swimsim_kernel_units(swimsim_t *h, const char **names, double *values, size_
                                "bitmap_words_per_row", "diag_stamp0", "diag_stamp1", "diag_stamp2", "diag_stamp3",
                                "hot_slots", "diag_stamp4", "diag_stamp5", "diag_stamp6", "diag_stamp7",
                                "dense_resp", "dense_jobs", "jobs_applied", "dense_heal", "defer", "defer_eq", "defer_norow",
-                               "defer_rep"};
+                               "defer_rep", "defer_undo"};
     const int ki[] = {C_X_CS_ROWS, C_X_CS_ROWS_N, C_X_CS_DUP, C_X_MERGED, C_X_APPLIED, C_X_RISSUED, C_X_RCALLS,
                       C_X_MERGED_R, C_X_APPLIED_R, C_X_BUMPED, C_X_ISSUED, -1, C_NALL, C_NALL + 1, C_NALL + 2, C_NALL + 3,
                       -2, C_NALL + 4, C_NALL + 5, C_NALL + 6, C_NALL + 7, C_X_DENSE_RESP, C_X_DENSE_JOBS, C_X_JOBS_APPLIED,
-                      C_X_DENSE_HEAL, C_X_DEFER, C_X_DEFER_EQ, C_X_DEFER_NOROW, C_X_DEFER_REP};
+                      C_X_DENSE_HEAL, C_X_DEFER, C_X_DEFER_EQ, C_X_DEFER_NOROW, C_X_DEFER_REP, C_X_DEFER_UNDO};
     uint32_t hot = 0;                                              // hot slots in use now (not a delta)
     if (h->d.hot_cnt) {
         HIPCHK(h, hipMemcpyAsync(&hot, h->d.hot_cnt, 4, hipMemcpyDeviceToHost, h->s));

@@ -246,6 +246,7 @@ struct RowPre {
     int32_t nhe, ping, dcnt, clast, maxp;
     uint32_t clen, dirty, cs, cpslot;
     unsigned long long fp, useq;
+    uint32_t ulog;                    // entries logged in d.ulog this phase (k_recv)
 };
 // (wave-uniform by construction: readfirstlane tells the compiler so, and the copy lives in scalar registers instead of
 // 13 vector registers that k_recv's merge and issue loops would otherwise spill)
@@ -261,6 +262,7 @@ __device__ __forceinline__ RowPre row_pre(const DS &d, uint32_t ol) {
     p.clen = uni(d.clen[ol]); p.dirty = uni(d.dirty[ol]); p.cs = uni(d.cs[ol]); p.cpslot = uni(d.cpslot[ol]);
     p.fp = uni64(d.fp[ol]);
     p.useq = d.useq ? uni64(d.useq[ol]) : 0ull;
+    p.ulog = 0;
     return p;
 }
 
@@ -353,9 +355,11 @@ __device__ __forceinline__ void merge_first(const DS &d, const MsgDesc &md, uint
         rec[u] = md.kind == 0 && i < md.len ? d.pool[off + i] : make_uint4(0xFFFFFFFFu, 0, 0, 0);
     }
 }
-// (dctr >= 0: the measurement counter a dense message adds one to; pre0: the first batch from merge_first, or null)
+// (dctr >= 0: the measurement counter a dense message adds one to; pre0: the first batch from merge_first, or null;
+// ulog: the receive phase's undo log position of this row (k_recv), or null)
 __device__ __forceinline__ void wave_merge_body(const DS &d, uint32_t ol, uint32_t o, const MsgDesc &md, uint32_t now_e,
-                                                uint32_t sched_r, MAcc &acc, int dctr, const uint4 *pre0 = nullptr) {
+                                                uint32_t sched_r, MAcc &acc, int dctr, const uint4 *pre0 = nullptr,
+                                                uint32_t *ulog = nullptr) {
     const uint32_t *rowp = d.mw + (size_t)ol * d.NP;
     const uint32_t *hrow = d.hmw + (size_t)ol * d.HP;
     if (md.kind == 0) {
@@ -376,14 +380,24 @@ __device__ __forceinline__ void wave_merge_body(const DS &d, uint32_t ol, uint32
             for (int u = 0; u < MB; u++)
                 cur[u] = rec[u].x == 0xFFFFFFFFu ? 0u : hk[u] != SRC_NONE ? hrow[hk[u]] : rowp[rec_m(rec[u])];
 #pragma unroll
-            for (int u = 0; u < MB; u++)
+            for (int u = 0; u < MB; u++) {
+                const int before = acc.napp;
                 if (rec[u].x != 0xFFFFFFFFu)
                     merge_change_w(d, ol, o, rec_m(rec[u]), cur[u], rec_st(rec[u]), rec_e(rec[u]), rec[u].z, rec[u].w, now_e,
                                    sched_r, acc, hk[u]);
+                if (ulog) {                                        // the overwritten word, in apply order
+                    const bool ap = acc.napp != before;
+                    const unsigned long long b = __ballot(ap);
+                    const uint32_t at = *ulog + (uint32_t)__popcll(b & lanemask_lt());
+                    if (ap && at < ULOG_CAP) d.ulog[(size_t)ol * ULOG_CAP + at] = make_uint2(rec_m(rec[u]), cur[u]);
+                    *ulog += (uint32_t)__popcll(b);
+                }
+            }
         }
     } else if (md.kind == 1) {
         wave_merge_dense(d, ol, o, md, now_e, sched_r, acc);
         if (dctr >= 0 && lane_id() == 0) ctr_add(d, dctr, 1ull);
+        if (ulog) *ulog = ULOG_CAP + 1u;                           // (not logged: the row's issue-time words are lost)
     }
     __threadfence_block();
 }
@@ -399,10 +413,10 @@ __device__ void wave_merge_msg(const DS &d, uint32_t ol, uint32_t o, const MsgDe
 // the same on a wave's register copy of the row scalars (RowPre)
 __device__ __forceinline__ void wave_merge_msg_pre(const DS &d, uint32_t ol, uint32_t o, const MsgDesc &md, uint32_t now_e,
                                                    uint32_t sched_r, int cset, RowPre &p, int dctr = -1,
-                                                   const uint4 *pre0 = nullptr) {
+                                                   const uint4 *pre0 = nullptr, bool logit = false) {
     MAcc acc;
     acc.tag = p.useq;
-    wave_merge_body(d, ol, o, md, now_e, sched_r, acc, dctr, pre0);
+    wave_merge_body(d, ol, o, md, now_e, sched_r, acc, dctr, pre0, logit && d.ulog ? &p.ulog : nullptr);
     wave_finalize_pre(d, ol, acc, cset, p);
 }
 
@@ -1118,6 +1132,9 @@ __global__ void k_list(DS d, int mode, const int32_t *tgt, const uint8_t *failed
     if (mode == 1) take = take && tgt[ol] >= 0;
     if (mode == 2) take = take && failed[ol];
     if (take) list[atomicAdd(cnt, 1u)] = ol;
+    // (phase C: a listed row gets a new checksum, on the main stream or in a new side slot; a pending one of an older
+    // side half must not overwrite it when that half retires)
+    if (take && mode == 0) d.cpslot[ol] = SRC_NONE;
 }
 
 __global__ void k_list_one(uint32_t *list, uint32_t *cnt, uint32_t ol, const DS d) {
@@ -1320,7 +1337,7 @@ __device__ __forceinline__ void recv_one_pre(const DS &d, const RecvArgs &a, uin
     const bool early = md.kind == 0 && bound > 0 && bound <= min(4096ull, d.pool_cap / POOL_SHARDS / 16);
     unsigned long long roff = 0;
     if (early && lane_id() == 0) roff = pool_alloc_lane0(d, (uint32_t)bound);   // (read after the merge)
-    wave_merge_msg_pre(d, ol, j, md, a.r, a.r, 0, p);
+    wave_merge_msg_pre(d, ol, j, md, a.r, a.r, 0, p, -1, nullptr, true);
     MsgDesc resp;
     resp.kind = 0; resp.len = 0; resp.off_lo = resp.off_hi = 0;
     uint32_t kept = 0;
@@ -1397,6 +1414,7 @@ __global__ void __launch_bounds__(256, RECV_MIN_WAVES) k_recv(DS d, RecvArgs a) 
         const uint32_t pair = off + w;
         recv_one_pre(d, a, key, a.pinfo[2 * (size_t)pair], a.pinfo[2 * (size_t)pair + 1], pair, nslots, p);
     }
+    if (d.ulog_cnt && lane_id() == 0) d.ulog_cnt[key - d.lo] = min(p.ulog, ULOG_CAP + 1u);
 }
 
 // DS::colx from the rows themselves (one lane per column, a wave's 64 columns in two bitmap words): after raw row
@@ -1522,6 +1540,38 @@ __device__ bool wave_rows_differ(const DS &d, const uint32_t *a, const uint32_t 
     return __any(diff);
 }
 
+// one wave: does snapshot a differ from live row b as it was before its logged merges (the first logged old word of each
+// member restored; nlog <= ULOG_CAP entries of log, members inside the divergent columns: every row-word write marks its
+// column)? Only over the divergent columns; false when they are more than N/4 (the caller hashes instead)
+__device__ bool wave_rows_differ_undo(const DS &d, const uint32_t *a, const uint32_t *b, const uint2 *log, uint32_t nlog,
+                                      bool &done) {
+    const uint32_t lane = lane_id();
+    const uint32_t nu = d.ucnt[0];
+    done = nu <= d.N / 4;
+    if (!done) return true;
+    const uint2 L = lane < nlog ? log[lane] : make_uint2(0xFFFFFFFFu, 0u);
+    bool diff = false;
+    for (uint32_t c0 = 0; c0 < nu && !__any(diff); c0 += 64 * MB) {
+        uint32_t m[MB], x[MB], y[MB];
+#pragma unroll
+        for (int u = 0; u < MB; u++) {
+            const uint32_t c = c0 + u * 64 + lane;
+            m[u] = c < nu ? d.ucl[c] : 0xFFFFFFFEu;
+            x[u] = c < nu ? a[m[u]] : 0u;
+            y[u] = c < nu ? b[m[u]] : 0u;
+        }
+        for (int k = (int)nlog - 1; k >= 0; k--) {               // (descending: the first logged word of a member wins)
+            const uint32_t lm = (uint32_t)__builtin_amdgcn_readlane((int)L.x, k);
+            const uint32_t lw = (uint32_t)__builtin_amdgcn_readlane((int)L.y, k);
+#pragma unroll
+            for (int u = 0; u < MB; u++) y[u] = m[u] == lm ? lw : y[u];
+        }
+#pragma unroll
+        for (int u = 0; u < MB; u++) diff |= x[u] != y[u];
+    }
+    return __any(diff);
+}
+
 // resolve deferred full-sync decisions once the snapshot checksums exist (phase 2 = heal ping:
 // the job is queued at once; heal runs in phase E, before any phase-D job of the round)
 // Equal rows have equal checksums: a deferred decision whose receiver snapshot equals the sender's
@@ -1588,13 +1638,26 @@ __global__ void k_defer_eq(DS d, const uint4 *defer, const uint32_t *defer_cnt, 
             }
         }
     }
-    bool same = false;
-    if (srow) same = !wave_rows_differ(d, d.dense + (size_t)e.y * d.NP, srow, nullptr, nullptr);
+    bool same = false, viaundo = false;
+    if (srow) {
+        same = !wave_rows_differ(d, d.dense + (size_t)e.y * d.NP, srow, nullptr, nullptr);
+    } else if (phase != 2 && !(e.w & 0x80000000u) && d.ulog && sender >= d.lo && sender < d.lo + d.NL) {
+        // the sender was clean at issue (C_o = e.z) and has changed since only by this phase's merges: its issue-time
+        // row is its row with the logged words restored
+        const uint32_t sl = sender - d.lo, nlog = d.ulog_cnt[sl];
+        if (nlog <= ULOG_CAP) {
+            bool done = false;
+            const bool differ = wave_rows_differ_undo(d, d.dense + (size_t)e.y * d.NP, d.mw + (size_t)sl * d.NP,
+                                                      d.ulog + (size_t)sl * ULOG_CAP, nlog, done);
+            viaundo = done;
+            same = done && !differ;
+        }
+    }
     if (lane_id() == 0) {
         eq[i] = same ? 1 : 0;
         ctr_add(d, C_X_DEFER, 1ull);
-        if (same) ctr_add(d, viarep ? C_X_DEFER_REP : C_X_DEFER_EQ, 1ull);
-        if (!srow) ctr_add(d, C_X_DEFER_NOROW, 1ull);
+        if (same) ctr_add(d, viarep ? C_X_DEFER_REP : viaundo ? C_X_DEFER_UNDO : C_X_DEFER_EQ, 1ull);
+        if (!srow && !viaundo) ctr_add(d, C_X_DEFER_NOROW, 1ull);
     }
 }
 
@@ -1795,16 +1858,16 @@ __global__ void k_fp_copy(DS d, const uint32_t *vals, uint32_t n, const uint32_t
 }
 
 // ---------------------------------------------------------------------------------------------
-// phase C on the side stream: the rows left after dedup are copied into dense slots
-// [dense_cap, dense_cap + n) (one wave per row) and hashed there while the next round runs on the main
-// stream; every listed row (dedup heads and duplicates) is marked clean with cpslot = the slot whose
-// dense_cs carries its checksum. k_side_scatter writes cs[] when the hash is done.
+// phase C on the side stream: the rows left after dedup are copied into dense slots of one side half
+// [slot0, slot0 + n) (one wave per row) and hashed there while the next rounds run on the main stream; every
+// listed row (dedup heads and duplicates) is marked clean with cpslot = the slot whose dense_cs carries its
+// checksum. k_side_retire writes cs[] on the main stream when the half is reused or synchronised.
 // ---------------------------------------------------------------------------------------------
-__global__ void k_snap_rows(DS d, const uint32_t *rows, uint32_t n, uint32_t *ids, uint32_t *idcnt) {
+__global__ void k_snap_rows(DS d, const uint32_t *rows, uint32_t n, uint32_t *ids, uint32_t *idcnt, uint32_t slot0) {
     const uint32_t k = wave_gid();
     if (k == 0 && lane_id() == 0) *idcnt = n;
     if (k >= n) return;
-    const uint32_t ol = rows[k], slot = d.dense_cap + k;
+    const uint32_t ol = rows[k], slot = slot0 + k;
     const uint4 *src = (const uint4 *)(d.mw + (size_t)ol * d.NP);
     uint4 *dst = (uint4 *)(d.dense + (size_t)slot * d.NP);
     for (uint32_t i = lane_id(); i < d.NP / 4; i += 64 * SNAP_MB) {
@@ -1826,8 +1889,8 @@ __global__ void k_snap_rows(DS d, const uint32_t *rows, uint32_t n, uint32_t *id
 }
 
 // dedup duplicates (vals = the dirty rows sorted by fingerprint, dup_of from k_fp_verify) take their
-// head's slot; map[i] = {row, slot} for every dirty row, consumed by k_side_scatter
-__global__ void k_snap_dups(DS d, const uint32_t *vals, uint32_t n, const uint32_t *dup_of, uint2 *map) {
+// head's slot (k_side_retire copies the slot's checksum to every row that refers to it)
+__global__ void k_snap_dups(DS d, const uint32_t *vals, uint32_t n, const uint32_t *dup_of) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t row = vals[i], h = dup_of ? dup_of[row] : SRC_NONE;
@@ -1835,15 +1898,17 @@ __global__ void k_snap_dups(DS d, const uint32_t *vals, uint32_t n, const uint32
         d.cpslot[row] = d.cpslot[h];
         d.dirty[row] = 0;
     }
-    map[i] = make_uint2(row, h != SRC_NONE ? d.cpslot[h] : d.cpslot[row]);
 }
 
-__global__ void k_side_scatter(DS d, const uint2 *map, uint32_t n, uint32_t nhashed) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i == 0) ctr_add(d, C_X_CS_DUP, (unsigned long long)(n - nhashed));   // (hashed rows: counted by the kernels)
-    if (i >= n) return;
-    const uint2 e = map[i];
-    d.cs[e.x] = d.dense_cs[e.y];
+// a side half's checksums into cs[] of the rows still referring to its slots [lo, hi), on the main stream after the
+// half's launch (a row listed by a later phase C had its cpslot cleared or replaced there: its newer checksum stands)
+__global__ void k_side_retire(DS d, uint32_t lo, uint32_t hi) {
+    const uint32_t ol = blockIdx.x * blockDim.x + threadIdx.x;
+    if (ol >= d.NL) return;
+    const uint32_t s = d.cpslot[ol];
+    if (s < lo || s >= hi) return;
+    d.cs[ol] = d.dense_cs[s];
+    d.cpslot[ol] = SRC_NONE;
 }
 
 #include "swimsim_checksum.hip"

@@ -137,3 +137,14 @@ def test_side_stream_reference_row_path_equals_narrow_kernel():
     sa, sb = a.checksum_path_stats(), b.checksum_path_stats()
     print("side set", sa, "none", sb)
     assert sa["delta_launches"] > sb["delta_launches"], (sa, sb)
+
+
+@pytest.mark.parametrize("tuning", [{"fault_inject": 1024}, {}])
+def test_side_generations_vs_oracle(tuning):
+    """Two generations of side-stream snapshot slots (default): phase C of a round snapshots into the half the round
+    before did not use and does not wait for that round's side launch; a half's checksums reach cs[] when the half is
+    reused or a full synchronisation retires it. Stepped 7 rounds per call (so up to three side launches overlap the
+    main stream) through the cascade and churn, every chunk against the oracle; fault_inject 1024 keeps one generation."""
+    for wl in (W.config3(n=1024, rounds=42, kill_round=5), W.config2(n=512, rounds=35)):
+        eng, ora = make_pair(wl.n, tuning=tuning)
+        run_chunked(eng, ora, wl.n, wl.rounds, wl.events, chunk=7)
