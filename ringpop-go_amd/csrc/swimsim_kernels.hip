@@ -1583,38 +1583,27 @@ __device__ bool wave_rows_differ_undo(const DS &d, const uint32_t *a, const uint
 // decision hashed the receiver's snapshot (a one-row chain, 3.3 ms, on the round's critical path in the cascade's
 // suspect wave). Any row whose content is unchanged since it was hashed to C_o has the sender's issue-time content, up
 // to a checksum collision that the word comparison itself rules out: the receiver's snapshot equal to such a row has
-// checksum C_o exactly. k_cs_reps indexes the clean rows of known checksum by that checksum (open addressing, 8-bit
-// build generation in the top byte, so the table is never cleared: an entry of another build reads as empty, and every
-// hit is verified against the row); it runs only when the phase deferred a decision.
+// checksum C_o exactly. k_cs_reps indexes the clean rows of known checksum by that checksum: a direct-mapped table of
+// plain 64-bit stores {8-bit build generation, row, checksum} (any row of a checksum will do, so the last store wins and
+// no atomic is needed: a first version with compare-and-swap probing spent 0.15-0.6 ms per build on the many rows that
+// share a checksum; two checksums on one slot lose one of them, whose decision then tries the undo log or the hash).
+// The table is never cleared (an entry of another build reads as empty) and every hit is verified against the row. It
+// runs only when the phase deferred a decision.
 __device__ __forceinline__ uint32_t rep_hash(uint32_t cs, uint32_t mask) { return fmix32(cs ^ 0x9E3779B9u) & mask; }
-constexpr uint32_t REP_PROBES = 64;
 __global__ void k_cs_reps(DS d, const uint32_t *defer_cnt, unsigned long long *tab, uint32_t mask, uint32_t gen) {
     const uint32_t ol = blockIdx.x * blockDim.x + threadIdx.x;
     if (*defer_cnt == 0 || ol >= d.NL) return;
     if (d.dirty[ol] || d.cpslot[ol] != SRC_NONE) return;
     const uint32_t cs = d.cs[ol];
-    const unsigned long long mine = ((unsigned long long)gen << 56) | ((unsigned long long)ol << 32) | cs;
-    for (uint32_t q = 0, s = rep_hash(cs, mask); q < REP_PROBES; q++, s = (s + 1) & mask) {
-        unsigned long long cur = __hip_atomic_load(tab + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        while ((uint32_t)(cur >> 56) != gen) {                      // empty for this build: claim it
-            const unsigned long long seen = atomicCAS(tab + s, cur, mine);
-            if (seen == cur) return;
-            cur = seen;
-        }
-        if ((uint32_t)cur == cs) return;                           // this checksum has a representative
-    }
+    tab[rep_hash(cs, mask)] = ((unsigned long long)gen << 56) | ((unsigned long long)ol << 32) | cs;
 }
 // a clean local row whose current checksum is cs, or SRC_NONE
 __device__ __forceinline__ uint32_t rep_find(const DS &d, const unsigned long long *tab, uint32_t mask, uint32_t gen,
                                              uint32_t cs) {
-    for (uint32_t q = 0, s = rep_hash(cs, mask); q < REP_PROBES; q++, s = (s + 1) & mask) {
-        const unsigned long long cur = tab[s];
-        if ((uint32_t)(cur >> 56) != gen) return SRC_NONE;
-        if ((uint32_t)cur != cs) continue;
-        const uint32_t r = (uint32_t)(cur >> 32) & 0xFFFFFFu;
-        return r < d.NL && !d.dirty[r] && d.cpslot[r] == SRC_NONE && d.cs[r] == cs ? r : SRC_NONE;
-    }
-    return SRC_NONE;
+    const unsigned long long cur = tab[rep_hash(cs, mask)];
+    if ((uint32_t)(cur >> 56) != gen || (uint32_t)cur != cs) return SRC_NONE;
+    const uint32_t r = (uint32_t)(cur >> 32) & 0xFFFFFFu;
+    return r < d.NL && !d.dirty[r] && d.cpslot[r] == SRC_NONE && d.cs[r] == cs ? r : SRC_NONE;
 }
 
 __global__ void k_defer_eq(DS d, const uint4 *defer, const uint32_t *defer_cnt, int phase, uint8_t *eq,
