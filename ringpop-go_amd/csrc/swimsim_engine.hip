@@ -2378,7 +2378,7 @@ __global__ void k_iota(uint32_t *list, uint32_t *cnt, uint32_t n) {
 int swimsim_bench_checksum(swimsim_t *h, uint32_t nrows, int32_t mode, int32_t reps, double *ms) {
     if (!h || !ms || nrows == 0 || nrows > h->NL || reps < 1) return SWIMSIM_EINVAL;
 #ifndef SWIMSIM_DIAG
-    if (mode < 0 || mode > 5 || mode == 3)
+    if (mode < 0 || mode > 6 || mode == 3)
         return h->fail(SWIMSIM_EINVAL, "checksum mode %d: diagnostics build only", mode);
     const bool csd = false;
 #else
@@ -2389,6 +2389,31 @@ int swimsim_bench_checksum(swimsim_t *h, uint32_t nrows, int32_t mode, int32_t r
     if (csd && (csd_alloc(h) || nrows > h->NL)) return h->fail(SWIMSIM_EINVAL, "reference-row path unavailable");
 #endif
     if (mode == 5 && csr_alloc(h)) return h->fail(SWIMSIM_EINVAL, "reference-row path unavailable");
+    // mode 6: the reference-row path with the side-stream buffer set on the side stream, as a round-end side launch runs
+    // it (nrows at most the set's rows), timed on that stream
+    if (mode == 6) {
+        if (!h->csr2.ready || nrows > h->csr2.rows) return h->fail(SWIMSIM_EINVAL, "side-stream reference-row path unavailable");
+        if (int rc = sync_side(h)) return rc;
+        hipLaunchKernelGGL(k_iota, dim3(blocks_for_threads(nrows)), dim3(256), 0, h->s, h->list, h->cnt, nrows);
+        HIPCHK(h, hipEventRecord(h->ev_snap, h->s));
+        HIPCHK(h, hipStreamWaitEvent(h->side, h->ev_snap, 0));
+        hipEvent_t a, b;
+        HIPCHK(h, hipEventCreate(&a));
+        HIPCHK(h, hipEventCreate(&b));
+        int rc6 = csr_hash(h, h->csr2, h->list, h->cnt, nrows, h->side);   // warm-up
+        HIPCHK(h, hipEventRecord(a, h->side));
+        for (int i = 0; i < reps && rc6 <= 0; i++) rc6 = csr_hash(h, h->csr2, h->list, h->cnt, nrows, h->side);
+        HIPCHK(h, hipEventRecord(b, h->side));
+        HIPCHK(h, hipEventSynchronize(b));
+        float t = 0;
+        hipEventElapsedTime(&t, a, b);
+        hipEventDestroy(a);
+        hipEventDestroy(b);
+        if (rc6 < 0) return rc6;
+        if (rc6 > 0) return h->fail(SWIMSIM_EINVAL, "side-stream reference-row path declined");
+        *ms = t / reps;
+        return check_err(h);
+    }
     int rc5 = 0;
     auto launch = [&]() {
         if (csd) {                                                 // the path itself, never declined here

@@ -39,12 +39,12 @@ for mode in "$@"; do
                 "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS" \
                 "TCC_HIT_sum TCC_MISS_sum"; do
       i=$((i+1))
-      timeout -k 10 -s KILL 400 rocprofv3 --pmc $pass --kernel-trace -d gpurun_out/pmc_$i -o run \
+      timeout -k 10 -s KILL 400 rocprofv3 --pmc $pass --kernel-trace -d /tmp/pmc_$i -o run \
         --output-format csv -- python3 bench.py $PROF_ARGS > gpurun_out/pmc_$i.log 2>&1
       rc=$?; echo "pmc pass $i ($pass) rc=$rc" >> gpurun_out/pmc_$i.log; [ $rc -eq 0 ] || exit $rc
     done
     dirs=""
-    for k in $(seq 1 $i); do dirs="$dirs $(dirname $(ls gpurun_out/pmc_$k/*/run_counter_collection.csv gpurun_out/pmc_$k/run_counter_collection.csv 2>/dev/null | head -n 1))"; done
+    for k in $(seq 1 $i); do dirs="$dirs $(dirname $(ls /tmp/pmc_$k/*/run_counter_collection.csv /tmp/pmc_$k/run_counter_collection.csv 2>/dev/null | head -n 1))"; done
     python3 tools/pmc_summary.py --workload $WL --window gpurun_out/pmc_summary.json $dirs || exit 1
     ;;&
   calib|all)

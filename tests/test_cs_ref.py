@@ -237,3 +237,20 @@ def test_colx_rebuild_after_raw_writes_every_round():
         bad = np.nonzero(eng.checksums() != ora.checksums())[0]
         assert len(bad) == 0, f"round {r}: {len(bad)} checksums differ, first rows {bad[:5]}"
         assert eng.digest() == ora.digest(), f"round {r}: state digest differs"
+
+
+def test_side_stream_path_on_real_cascade_rows():
+    """swimsim_bench_checksum mode 6: the reference-row path with the side-stream buffer set (csr2) on the side stream,
+    as a round-end side launch runs it, over the first 8,192 and 12,288 rows of a 16,384-member cascade in the suspect
+    wave: every checksum equals the engine's own (memberlist.go:83-128)."""
+    n = 16384
+    wl = W.config3(n=n, rounds=17, kill_round=10)
+    c = swimsim.Cluster(n)
+    for r in range(16):
+        c.step(1, wl.events_for(r))
+    ref = c.checksums().copy()
+    for rows in (8192, 12288):
+        ms = c.bench_checksum(rows, 6, reps=1)
+        got = c.checksums()
+        assert (got[:rows] == ref[:rows]).all(), f"{rows} rows: {(got[:rows] != ref[:rows]).sum()} differ"
+        print(f"side-stream path, {rows} rows: {ms:.2f} ms")
