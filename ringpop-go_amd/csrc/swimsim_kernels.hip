@@ -579,6 +579,73 @@ __device__ __forceinline__ uint32_t wave_issue_body(const DS &d, uint32_t ol, ui
             }
             pos += tot;
         }
+    } else if ((uint64_t)cnt * 4u > d.NP) {
+        // a long buffer (more than a quarter of the members: a partition's rows, config 4; churned rows, config 2): the
+        // walk streams the row's cells and words (most sectors are touched anyway at that density) instead of
+        // driving one gather per set presence bit; a member with a hot slot takes its cell and word from the slot
+        // (the dense cell is stale while it holds one). Deletions clear their presence bits one ballot per word.
+        const uint2 *dcell = d.dent + rb;
+        const uint32_t *drow = d.mw + rb;
+        for (uint32_t base = 0; base < d.NP; base += 64 * MB) {
+            uint2 ce[MB];
+            uint32_t wv[MB], hk[MB];
+#pragma unroll
+            for (int u = 0; u < MB; u++) {
+                const uint32_t m = base + u * 64 + lane_id();
+                const bool in = m < d.N;
+                hk[u] = in && d.hidx ? d.hidx[m] : SRC_NONE;
+                ce[u] = in ? dcell[m] : make_uint2(DE_NONE, 0);
+                wv[u] = in ? drow[m] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < MB; u++)
+                if (hk[u] != SRC_NONE) {
+                    ce[u] = d.hde[hb + hk[u]];
+                    wv[u] = d.hmw[hb + hk[u]];
+                }
+            bool keep[MB];
+            uint32_t nk = 0;
+#pragma unroll
+            for (int u = 0; u < MB; u++) {
+                keep[u] = de_p(ce[u].x) != DP_NONE &&
+                          !(RECV && de_src(ce[u].x) == sender && ce[u].y == sinc);   // filterChangesFromSender
+                nk += keep[u] ? 1u : 0u;
+            }
+            uint32_t tot;
+            uint32_t at = pos + wscan_excl(nk, tot);
+#pragma unroll
+            for (int u = 0; u < MB; u++) {
+                const uint32_t m = base + u * 64 + lane_id();
+                bool gone = false;
+                if (keep[u]) {
+                    const uint32_t st = (wv[u] & 7u) == ST_UNKNOWN ? ST_TOMB : (wv[u] & 7u);   // evicted: (tombstone, inc)
+                    if (at < cnt) d.pool[off + at] = rec_make(m, st, wv[u] >> 3, de_src(ce[u].x), ce[u].y, tag_of_slot(hk[u]));
+                    at++;
+                    if (RECV) {                                               // bump
+                        uint32_t nx;
+                        if ((int)(de_p(ce[u].x) + 1) >= maxp) {
+                            nx = ce[u].x | 0xFF000000u;
+                            gone = true;
+                            del++;
+                            delnh += hk[u] == SRC_NONE;
+                        } else {
+                            nx = ce[u].x + (1u << 24);
+                        }
+                        if (hk[u] != SRC_NONE) d.hde[hb + hk[u]].x = nx;
+                        else d.dent[rb + m].x = nx;
+                    }
+                }
+                if (RECV) {                                                   // (bits of members base + 64 u ..)
+                    const unsigned long long g = __ballot(gone);
+                    if (lane_id() == 0 && g) {
+                        const uint32_t w0 = (base + u * 64) >> 5;
+                        if ((uint32_t)g) atomicAnd(bits + w0, ~(uint32_t)g);
+                        if (g >> 32) atomicAnd(bits + w0 + 1, ~(uint32_t)(g >> 32));
+                    }
+                }
+            }
+            pos += tot;
+        }
     } else
     for (uint32_t q0 = 0; q0 < d.NBIT; q0 += 256) {
         const uint32_t q = q0 + lane_id() * 4;
