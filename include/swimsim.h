@@ -258,8 +258,9 @@ int swimsim_kernel_units(swimsim_t *h, const char **names, double *values, size_
 int swimsim_profile_mark(swimsim_t *h, uint32_t id);
 /* time the checksum kernel alone on the first nrows rows — average ms per launch. mode 0: the production choice for
  * nrows rows, 1: the wide kernel (k_checksum3), 2: the narrow kernel (k_checksum_q16), 4: k_checksum3 with four row
- * groups per workgroup, 5: the reference-row path forced (reference row, k_csd_scan, k_csr_rec, k_csr and the
- * fallback launches for the rows it leaves); other modes (diagnostic variants) only in the diagnostics library
+ * groups per workgroup, 5: the reference-row path forced (reference row, k_csd_scan, k_csr_rec, k_csr3 and the
+ * fallback launches for the rows it leaves), 6: the same on the side stream with its own buffer set (csr2; at most
+ * 12,288 rows; SWIMSIM_EINVAL when the set was not allocated); other modes (diagnostic variants) only in the diagnostics library
  * tools/libswimsim_diag.so */
 int swimsim_bench_checksum(swimsim_t *h, uint32_t nrows, int32_t mode, int32_t reps, double *ms);
 /* the reference-row checksum path so far (swimsim_checksum_ref.hip + swimsim_checksum_csr.hip; swimsim_tuning.cs_ref =
