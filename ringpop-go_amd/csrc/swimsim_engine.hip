@@ -284,6 +284,13 @@ struct swimsim {
     // phase C of a round can hash its rows on a side stream while the next round runs
     hipStream_t side = nullptr;
     hipEvent_t ev_snap = nullptr, ev_side[2] = {nullptr, nullptr};
+    hipEvent_t ev_rt = nullptr;                   // host round trips on the main stream (stream_sync)
+    // side generation g's launches run on side_st[g] (side, side2): two generations' latency-bound launches overlap
+    // instead of queueing behind each other; the side buffer set (csr2) is handed between them with ev_csr2
+    hipStream_t side2 = nullptr;
+    hipEvent_t ev_csr2 = nullptr;
+    bool csr2_used = false;
+    bool sync_spin = true;                        // stream_sync polls instead of sleeping in the runtime's wait
     bool cs_async = true, side_pending = false;
     // two generations of side slots (round 6): phase C of round r + 1 snapshots into the half round r did not use, so it
     // need not wait for round r's side launch; a half is retired (its checksums copied into cs[], its rows' cpslot
@@ -582,10 +589,26 @@ int build_tail_table(swimsim *h, uint32_t ecap) {
     return 0;
 }
 
+// wait for everything issued on the main stream so far (a host round trip: a count read back that sizes the next
+// launches). The runtime's stream wait sleeps once a short spin expires, and the wake-up costs tens of microseconds per
+// round trip (about 40 of them per round); polling an event returns as soon as the stream drains.
+hipError_t stream_sync(swimsim *h) {
+    if (!h->sync_spin || !h->ev_rt) return hipStreamSynchronize(h->s);
+    // (a launch error raised before the wait is returned here; the polls' "not ready" answers are cleared so that the
+    // round's closing hipGetLastError sees only real errors)
+    const hipError_t prior = hipPeekAtLastError();
+    hipError_t e = hipEventRecord(h->ev_rt, h->s);
+    if (e != hipSuccess) return e;
+    while ((e = hipEventQuery(h->ev_rt)) == hipErrorNotReady) {
+    }
+    (void)hipGetLastError();
+    return prior != hipSuccess ? prior : e;
+}
+
 int check_err(swimsim *h) {
     uint32_t e = 0;
     HIPCHK(h, hipMemcpyAsync(&e, h->d.err, 4, hipMemcpyDeviceToHost, h->s));
-    HIPCHK(h, hipStreamSynchronize(h->s));
+    HIPCHK(h, stream_sync(h));
     if (!e) return 0;
     hipMemsetAsync(h->d.err, 0, 4, h->s);
     if (e & E_POOL) return h->fail(SWIMSIM_ECAPACITY, "message pool overflow (raise message_pool_bytes)");
@@ -600,7 +623,7 @@ int check_err(swimsim *h) {
 int read_counters(swimsim *h, uint64_t *out /* [CTR_STRIDE] */) {
     std::vector<uint64_t> c((size_t)CTR_SHARDS * CTR_STRIDE);
     HIPCHK(h, hipMemcpyAsync(c.data(), h->d.ctr, c.size() * 8, hipMemcpyDeviceToHost, h->s));
-    HIPCHK(h, hipStreamSynchronize(h->s));
+    HIPCHK(h, stream_sync(h));
     for (int i = 0; i < CTR_STRIDE; i++) {
         uint64_t t = 0;
         for (int k = 0; k < CTR_SHARDS; k++) t += c[(size_t)k * CTR_STRIDE + i];
@@ -628,7 +651,7 @@ int sort_inbox(swimsim *h, uint32_t n, uint32_t *host_info) {
     hipLaunchKernelGGL(k_runs_info, dim3(blocks_for_threads(n)), dim3(256), 0, h->s, h->ukeys, h->counts, h->nruns, h->N,
                        h->info);
     HIPCHK(h, hipMemcpyAsync(host_info, h->info, 16, hipMemcpyDeviceToHost, h->s));
-    HIPCHK(h, hipStreamSynchronize(h->s));
+    HIPCHK(h, stream_sync(h));
     return 0;
 }
 
@@ -678,7 +701,7 @@ int xchg(swimsim *h) {
     }
     HIPCHK(h, hipMemcpyAsync(sz.data(), h->xsz, 2 * G * 8, hipMemcpyDeviceToHost, h->s));
     HIPCHK(h, hipMemcpyAsync(&nitems, h->xcnt, 4, hipMemcpyDeviceToHost, h->s));
-    HIPCHK(h, hipStreamSynchronize(h->s));
+    HIPCHK(h, stream_sync(h));
     h->x_syncs++;
     if (nitems > h->xcap) return h->fail(SWIMSIM_ECAPACITY, "exchange item list overflow (%u items)", nitems);
     // send segments: [parcel offset table][parcels], 16-byte aligned
@@ -708,7 +731,7 @@ int xchg(swimsim *h) {
                            h->xcap, h->sbuf, h->xseg, h->xtcur, h->xdcur);
     if (!dev_sizes) {
         // the packed segments are read by the peers (local copies) or staged through the host: complete them first
-        HIPCHK(h, hipStreamSynchronize(h->s));
+        HIPCHK(h, stream_sync(h));
         if (int rc = h->xp->sizes(sendsz.data(), recvsz.data(), 2)) return h->fail(rc, "shard size exchange failed (%s)", h->xp->name());
         h->x_syncs += 2;
     }
@@ -817,7 +840,7 @@ int csd_hash(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t n, 
             HIPCHK(h, hipMemsetAsync(h->csd_fbcnt, 0, 4, h->s));
             hipLaunchKernelGGL(k_csd_sample, dim3(CSD_NSAMPLE), dim3(256), 0, h->s, h->d, list, n, h->csd_B, h->csd_fbcnt);
             HIPCHK(h, hipMemcpyAsync(h->hinfo + 16, h->csd_fbcnt, 4, hipMemcpyDeviceToHost, h->s));
-            HIPCHK(h, hipStreamSynchronize(h->s));
+            HIPCHK(h, stream_sync(h));
             h->csd_last_mean = (double)h->hinfo[16] / CSD_NSAMPLE;
             if (h->csd_last_mean > (double)h->csd_maxdiff) { h->csd_declined++; return 1; }
         }
@@ -837,7 +860,7 @@ int csd_hash(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t n, 
     // rows the path left (flags): hashed by the production kernels
     uint32_t hf[1 + CSD_NFLAGS];
     HIPCHK(h, hipMemcpyAsync(h->hinfo + 16, h->csd_fbcnt, 4 * (1 + CSD_NFLAGS), hipMemcpyDeviceToHost, h->s));
-    HIPCHK(h, hipStreamSynchronize(h->s));
+    HIPCHK(h, stream_sync(h));
     memcpy(hf, h->hinfo + 16, sizeof hf);
     const uint32_t nf = hf[0];
     if (nf) {
@@ -1051,7 +1074,10 @@ int hash_rows(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t ma
         if (rc <= 0) return rc;                                    // done, or failed (h->err)
     }
     if (st && nrows != ~0u && csr_side_wanted(h, n)) {            // the same on the side stream, its own buffers
+        if (h->csr2_used) HIPCHK(h, hipStreamWaitEvent(st, h->ev_csr2, 0));   // (the other side stream's use of them)
         const int rc = csr_hash(h, h->csr2, list, cnt, n, st);
+        HIPCHK(h, hipEventRecord(h->ev_csr2, st));
+        h->csr2_used = true;
         if (rc <= 0) return rc;
     }
 #ifdef SWIMSIM_DIAG
@@ -1129,7 +1155,7 @@ int checksum_dirty(swimsim *h, int mode, bool async = false) {
     if (mode != 0) return hash_rows(h, h->list, h->cnt, h->NL, ~0u);
     uint32_t *hn = h->hinfo + 8;
     HIPCHK(h, hipMemcpyAsync(hn, h->cnt, 4, hipMemcpyDeviceToHost, h->s));
-    HIPCHK(h, hipStreamSynchronize(h->s));
+    HIPCHK(h, stream_sync(h));
     const uint32_t n = *hn;
     // async: snapshot the rows to hash, mark every dirty row clean (cpslot = the slot carrying its
     // checksum) and hash the snapshots on the side stream; the round reads cs[] only after sync_side
@@ -1143,9 +1169,10 @@ int checksum_dirty(swimsim *h, int mode, bool async = false) {
             hipLaunchKernelGGL(k_ctr_add, dim3(1), dim3(1), 0, h->s, h->d, (int)C_X_CS_DUP, (unsigned long long)(n - n2));
         }
         HIPCHK(h, hipEventRecord(h->ev_snap, h->s));
-        HIPCHK(h, hipStreamWaitEvent(h->side, h->ev_snap, 0));
-        if (int rc = hash_rows(h, ids, icnt, n2, n2, h->side)) return rc;
-        HIPCHK(h, hipEventRecord(h->ev_side[g], h->side));
+        hipStream_t ss = g == 0 || !h->side2 ? h->side : h->side2;
+        HIPCHK(h, hipStreamWaitEvent(ss, h->ev_snap, 0));
+        if (int rc = hash_rows(h, ids, icnt, n2, n2, ss)) return rc;
+        HIPCHK(h, hipEventRecord(h->ev_side[g], ss));
         h->side_pend[g] = true;
         h->side_pending = true;
         h->side_gen = (g + 1) % h->side_halves;
@@ -1180,7 +1207,7 @@ int checksum_dirty(swimsim *h, int mode, bool async = false) {
                            h->fpcnt);
         HIPCHK(h, hipMemcpyAsync(hn + 1, h->fpcnt, 4, hipMemcpyDeviceToHost, h->s));   // rows left after dedup:
     }
-    HIPCHK(h, hipStreamSynchronize(h->s));                                         // picks the variant
+    HIPCHK(h, stream_sync(h));                                         // picks the variant
     if (side_ok && hn[1] <= h->snap_cap) return go_side(h->fplist, hn[1], h->fpv_s, h->dup_of);
     if (int rc = hash_rows(h, h->fplist, h->fpcnt, n, hn[1])) return rc;          // (sorted to row order there)
     Scope sc(h, F_CSPREP);
@@ -1202,7 +1229,7 @@ int bound_lazy_snapshots(swimsim *h, int mode) {
                        h->list, h->cnt);
     uint32_t *hc = h->hinfo + 12;
     HIPCHK(h, hipMemcpyAsync(hc, h->cnt, 4, hipMemcpyDeviceToHost, h->s));
-    HIPCHK(h, hipStreamSynchronize(h->s));
+    HIPCHK(h, stream_sync(h));
     if (*hc <= h->d.dense_cap / 2) return 0;
     if (int rc = sync_side(h)) return rc;
     if (int rc = hash_rows(h, h->list, h->cnt, h->NL, *hc)) return rc;
@@ -1249,7 +1276,7 @@ int resolve_deferred(swimsim *h, int phase, MsgDesc *rdesc, uint32_t maxn) {
         uint32_t *hc = h->hinfo + 10;
         HIPCHK(h, hipMemcpyAsync(hc, h->cnt, 4, hipMemcpyDeviceToHost, h->s));
         HIPCHK(h, hipMemcpyAsync(hc + 1, h->cnt + 1, 4, hipMemcpyDeviceToHost, h->s));
-        HIPCHK(h, hipStreamSynchronize(h->s));
+        HIPCHK(h, stream_sync(h));
         // the list holds main-stream snapshot slots only (k_defer_ids), so their hash needs nothing from the side
         // stream and runs beside the previous phase C's side-stream launch (both are latency-bound launches of
         // few rows); k_recv_finish then compares with side-stream checksums, so it waits for the side stream
@@ -1372,7 +1399,7 @@ int do_heal(swimsim *h, uint32_t o, std::vector<int32_t> *ret) {
     if (me) {
         std::vector<uint32_t> row(h->NP);
         HIPCHK(h, hipMemcpyAsync(row.data(), h->d.mw + (size_t)ol * h->NP, h->NP * 4, hipMemcpyDeviceToHost, h->s));
-        HIPCHK(h, hipStreamSynchronize(h->s));
+        HIPCHK(h, stream_sync(h));
         for (uint32_t m = 0; m < h->N; m++)                                  // heal_via_discover_provider.go:136-142
             if ((row[m] & 7u) >= ST_FAULTY) targets.push_back((int32_t)m);
         for (uint32_t i = 0; i < targets.size(); i++) {                      // ShuffleStringsInPlace (util.go:189-194)
@@ -1425,7 +1452,7 @@ int do_heal(swimsim *h, uint32_t o, std::vector<int32_t> *ret) {
             hipLaunchKernelGGL(k_heal_diff, dim3(1), dim3(64), 0, h->s, h->d, h->hdesc + 0, h->hdesc + 1, h->hdesc + 2,
                                h->hdesc + 3);
             HIPCHK(h, hipMemcpyAsync(hd, h->hdesc, sizeof hd, hipMemcpyDeviceToHost, h->s));
-            HIPCHK(h, hipStreamSynchronize(h->s));
+            HIPCHK(h, stream_sync(h));
             if (hd[0].kind != 1 || hd[1].kind != 1) return h->fail(SWIMSIM_ECAPACITY, "dense snapshot pool overflow in heal");
             lens[0] = hd[2].len;
             lens[1] = hd[3].len;
@@ -1447,7 +1474,7 @@ int do_heal(swimsim *h, uint32_t o, std::vector<int32_t> *ret) {
             std::vector<uint32_t> mb(h->NP);                                 // pingableHosts(MB)
             HIPCHK(h, hipMemcpyAsync(mb.data(), h->d.dense + (size_t)hd[1].off_lo * h->NP, h->NP * 4,
                                      hipMemcpyDeviceToHost, h->s));
-            HIPCHK(h, hipStreamSynchronize(h->s));
+            HIPCHK(h, stream_sync(h));
             for (uint32_t m = 0; m < h->N; m++) {
                 const uint32_t st = mb[m] & 7u;
                 if (st != ST_UNKNOWN && is_pingable(st == ST_TOMB ? ST_FAULTY : st)) del(targets, (int32_t)m);
@@ -1540,7 +1567,7 @@ int step_one(swimsim *h, const swimsim_event *ev, size_t nev) {
     // (the failed-ping count info[2] reaches the host with sort_inbox's copy of info[0..3]; a sharded inbox size
     // needs its own round trip first)
     if (sharded) {
-        HIPCHK(h, hipStreamSynchronize(h->s));
+        HIPCHK(h, stream_sync(h));
         ninbox = std::min(hi[5], h->keycap);
     }
     if (int rc = sort_inbox(h, ninbox, hi)) return rc;
@@ -1583,7 +1610,7 @@ int step_one(swimsim *h, const swimsim_event *ev, size_t nev) {
             HIPCHK(h, hipMemcpyAsync(h->npairs, &ninbox2, 4, hipMemcpyHostToDevice, h->s));
             if (int rc = xchg(h)) return rc;
             HIPCHK(h, hipMemcpyAsync(&hi[5], h->npairs, 4, hipMemcpyDeviceToHost, h->s));
-            HIPCHK(h, hipStreamSynchronize(h->s));
+            HIPCHK(h, stream_sync(h));
             ninbox2 = std::min(hi[5], h->keycap);
         }
         if (int rc = sort_inbox(h, ninbox2, hi)) return rc;
@@ -1643,7 +1670,7 @@ int ensure_ecap(swimsim *h, uint32_t upto) {
         return h->fail(SWIMSIM_ERANGE, "incarnation step %u beyond the checksum tables (at most 2^24 steps of the period)", upto);
     uint32_t c = h->ecap;
     while (c <= upto) c = c >= kMaxEcap / 2 ? kMaxEcap : c * 2;
-    HIPCHK(h, hipStreamSynchronize(h->s));
+    HIPCHK(h, stream_sync(h));
     return build_tail_table(h, c);
 }
 
@@ -1775,9 +1802,12 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
     }
     if (hipStreamCreateWithFlags(&h->s, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&h->side2, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&h->ev_csr2, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_snap, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_side[0], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&h->ev_side[1], hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&h->ev_side[1], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&h->ev_rt, hipEventDisableTiming) != hipSuccess) {
         h->err = "hipStreamCreate / hipEventCreate failed";
         return bail(SWIMSIM_EHIP);
     }
@@ -1788,6 +1818,9 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
     if (tun && tun->fault_inject > 0) h->fault_inject = tun->fault_inject;
     if (h->fault_inject & 32) h->csr_ecap = 24;      // (tests: rows whose exception entries end within CSR_EREG of the cap)
     if (h->fault_inject & 256) h->csr_side_min = 1024;   // (tests: side launches of 1,024 rows and more take the path)
+    if (const char *v = getenv("SWIMSIM_SYNC_SPIN")) h->sync_spin = atoi(v) != 0;   // (experiment: 0 = the runtime's wait)
+    if (const char *v = getenv("SWIMSIM_SIDE2"))                  // (experiment: 0 = one side stream for both generations)
+        if (atoi(v) == 0 && h->side2) { hipStreamDestroy(h->side2); h->side2 = nullptr; }
 #ifdef SWIMSIM_DIAG                                 // diagnostics library only: the reference-row path
     if (const char *v = getenv("SWIMSIM_CS_DELTA")) h->csd_mode = atoi(v);
     if (const char *v = getenv("SWIMSIM_CS_DELTA_MAXDIFF")) h->csd_maxdiff = (uint32_t)strtoul(v, nullptr, 10);
@@ -1997,6 +2030,7 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
 int swimsim_destroy(swimsim_t *h) {
     if (!h) return SWIMSIM_OK;
     if (h->side) hipStreamSynchronize(h->side);
+    if (h->side2) hipStreamSynchronize(h->side2);
     if (h->s) hipStreamSynchronize(h->s);
     for (auto &t : h->pending) { hipEventDestroy(t.a); hipEventDestroy(t.b); }
     for (auto e : h->round_ev) hipEventDestroy(e);
@@ -2007,9 +2041,12 @@ int swimsim_destroy(swimsim_t *h) {
     h->xp.reset();
     if (h->hinfo) hipHostFree(h->hinfo);
     if (h->ev_snap) hipEventDestroy(h->ev_snap);
+    if (h->ev_rt) hipEventDestroy(h->ev_rt);
     for (hipEvent_t e : h->ev_side)
         if (e) hipEventDestroy(e);
     if (h->side) hipStreamDestroy(h->side);
+    if (h->side2) hipStreamDestroy(h->side2);
+    if (h->ev_csr2) hipEventDestroy(h->ev_csr2);
     if (h->s) hipStreamDestroy(h->s);
     delete h;
     return SWIMSIM_OK;
@@ -2043,7 +2080,7 @@ int swimsim_set_member(swimsim_t *h, uint32_t o, uint32_t m, int32_t status, int
     hot_reset(h, true);
     HIPCHK(h, hipMemcpyAsync(h->d.mw + (size_t)(o - h->lo) * h->NP + m, &w, 4, hipMemcpyHostToDevice, h->s));
     hipLaunchKernelGGL(k_recount, dim3(1), dim3(64), 0, h->s, h->d, o - h->lo);
-    HIPCHK(h, hipStreamSynchronize(h->s));
+    HIPCHK(h, stream_sync(h));
     return SWIMSIM_OK;
 }
 
@@ -2067,7 +2104,7 @@ int swimsim_set_row(swimsim_t *h, uint32_t o, const uint8_t *status, const int64
     HIPCHK(h, hipMemcpyAsync(h->d.mw + (size_t)(o - h->lo) * h->NP, row.data(), (size_t)h->N * 4,
                              hipMemcpyHostToDevice, h->s));
     hipLaunchKernelGGL(k_recount, dim3(1), dim3(64), 0, h->s, h->d, o - h->lo);
-    HIPCHK(h, hipStreamSynchronize(h->s));
+    HIPCHK(h, stream_sync(h));
     return SWIMSIM_OK;
 }
 
@@ -2079,14 +2116,14 @@ int swimsim_make_change(swimsim_t *h, uint32_t o, uint32_t m, int64_t inc_ms, in
     if (int rc = flush_events(h, b)) return rc;
     uint32_t applied = 0;
     HIPCHK(h, hipMemcpyAsync(&applied, h->ev_applied, 4, hipMemcpyDeviceToHost, h->s));
-    HIPCHK(h, hipStreamSynchronize(h->s));
+    HIPCHK(h, stream_sync(h));
     return (int)applied;
 }
 
 int swimsim_clear_changes(swimsim_t *h, uint32_t o) {
     if (!h || !own(h, o)) return SWIMSIM_EINVAL;
     hipLaunchKernelGGL(k_clear_changes, dim3(1), dim3(256), 0, h->s, h->d, o - h->lo);
-    HIPCHK(h, hipStreamSynchronize(h->s));
+    HIPCHK(h, stream_sync(h));
     return SWIMSIM_OK;
 }
 
@@ -2123,7 +2160,7 @@ int swimsim_add_join_list(swimsim_t *h, uint32_t o, const int32_t *member, const
                            h->ev_applied);
         HIPCHK(h, hipMemcpyAsync(&napp, h->ev_applied, 4, hipMemcpyDeviceToHost, h->s));
     }
-    HIPCHK(h, hipStreamSynchronize(h->s));
+    HIPCHK(h, stream_sync(h));
     if (applied) *applied = napp;
     return check_err(h);
 }
@@ -2204,7 +2241,7 @@ int swimsim_row(swimsim_t *h, uint32_t o, uint8_t *status, int64_t *inc_ms) {
     if (!h || !own(h, o)) return SWIMSIM_EINVAL;
     std::vector<uint32_t> row(h->NP);
     HIPCHK(h, hipMemcpyAsync(row.data(), h->d.mw + (size_t)(o - h->lo) * h->NP, h->NP * 4, hipMemcpyDeviceToHost, h->s));
-    HIPCHK(h, hipStreamSynchronize(h->s));
+    HIPCHK(h, stream_sync(h));
     for (uint32_t m = 0; m < h->N; m++) {
         if (status) status[m] = (uint8_t)(row[m] & 7u);
         if (inc_ms) inc_ms[m] = from_e(h, row[m] >> 3);
@@ -2243,7 +2280,7 @@ int swimsim_node_stats(swimsim_t *h, uint32_t o, int32_t *pingable, int32_t *max
     HIPCHK(h, hipMemcpyAsync(&v[0], h->d.ping + ol, 4, hipMemcpyDeviceToHost, h->s));
     HIPCHK(h, hipMemcpyAsync(&v[1], h->d.maxp + ol, 4, hipMemcpyDeviceToHost, h->s));
     HIPCHK(h, hipMemcpyAsync(&v[2], h->d.dcnt + ol, 4, hipMemcpyDeviceToHost, h->s));
-    HIPCHK(h, hipStreamSynchronize(h->s));
+    HIPCHK(h, stream_sync(h));
     if (pingable) *pingable = v[0];
     if (maxp) *maxp = v[1];
     if (changes) *changes = v[2];
@@ -2264,7 +2301,7 @@ int swimsim_changes(swimsim_t *h, uint32_t o, int32_t *member, int32_t *p, int32
     std::vector<uint2> ent(h->NP);
     hot_flush(h, o - h->lo, 1);                                     // hot members' cells live in their slots
     HIPCHK(h, hipMemcpyAsync(ent.data(), h->d.dent + base, h->NP * 8, hipMemcpyDeviceToHost, h->s));
-    HIPCHK(h, hipStreamSynchronize(h->s));
+    HIPCHK(h, stream_sync(h));
     size_t k = 0;
     for (uint32_t m = 0; m < h->N; m++) {
         const uint32_t pm = de_p(ent[m].x), src = de_src(ent[m].x);
@@ -2289,7 +2326,7 @@ int swimsim_timers(swimsim_t *h, uint32_t o, int32_t *member, int32_t *state, in
     std::vector<uint2> aux(h->NP);
     HIPCHK(h, hipMemcpyAsync(ts.data(), h->d.tst + base, h->NP, hipMemcpyDeviceToHost, h->s));
     HIPCHK(h, hipMemcpyAsync(aux.data(), h->d.tmr + base, h->NP * 8, hipMemcpyDeviceToHost, h->s));
-    HIPCHK(h, hipStreamSynchronize(h->s));
+    HIPCHK(h, stream_sync(h));
     size_t k = 0;
     for (uint32_t m = 0; m < h->N; m++) {
         if (!(ts[m] & 7u)) continue;
@@ -2312,7 +2349,7 @@ int swimsim_iter_state(swimsim_t *h, uint32_t o, int64_t *idx, uint32_t *epoch) 
     uint32_t ep;
     HIPCHK(h, hipMemcpyAsync(&i, h->d.it_idx + (o - h->lo), 4, hipMemcpyDeviceToHost, h->s));
     HIPCHK(h, hipMemcpyAsync(&ep, h->d.it_ep + (o - h->lo), 4, hipMemcpyDeviceToHost, h->s));
-    HIPCHK(h, hipStreamSynchronize(h->s));
+    HIPCHK(h, stream_sync(h));
     if (idx) *idx = i;
     if (epoch) *epoch = ep;
     return SWIMSIM_OK;
@@ -2321,7 +2358,7 @@ int swimsim_iter_state(swimsim_t *h, uint32_t o, int64_t *idx, uint32_t *epoch) 
 int swimsim_last_targets(swimsim_t *h, int32_t *out) {
     if (!h || !out) return SWIMSIM_EINVAL;
     HIPCHK(h, hipMemcpyAsync(out, h->tgt, h->NL * 4, hipMemcpyDeviceToHost, h->s));
-    HIPCHK(h, hipStreamSynchronize(h->s));
+    HIPCHK(h, stream_sync(h));
     return SWIMSIM_OK;
 }
 
@@ -2339,7 +2376,7 @@ int swimsim_digest(swimsim_t *h, uint64_t *rows, uint64_t *dis, uint64_t *tim) {
     hipLaunchKernelGGL(k_digest, dim3(blocks_for_waves(h->NL)), dim3(SWIM_WAVE_BLOCK), 0, h->s, h->d, h->digest_buf, 0u);
     unsigned long long v[3];
     HIPCHK(h, hipMemcpyAsync(v, h->digest_buf, 24, hipMemcpyDeviceToHost, h->s));
-    HIPCHK(h, hipStreamSynchronize(h->s));
+    HIPCHK(h, stream_sync(h));
     if (rows) *rows = v[0];
     if (dis) *dis = v[1];
     if (tim) *tim = v[2];
@@ -2352,7 +2389,7 @@ int swimsim_converged(swimsim_t *h, int32_t *out) {
     std::vector<int32_t> dc(h->NL);
     if (int rc = swimsim_checksums(h, cs.data())) return rc;
     HIPCHK(h, hipMemcpyAsync(dc.data(), h->d.dcnt, h->NL * 4, hipMemcpyDeviceToHost, h->s));
-    HIPCHK(h, hipStreamSynchronize(h->s));
+    HIPCHK(h, stream_sync(h));
     bool ok = true, have = false;
     uint32_t first = 0;
     for (uint32_t ol = 0; ol < h->NL && ok; ol++) {
@@ -2463,7 +2500,7 @@ int swimsim_debug_cs_stream(swimsim_t *h, uint32_t ol, uint32_t *out, size_t cap
     HIPCHK(h, hipMemcpyAsync(h->cnt, &one, 4, hipMemcpyHostToDevice, h->s));
     launch_checksum_dump(h->d, h->list, h->cnt, dev, (uint32_t)cap_words, h->s);
     HIPCHK(h, hipMemcpyAsync(out, dev, cap_words * 4, hipMemcpyDeviceToHost, h->s));
-    HIPCHK(h, hipStreamSynchronize(h->s));
+    HIPCHK(h, stream_sync(h));
     hipFree(dev);
     return check_err(h);
 #endif
@@ -2479,7 +2516,7 @@ int swimsim_profile_mark(swimsim_t *h, uint32_t id) {
     if (!h) return SWIMSIM_EINVAL;
     if (int rc = sync_side(h)) return rc;
     hipLaunchKernelGGL(k_profile_mark, dim3(1), dim3(64), 0, h->s, id, h->scratch);
-    HIPCHK(h, hipStreamSynchronize(h->s));
+    HIPCHK(h, stream_sync(h));
     return SWIMSIM_OK;
 }
 
@@ -2526,13 +2563,13 @@ int swimsim_watch(swimsim_t *h, uint32_t o, int32_t on) {
         HIPCHK(h, hipMemsetAsync(h->d.wlog + (size_t)slot * h->NP, 0, (size_t)h->NP * 16, h->s));
         HIPCHK(h, hipMemcpyAsync(h->d.wslot + ol, &slot, 4, hipMemcpyHostToDevice, h->s));
         HIPCHK(h, hipMemcpyAsync(&h->wcs[slot], h->d.cs + ol, 4, hipMemcpyDeviceToHost, h->s));
-        HIPCHK(h, hipStreamSynchronize(h->s));
+        HIPCHK(h, stream_sync(h));
         h->wused[slot] = 1;
         h->wslot_h[ol] = slot;
     } else if (!on && slot != SRC_NONE) {
         const uint32_t none = SRC_NONE;
         HIPCHK(h, hipMemcpyAsync(h->d.wslot + ol, &none, 4, hipMemcpyHostToDevice, h->s));
-        HIPCHK(h, hipStreamSynchronize(h->s));
+        HIPCHK(h, stream_sync(h));
         h->wused[slot] = 0;
         h->wslot_h[ol] = SRC_NONE;
         h->d.wev_mask &= ~(1ull << slot);
@@ -2550,7 +2587,7 @@ int swimsim_watch(swimsim_t *h, uint32_t o, int32_t on) {
         if (int rc = checksum_dirty(h, 0)) return rc;
         HIPCHK(h, hipMemsetAsync(h->d.wev_cnt + slot, 0, 4, h->s));
         HIPCHK(h, hipMemcpyAsync(&h->wcs_ev[slot], h->d.cs + ol, 4, hipMemcpyDeviceToHost, h->s));
-        HIPCHK(h, hipStreamSynchronize(h->s));
+        HIPCHK(h, stream_sync(h));
         h->d.wev_mask |= 1ull << slot;
     } else if (on == 1) {
         h->d.wev_mask &= ~(1ull << slot);
@@ -2577,7 +2614,7 @@ int swimsim_applied_events(swimsim_t *h, uint32_t o, int32_t *member, int32_t *s
     HIPCHK(h, hipMemcpyAsync(&cs, h->d.cs + ol, 4, hipMemcpyDeviceToHost, h->s));
     uint32_t known = 0;
     HIPCHK(h, hipMemcpyAsync(&known, h->winfo, 4, hipMemcpyDeviceToHost, h->s));
-    HIPCHK(h, hipStreamSynchronize(h->s));
+    HIPCHK(h, stream_sync(h));
     if (cnt > h->d.wev_cap) {
         HIPCHK(h, hipMemsetAsync(h->d.wev_cnt + slot, 0, 4, h->s));
         h->wcs_ev[slot] = cs;
@@ -2591,7 +2628,7 @@ int swimsim_applied_events(swimsim_t *h, uint32_t o, int32_t *member, int32_t *s
         HIPCHK(h, hipMemcpyAsync(tag.data(), h->wevt_h[slot], (size_t)cnt * 8, hipMemcpyDeviceToHost, h->s));
     }
     HIPCHK(h, hipMemsetAsync(h->d.wev_cnt + slot, 0, 4, h->s));
-    HIPCHK(h, hipStreamSynchronize(h->s));
+    HIPCHK(h, stream_sync(h));
     std::vector<uint32_t> ord(cnt);
     for (uint32_t i = 0; i < cnt; i++) ord[i] = i;
     std::sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) {
@@ -2632,11 +2669,11 @@ int swimsim_applied_changes(swimsim_t *h, uint32_t o, int32_t *member, int32_t *
     uint32_t info[2] = {0, 0}, cs = 0;
     HIPCHK(h, hipMemcpyAsync(info, h->winfo, 8, hipMemcpyDeviceToHost, h->s));
     HIPCHK(h, hipMemcpyAsync(&cs, h->d.cs + ol, 4, hipMemcpyDeviceToHost, h->s));
-    HIPCHK(h, hipStreamSynchronize(h->s));
+    HIPCHK(h, stream_sync(h));
     std::vector<uint4> rec(info[0]);
     if (info[0]) {
         HIPCHK(h, hipMemcpyAsync(rec.data(), h->wout, (size_t)info[0] * 16, hipMemcpyDeviceToHost, h->s));
-        HIPCHK(h, hipStreamSynchronize(h->s));
+        HIPCHK(h, stream_sync(h));
     }
     for (size_t i = 0; i < rec.size() && i < cap; i++) {
         const uint4 v = rec[i];
@@ -2799,7 +2836,7 @@ int swimsim_kernel_units(swimsim_t *h, const char **names, double *values, size_
     uint32_t hot = 0;                                              // hot slots in use now (not a delta)
     if (h->d.hot_cnt) {
         HIPCHK(h, hipMemcpyAsync(&hot, h->d.hot_cnt, 4, hipMemcpyDeviceToHost, h->s));
-        HIPCHK(h, hipStreamSynchronize(h->s));
+        HIPCHK(h, stream_sync(h));
     }
     const size_t k = sizeof(ki) / sizeof(ki[0]);
     for (size_t i = 0; i < k && i < cap; i++) {
@@ -2967,7 +3004,7 @@ int swimsim_checksum_path_stats(swimsim_t *h, uint64_t *delta_launches, uint64_t
         if (!c->ready) continue;            // counted on the device (k_csr_fbsplit), both buffer sets
         unsigned long long a2[8];
         HIPCHK(h, hipMemcpyAsync(a2, c->acc, sizeof a2, hipMemcpyDeviceToHost, h->s));
-        HIPCHK(h, hipStreamSynchronize(h->s));
+        HIPCHK(h, stream_sync(h));
         for (int i = 0; i < 8; i++) acc[i] += a2[i];
     }
     if (delta_launches) *delta_launches = h->csr_launches;
