@@ -350,6 +350,7 @@ struct swimsim {
     uint32_t *defer_cnt = nullptr;
     uint8_t *defer_eq = nullptr;                  // deferred decision settled by row equality
     unsigned long long *rep_tab = nullptr;        // checksum representatives (k_cs_reps), rep_mask + 1 entries
+    unsigned long long *fp_tab = nullptr;         // phase-C dedup groups (k_fp_table): two tables of 2 (rep_mask + 1)
     uint32_t rep_mask = 0, rep_gen = 0;
     uint32_t *exh_list = nullptr, *exh_cnt = nullptr, *scratch = nullptr;
     uint8_t *need = nullptr, *fsflag = nullptr;
@@ -1056,9 +1057,10 @@ int csr_hash(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t n, 
 // list / fplist the caller is not using; neither is read again in its old order.
 // Returns 0 or a negative SWIMSIM_E* code (h->err set); every caller passes it on.
 int hash_rows(swimsim *h, const uint32_t *list, const uint32_t *cnt, uint32_t maxn, uint32_t nrows,
-              hipStream_t st = nullptr) {
+              hipStream_t st = nullptr, bool ordered = false) {
     if (std::min(maxn, nrows) == 0) return 0;
-    if (!st && nrows != ~0u && nrows >= 64 && nrows <= h->NL && (list == h->list || list == h->fplist)) {
+    // (lists compacted with atomics are sorted to row order: the same rows per workgroup in every run, close in memory)
+    if (!st && !ordered && nrows != ~0u && nrows >= 64 && nrows <= h->NL && (list == h->list || list == h->fplist)) {
         Scope sc(h, F_CSPREP);
         uint32_t *out = list == h->list ? h->fplist : h->list;
         const uint32_t maxid = h->NL + h->d.dense_cap;
@@ -1185,33 +1187,26 @@ int checksum_dirty(swimsim *h, int mode, bool async = false) {
     }
     {
         Scope sc(h, F_CSPREP);
-        // (k_list compacts with atomics: its order changes from run to run. Sorted by row first, the stable
-        // fingerprint sort leaves every group in row order, so the group heads, the rows hashed and the reference-row
-        // path's fallbacks are the same in every run of one command)
-        size_t bytes = h->cub_bytes;
-        HIPCHK(h, hipcub::DeviceRadixSort::SortKeys(h->cub_tmp, bytes, h->list, h->fplist, (int)n, 0,
-                                                    32 - __builtin_clz(h->NL), h->s));
-        hipLaunchKernelGGL(k_fp_keys, dim3(blocks_for_threads(n)), dim3(256), 0, h->s, h->d, h->fplist, n, h->keys, h->fpv,
-                           (h->fault_inject & 8) ? 7ull : ~0ull);
-        bytes = h->cub_bytes;
-        HIPCHK(h, hipcub::DeviceRadixSort::SortPairs(h->cub_tmp, bytes, h->keys, h->keys_sorted, h->fpv, h->fpv_s, (int)n, 0,
-                                                     64, h->s));
-        hipLaunchKernelGGL(k_fp_heads, dim3(blocks_for_threads(n)), dim3(256), 0, h->s, h->keys_sorted, n, h->fph);
-        hipLaunchKernelGGL(k_ucols, dim3(1), dim3(1024), 0, h->s, h->d);   // (k_fp_verify compares by them)
-        bytes = h->cub_bytes;
-        HIPCHK(h, hipcub::DeviceScan::InclusiveScan(h->cub_tmp, bytes, h->fph, h->fph_s, hipcub::Max(), (int)n, h->s));
-        HIPCHK(h, hipMemsetAsync(h->fpcnt, 0, 4, h->s));
-        hipLaunchKernelGGL(k_fp_verify, dim3(blocks_for_waves(n)), dim3(SWIM_WAVE_BLOCK), 0, h->s, h->d, h->fpv_s, h->fph_s, n, h->hflag,
-                           h->dup_of);
-        hipLaunchKernelGGL(k_list_flagged, dim3(blocks_for_threads(h->NL)), dim3(256), 0, h->s, h->NL, h->hflag, h->fplist,
-                           h->fpcnt);
+        // groups by fingerprint without sorting (k_fp_table: the smallest {tag, row} offer wins a slot, so the heads and
+        // the rows hashed are the same in every run of one command, whatever order k_list's atomics left the list in)
+        const unsigned long long keymask = (h->fault_inject & 8) ? 7ull : ~0ull;
+        const uint32_t fmask = 2u * (h->rep_mask + 1u) - 1u;       // (two tables of 4 NL slots or more)
+        HIPCHK(h, hipMemsetAsync(h->fp_tab, 0xFF, (size_t)(fmask + 1) * 2 * 8, h->s));
+        for (int pass = 0; pass < 2; pass++)
+            hipLaunchKernelGGL(k_fp_table, dim3(blocks_for_threads(n)), dim3(256), 0, h->s, h->d, h->list, n, h->fp_tab,
+                               fmask, keymask, pass);
+        hipLaunchKernelGGL(k_ucols, dim3(1), dim3(1024), 0, h->s, h->d);   // (k_fp_verify_tab compares by them)
+        hipLaunchKernelGGL(k_fp_verify_tab, dim3(blocks_for_waves(n)), dim3(SWIM_WAVE_BLOCK), 0, h->s, h->d, h->list, n,
+                           h->fp_tab, fmask, keymask, h->hflag, h->dup_of);
+        // the rows to hash in row order (one workgroup): no sort before the hash either
+        hipLaunchKernelGGL(k_list_flagged_ordered, dim3(1), dim3(1024), 0, h->s, h->NL, h->hflag, h->fplist, h->fpcnt);
         HIPCHK(h, hipMemcpyAsync(hn + 1, h->fpcnt, 4, hipMemcpyDeviceToHost, h->s));   // rows left after dedup:
     }
-    HIPCHK(h, stream_sync(h));                                         // picks the variant
-    if (side_ok && hn[1] <= h->snap_cap) return go_side(h->fplist, hn[1], h->fpv_s, h->dup_of);
-    if (int rc = hash_rows(h, h->fplist, h->fpcnt, n, hn[1])) return rc;          // (sorted to row order there)
+    HIPCHK(h, stream_sync(h));                                                      // picks the variant
+    if (side_ok && hn[1] <= h->snap_cap) return go_side(h->fplist, hn[1], h->list, h->dup_of);
+    if (int rc = hash_rows(h, h->fplist, h->fpcnt, n, hn[1], nullptr, true)) return rc;
     Scope sc(h, F_CSPREP);
-    hipLaunchKernelGGL(k_fp_copy, dim3(blocks_for_threads(n)), dim3(256), 0, h->s, h->d, h->fpv_s, n, h->dup_of);
+    hipLaunchKernelGGL(k_fp_copy, dim3(blocks_for_threads(n)), dim3(256), 0, h->s, h->d, h->list, n, h->dup_of);
     return 0;
 }
 
@@ -1959,6 +1954,7 @@ int swimsim_create(const swimsim_config *cfg, swimsim_t **out) {
         (rc = dalloc(h, &h->cnt, 2, "cnt")) || (rc = dalloc(h, &h->defer, KC + 2 * (size_t)h->NL + 64, "defer")) ||
         (rc = dalloc(h, &h->defer_eq, KC + 2 * (size_t)h->NL + 64, "defer eq")) ||
         (rc = dalloc(h, &h->rep_tab, (size_t)rep_slots(h->NL), "checksum representatives")) ||
+        (rc = dalloc(h, &h->fp_tab, (size_t)rep_slots(h->NL) * 4, "dedup groups")) ||
         (rc = dalloc(h, &h->d.ulog, (size_t)h->NL * ULOG_CAP, "receive-phase undo log")) ||
         (rc = dalloc(h, &h->d.ulog_cnt, (size_t)h->NL, "receive-phase undo log counts")) ||
         (rc = dalloc(h, &h->defer_cnt, 1, "defer_cnt")) || (rc = dalloc(h, &h->exh_list, h->NL, "exh_list")) ||

@@ -1903,6 +1903,92 @@ __global__ void k_list_flagged(uint32_t nl, uint8_t *flag, uint32_t *list, uint3
     list[atomicAdd(cnt, 1u)] = ol;
 }
 
+// Round 6: the groups without a sort. Every listed row offers {tag, row} to slot (fp & mask) of a direct-mapped table
+// (tag = the fingerprint's high word); the smallest offer wins (atomicMin), so the winner does not depend on the list's
+// order or on timing. A row whose slot was won by another tag offers itself again to a second table at slot
+// (tag & mask) (the rows that do is again the same set in every run), so that few duplicate groups lose their dedup to
+// a slot conflict. A row compares itself with the winner of the first of its slots that holds its own tag (its group
+// head); rows that find none are hashed themselves. Exact either way: equality is decided by the comparison.
+__device__ __forceinline__ void fp_slot_tag(unsigned long long fp, uint32_t mask, uint32_t &slot, uint32_t &slot2,
+                                            uint32_t &tag) {
+    slot = (uint32_t)fp & mask;
+    tag = (uint32_t)(fp >> 32);
+    slot2 = (tag ^ (uint32_t)(fp >> 13)) & mask;
+}
+// pass 0: every listed row into table 0; pass 1: the rows whose table-0 slot holds another tag into table 1
+__global__ void k_fp_table(DS d, const uint32_t *list, uint32_t n, unsigned long long *tab, uint32_t mask,
+                           unsigned long long keymask, int pass) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t row = list[i];
+    uint32_t slot, slot2, tag;
+    fp_slot_tag(d.fp[row] & keymask, mask, slot, slot2, tag);     // (tests narrow the keys: collision groups)
+    const unsigned long long key = ((unsigned long long)tag << 32) | row;
+    if (pass == 0) atomicMin(tab + slot, key);
+    else if ((uint32_t)(tab[slot] >> 32) != tag) atomicMin(tab + (mask + 1) + slot2, key);
+}
+// one wave per listed row: heads and rows unequal to their head are flagged for hashing, the others get dup_of = head
+__global__ void k_fp_verify_tab(DS d, const uint32_t *list, uint32_t n, const unsigned long long *tab, uint32_t mask,
+                                unsigned long long keymask, uint8_t *hflag, uint32_t *dup_of) {
+    const uint32_t i = wave_gid();
+    if (i >= n) return;
+    const uint32_t row = list[i];
+    uint32_t slot, slot2, tag;
+    fp_slot_tag(d.fp[row] & keymask, mask, slot, slot2, tag);
+    unsigned long long key = tab[slot];
+    if ((uint32_t)(key >> 32) != tag) key = tab[(mask + 1) + slot2];
+    const uint32_t head = (uint32_t)key;
+    bool same = false;
+    if ((uint32_t)(key >> 32) == tag && head != row) {
+        const uint32_t *ha = d.hidx ? d.hmw + (size_t)head * d.HP : nullptr, *hb = d.hidx ? d.hmw + (size_t)row * d.HP : nullptr;
+        same = !wave_rows_differ(d, d.mw + (size_t)head * d.NP, d.mw + (size_t)row * d.NP, ha, hb);
+    }
+    if (lane_id() == 0) {
+        dup_of[row] = same ? head : SRC_NONE;
+        hflag[row] = same ? 0 : 1;
+    }
+}
+// the flagged rows in row order (one workgroup: a thread per run of consecutive rows, read 16 flags at a time; a block
+// prefix sum places them); clears the flags and writes the count
+__device__ __forceinline__ uint4 flags16(const uint8_t *flag, uint32_t base, uint32_t nl) {
+    if (base + 16u <= nl) return *(const uint4 *)(flag + base);
+    uint32_t w[4] = {0, 0, 0, 0};
+    for (uint32_t k = 0; base + k < nl && k < 16u; k++) w[k >> 2] |= (uint32_t)flag[base + k] << (8u * (k & 3u));
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+__global__ void __launch_bounds__(1024) k_list_flagged_ordered(uint32_t nl, uint8_t *flag, uint32_t *list, uint32_t *cnt) {
+    __shared__ uint32_t wtot[16];
+    const uint32_t t = threadIdx.x, per = ((nl + 1023u) / 1024u + 15u) & ~15u;   // (flags are 0 or 1: a popcount each)
+    const uint32_t lo = t * per;
+    uint32_t c = 0;
+    for (uint32_t q = 0; q < per && lo + q < nl; q += 16) {
+        const uint4 v = flags16(flag, lo + q, nl);
+        c += __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
+    }
+    uint32_t wt;
+    const uint32_t ex = wscan_excl(c, wt);
+    if (lane_id() == 63) wtot[t >> 6] = wt;
+    __syncthreads();
+    uint32_t base = 0, all = 0;
+    for (uint32_t w = 0; w < 16; w++) {
+        const uint32_t v = wtot[w];
+        base += w < (t >> 6) ? v : 0u;
+        all += v;
+    }
+    uint32_t p = base + ex;
+    for (uint32_t q = 0; q < per && lo + q < nl && c; q += 16) {
+        const uint4 v = flags16(flag, lo + q, nl);
+        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+        if ((v.x | v.y | v.z | v.w) == 0) continue;
+        for (uint32_t k = 0; k < 16u; k++)
+            if ((w4[k >> 2] >> (8u * (k & 3u))) & 0xFFu) {
+                list[p++] = lo + q + k;
+                flag[lo + q + k] = 0;
+            }
+    }
+    if (t == 0) *cnt = all;
+}
+
 __global__ void k_fp_copy(DS d, const uint32_t *vals, uint32_t n, const uint32_t *dup_of) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
