@@ -93,6 +93,9 @@ typedef struct swimsim_tuning {
                                  generation of side-stream snapshot slots (phase C waits for the previous round's side
                                  launch); default 0. Results are identical with 4, 8, 16, 32, 64, 128, 256 and 1024. */
 } swimsim_tuning;
+/* Environment, read at swimsim_create (A/B experiments; results are identical either way): SWIMSIM_SYNC_SPIN=0 waits for
+ * the main stream's host round trips in the runtime's stream wait instead of polling an event; SWIMSIM_SIDE2=0 runs both
+ * generations of side-stream checksum launches on one stream. */
 
 /* Events applied in phase E of a round (docs/ROUND_SEMANTICS.md §4). */
 enum {
