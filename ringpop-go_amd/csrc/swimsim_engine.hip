@@ -1642,9 +1642,9 @@ int step_one(swimsim *h, const swimsim_event *ev, size_t nev) {
                            h->needcnt, h->xitems, h->xcnt, h->xcap);
         if (int rc = xchg(h)) return rc;
     }
-    for (uint32_t q = 0; q < h->maxjobs; q++) {
+    {
         Scope sc(h, F_JOBS_MERGE);
-        hipLaunchKernelGGL(k_jobs_merge, dim3(blocks_for_waves(h->NL)), dim3(SWIM_WAVE_BLOCK), 0, h->s, h->d, q, h->snapdesc, r);
+        hipLaunchKernelGGL(k_jobs_merge, dim3(blocks_for_waves(h->NL)), dim3(SWIM_WAVE_BLOCK), 0, h->s, h->d, h->snapdesc, r);
     }
     {
         Scope sc(h, F_JOBS);
@@ -2756,7 +2756,7 @@ int swimsim_enable_timing(swimsim_t *h, int32_t enable) {
     h->timing = enable != 0;
     // 1: every family; 2: the kernels the bench line's roofline reports (checksum chains, merges, issue): the other
     // families' event pairs cost the timed window about 10 us each (a dozen per round); 3: those and the reverse full
-    // syncs' dense merges (k_jobs_merge, maxjobs launches per round)
+    // syncs' dense merges (k_jobs_merge, one launch per round)
     const uint32_t m2 = (1u << F_CS_WIDE) | (1u << F_CS_NARROW) | (1u << F_RECV) | (1u << F_RESP) | (1u << F_ISSUE) |
                         (1u << F_CS_FALLBACK);
     h->timing_mask = enable == 2 ? m2 : enable == 3 ? m2 | (1u << F_JOBS_MERGE) : (1u << F_NFAM) - 1u;

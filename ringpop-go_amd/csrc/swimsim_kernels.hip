@@ -1843,12 +1843,17 @@ __global__ void k_jobs_snap(DS d, const uint8_t *need, MsgDesc *snapdesc) {
     if (lane_id() == 0) snapdesc[d.lo + ol] = md;
 }
 
-__global__ void k_jobs_merge(DS d, uint32_t q, const MsgDesc *snapdesc, uint32_t r) {
+// one wave per row merges its queued sources' snapshots in queue order (the sources are snapshots taken before this
+// launch and a row writes only itself, so one launch runs every queue position: round 5 launched one per position)
+__global__ void k_jobs_merge(DS d, const MsgDesc *snapdesc, uint32_t r) {
     const uint32_t ol = wave_gid();
-    if (ol >= d.NL || d.njobs[ol] <= q) return;
-    const uint32_t src = d.jobs[(size_t)ol * d.maxjobs + q];
-    wave_merge_msg(d, ol, d.lo + ol, snapdesc[src], r, r, 3, C_X_DENSE_JOBS);
-    if (lane_id() == 0) ctr_add(d, C_RFS_DONE, 1ull);
+    if (ol >= d.NL) return;
+    const uint32_t nj = d.njobs[ol];
+    for (uint32_t q = 0; q < nj; q++) {
+        const uint32_t src = d.jobs[(size_t)ol * d.maxjobs + q];
+        wave_merge_msg(d, ol, d.lo + ol, snapdesc[src], r, r, 3, C_X_DENSE_JOBS);
+    }
+    if (lane_id() == 0 && nj) ctr_add(d, C_RFS_DONE, (unsigned long long)nj);
 }
 
 __global__ void k_jobs_reset(DS d, uint8_t *need) {
